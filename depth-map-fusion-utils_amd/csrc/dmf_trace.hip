@@ -1,0 +1,674 @@
+// dmf_trace.hip — RayTracingEngine (RayTracingEngine.hpp:27-564) on gfx950.
+//
+//  * reverse visibility (reverseRayTraceFast :136-226, reverseRayTrace :45-134):
+//    one lane per (occupied voxel, pose), the reference 1 mm march toward the
+//    camera over the N-bit occupancy mask; results are per-pose ballot bitmasks in
+//    occupied_cells_ order, compacted order-preservingly into the good lists.
+//  * forward depth-plane march (rayTrace* :229-494): one lane per lattice pixel,
+//    first occupied sample per pixel; list outputs are ordered by the reference
+//    loop key (z_depth, r, c) through a per-voxel atomicMin + radix sort.
+//  * z-buffer splat rayTraceVolume (:498-564) and the willCollide segment march
+//    (tests/CameraPathGen.cpp:128-156).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "dmf_host.hpp"
+
+namespace dmf {
+
+struct EnumList {
+  const float* axes;  // xs | ys | zs (float-accumulated, RayTracingEngine.hpp:54-56)
+  int32_t nax[3];
+  const uint32_t* list;  // occupied enumeration indices (i*ny+j)*nz+k, enumeration order
+};
+
+__device__ inline void wave_add_u64(unsigned long long* dst, unsigned long long x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+  if ((threadIdx.x & 63) == 0 && x) atomicAdd(dst, x);
+}
+
+// The reverse 1 mm march (RayTracingEngine.hpp:81-103 / :172-200).  Returns true if
+// an occupied voxel other than the centroid's is hit before leaving the volume.
+// `capped` reports a march that never left (v == 0 or NaN: the reference loops
+// forever there) — treated as occluded and counted as a hazard.
+__device__ inline bool reverse_march(const Geom& g, const uint32_t* __restrict__ occ, const float cen[3],
+                                     const float v[3], int cx, int cy, int cz, int depth0, int max_steps,
+                                     int64_t& samples, bool& capped) {
+  capped = false;
+  for (int s = 0; s < max_steps; ++s) {
+    const float fd = (float)(depth0 + s);
+    const float px = cen[0] + ((v[0] * fd) / 1000.0f);
+    const float py = cen[1] + ((v[1] * fd) / 1000.0f);
+    const float pz = cen[2] + ((v[2] * fd) / 1000.0f);
+    ++samples;
+    if (!valid_points(g, px, py, pz)) return false;
+    const int a = bin_axis(g, 0, px), b = bin_axis(g, 1, py), c = bin_axis(g, 2, pz);
+    if (a == cx && b == cy && c == cz) continue;  // hash == centroid_hash
+    if (!valid_coords(g, a, b, c)) return false;
+    if (occ_test(occ, lin_index(g, a, b, c))) return true;
+  }
+  capped = true;
+  return true;
+}
+
+// kEnum = false: reverseRayTraceFast over occupied_cells_ (element = slot)
+// kEnum = true : reverseRayTrace over the float-accumulated enumeration list
+template <bool kEnum>
+__global__ __launch_bounds__(256) void k_reverse(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses,
+                                                 int64_t nelem, EnumList el, int depth0, int max_steps, float dstar,
+                                                 int viz, int normal_test, uint64_t* __restrict__ vis_mask,
+                                                 uint64_t* __restrict__ good_mask, int64_t words,
+                                                 unsigned long long* __restrict__ stats, int* __restrict__ found,
+                                                 unsigned long long* __restrict__ hazards) {
+  const int p = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool vis = false, good = false;
+  int64_t samples = 0;
+  if (e < nelem) {
+    float cen[3];
+    int64_t slot;
+    if (!kEnum) {
+      slot = e;
+      const uint64_t h = vd.hash[e];
+      const int xid = (int)(h >> 40), yid = (int)((h >> 20) & 0xFFFFF), zid = (int)(h & 0xFFFFF);
+      // :151-153 x = xid*xdelta_ + xmin_ (float); :157 centroid = x + xdelta_/2.0 (float)
+      const float x = (float)((double)xid * g.dl[0] + g.mn[0]);
+      const float y = (float)((double)yid * g.dl[1] + g.mn[1]);
+      const float z = (float)((double)zid * g.dl[2] + g.mn[2]);
+      cen[0] = (float)((double)x + g.hdl[0]);
+      cen[1] = (float)((double)y + g.hdl[1]);
+      cen[2] = (float)((double)z + g.hdl[2]);
+    } else {
+      const uint32_t en = el.list[e];
+      const uint32_t nyz = (uint32_t)el.nax[1] * (uint32_t)el.nax[2];
+      const uint32_t i = en / nyz, j = (en / el.nax[2]) % el.nax[1], k = en % el.nax[2];
+      const float x = el.axes[i], y = el.axes[el.nax[0] + j], z = el.axes[el.nax[0] + el.nax[1] + k];
+      slot = vd.slot_of[lin_index(g, bin_axis(g, 0, x), bin_axis(g, 1, y), bin_axis(g, 2, z))];
+      cen[0] = (float)((double)x + g.hdl[0]);
+      cen[1] = (float)((double)y + g.hdl[1]);
+      cen[2] = (float)((double)z + g.hdl[2]);
+    }
+    const PoseX& T = poses[p];
+    float t[3];
+    xform(T.i, cen[0], cen[1], cen[2], t);
+    int r, c;
+    if (deproject_valid(cam, t[0], t[1], t[2], r, c)) {
+      const float d[3] = {T.f[3] - cen[0], T.f[7] - cen[1], T.f[11] - cen[2]};
+      float v[3];
+      normalized(d, v);
+      bool capped;
+      const bool collided = reverse_march(g, vd.occ, cen, v, bin_axis(g, 0, cen[0]), bin_axis(g, 1, cen[1]),
+                                          bin_axis(g, 2, cen[2]), depth0, max_steps, samples, capped);
+      if (capped) atomicAdd(hazards, 1ull);
+      if (!collided) {
+        vis = true;
+        const double zz = (double)t[2];
+        if (zz >= kZMin && zz <= kZMax) {
+          if (normal_test) {
+            const int32_t a = vd.off[slot], b = vd.off[slot + 1];
+            for (int32_t j = a; j < b; ++j) {
+              const float4 n = vd.nrm[j];
+              if (n.w != 0.0f && angle_ok(n.x, n.y, n.z, v, dstar)) { good = true; break; }
+            }
+          } else {
+            good = true;
+          }
+        }
+      }
+    }
+    if (viz) {
+      if (vis) vd.view[slot] = 1;
+      if (good) vd.good[slot] = 1;
+    }
+  }
+  const uint64_t vb = __ballot(vis), gb = __ballot(good);
+  const int64_t w = e >> 6;
+  if ((threadIdx.x & 63) == 0 && w < words) {
+    if (vis_mask) vis_mask[(int64_t)p * words + w] = vb;
+    if (good_mask) good_mask[(int64_t)p * words + w] = gb;
+    if (vb) atomicOr(&found[p], 1);
+  }
+  if (stats) {
+    wave_add_u64(&stats[0], (unsigned long long)samples);
+    wave_add_u64(&stats[1], (unsigned long long)(e < nelem ? 1 : 0));
+  }
+}
+
+static int max_march_steps(const dmf_volume* v) {
+  const double dx = v->xmax - v->xmin, dy = v->ymax - v->ymin, dz = v->zmax - v->zmin;
+  const double diag_mm = std::sqrt(dx * dx + dy * dy + dz * dz) * 1000.0;
+  const double s = std::ceil(diag_mm * 1.01) + 64;
+  return s > 2e9 ? 2000000000 : (int)s;
+}
+
+// Runs k_reverse for P poses; masks land in scratch kScOut0 (vis | good).
+static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses, int P, bool poses_on_device,
+                       int viz, bool enumerate, uint64_t** d_vis, uint64_t** d_good, int64_t* words_out,
+                       int64_t* nelem_out, std::vector<int>* found_h, uint64_t* d_stats) {
+  DMF_TRY(require_constructed(v));
+  DMF_TRY(check_camera(cam));
+  if (P <= 0 || P > 65535) return fail(DMF_ERR_INVALID, "pose count %d out of range [1,65535]", P);
+  if (enumerate) DMF_TRY(ensure_enumeration(v));
+  PoseX* tab;
+  DMF_TRY(pose_table(v, poses, P, poses_on_device, &tab));
+  const int64_t nelem = enumerate ? v->nenum : v->V;
+  const int64_t words = (nelem + 63) / 64;
+  void *masks, *aux;
+  DMF_TRY(scratch(v, kScOut0, sizeof(uint64_t) * (size_t)std::max<int64_t>(2 * P * words, 1), &masks));
+  const size_t found_bytes = ((sizeof(int) * P + 7) / 8) * 8;
+  DMF_TRY(scratch(v, kScHost2, found_bytes + 2 * sizeof(unsigned long long), &aux));
+  int* found = (int*)aux;
+  unsigned long long* hz = (unsigned long long*)((char*)aux + found_bytes);
+  DMF_HIP(hipMemsetAsync(aux, 0, found_bytes + 2 * sizeof(unsigned long long), v->stream));
+  uint64_t* vis = (uint64_t*)masks;
+  uint64_t* good = vis + P * words;
+  if (nelem > 0) {
+    EnumList el{v->d_axes, {v->nax[0], v->nax[1], v->nax[2]}, v->d_enum};
+    const dim3 grid((unsigned)((nelem + 255) / 256), (unsigned)P);
+    const int depth0 = enumerate ? 1 : 50;  // :81 vs :172
+    if (enumerate)
+      hipLaunchKernelGGL(k_reverse<true>, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab,
+                         nelem, el, depth0, max_march_steps(v), v->dstar, viz, 0, vis, good, words,
+                         (unsigned long long*)d_stats, found, hz);
+    else
+      hipLaunchKernelGGL(k_reverse<false>, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab,
+                         nelem, el, depth0, max_march_steps(v), v->dstar, viz, 1, vis, good, words,
+                         (unsigned long long*)d_stats, found, hz);
+    DMF_LAUNCH_CHECK();
+  }
+  if (found_h) {
+    found_h->assign(P, 0);
+    unsigned long long hzh = 0;
+    DMF_HIP(hipMemcpyAsync(found_h->data(), found, sizeof(int) * P, hipMemcpyDeviceToHost, v->stream));
+    DMF_HIP(hipMemcpyAsync(&hzh, hz, sizeof(hzh), hipMemcpyDeviceToHost, v->stream));
+    DMF_HIP(hipStreamSynchronize(v->stream));
+    v->hazards += (int64_t)hzh;
+  }
+  *d_vis = vis;
+  *d_good = good;
+  *words_out = words;
+  *nelem_out = nelem;
+  return DMF_OK;
+}
+
+static int reverse_lists(dmf_volume* v, const dmf_camera* cam, const float* poses, int32_t P, int32_t viz,
+                         bool enumerate, uint8_t* found, int64_t* counts, uint64_t* hashes, int64_t cap) {
+  if (!poses || !counts) return fail(DMF_ERR_INVALID, "null argument");
+  uint64_t *vis, *good;
+  int64_t words, nelem;
+  std::vector<int> fh;
+  DMF_TRY(run_reverse(v, cam, poses, P, false, viz, enumerate, &vis, &good, &words, &nelem, &fh, nullptr));
+  if (found)
+    for (int p = 0; p < P; ++p) found[p] = fh[p] ? 1 : 0;
+  uint64_t* d_list;
+  int64_t total = 0;
+  DMF_TRY(compact_masks(v, good, P, words, nelem, counts, &d_list, &total,
+                        enumerate ? kValueEnumCentroidHash : kValueSlotHash));
+  if (total > cap) return fail(DMF_ERR_CAPACITY, "need %lld hashes", (long long)total);
+  if (total > 0) {
+    if (!hashes) return fail(DMF_ERR_INVALID, "null hashes");
+    DMF_HIP(hipMemcpyAsync(hashes, d_list, sizeof(uint64_t) * total, hipMemcpyDeviceToHost, v->stream));
+  }
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  return DMF_OK;
+}
+
+// ---------------------------------------------------------------- forward march
+// First occupied sample per lattice pixel (RayTracingEngine.hpp:280-308 loop body).
+__global__ __launch_bounds__(256) void k_forward(Geom g, const uint32_t* __restrict__ occ,
+                                                 const int32_t* __restrict__ slot_of, CamP cam,
+                                                 const PoseX* __restrict__ pose, int zstart, int zdelta, int rdelta,
+                                                 int cdelta, int R, int C, int32_t* __restrict__ k_out,
+                                                 int32_t* __restrict__ slot_out,
+                                                 unsigned long long* __restrict__ hazards,
+                                                 unsigned long long* __restrict__ stats) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t samples = 0;
+  if (idx < (int64_t)R * C) {
+    const int r = (int)(idx / C) * rdelta, c = (int)(idx % C) * cdelta;
+    int32_t kk = -1, sl = -1;
+    int k = 0;
+    for (int zd = zstart; (double)zd < kZMax * 1000; zd += zdelta, ++k) {
+      float pc[3], w[3];
+      project(cam, r, c, zd, pc);
+      xform(pose->f, pc[0], pc[1], pc[2], w);
+      ++samples;
+      if (!valid_points(g, w[0], w[1], w[2])) continue;
+      const int a = bin_axis(g, 0, w[0]), b = bin_axis(g, 1, w[1]), cc = bin_axis(g, 2, w[2]);
+      if (!valid_coords(g, a, b, cc)) {  // reference indexes voxels_ unguarded here (UB)
+        atomicAdd(hazards, 1ull);
+        continue;
+      }
+      const uint32_t lin = lin_index(g, a, b, cc);
+      if (occ_test(occ, lin)) {
+        kk = k;
+        sl = slot_of[lin];
+        break;
+      }
+    }
+    k_out[idx] = kk;
+    slot_out[idx] = sl;
+  }
+  if (stats) wave_add_u64(&stats[0], (unsigned long long)samples);
+}
+
+enum FwdMode { kTrace = 0, kClassify = 1, kGoodPoints = 2, kPoints = 3, kMinimum = 4 };
+
+// Side effects of the first hit per pixel (RayTracingEngine.hpp:299-305, 351-371,
+// 420-440, 480-489, 256-259).
+__global__ void k_forward_post(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ pose, int mode, int zstart,
+                               int zdelta, int rdelta, int cdelta, int R, int C, int view_arg, float dstar,
+                               const int32_t* __restrict__ k_in, const int32_t* __restrict__ slot_in,
+                               unsigned long long* __restrict__ minkey, int* __restrict__ kmin,
+                               int* __restrict__ found) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)R * C) return;
+  const int32_t kk = k_in[idx];
+  if (kk < 0) return;
+  const int32_t slot = slot_in[idx];
+  *found = 1;
+  if (mode == kMinimum) {
+    atomicMin(kmin, kk);
+    return;
+  }
+  if (mode == kTrace) {
+    vd.view[slot] = 1;
+    return;
+  }
+  const unsigned long long key = (unsigned long long)kk * (unsigned long long)((int64_t)R * C) + (unsigned long long)idx;
+  if (mode == kPoints) {
+    atomicMin(&minkey[slot], key);
+    return;
+  }
+  // classify / good points: pseudo-centroid = sample + delta/2, v toward the camera
+  const int zd = zstart + kk * zdelta;
+  const int r = (int)(idx / C) * rdelta, c = (int)(idx % C) * cdelta;
+  float pc[3], w[3];
+  project(cam, r, c, zd, pc);
+  xform(pose->f, pc[0], pc[1], pc[2], w);
+  const float cen[3] = {(float)((double)w[0] + g.hdl[0]), (float)((double)w[1] + g.hdl[1]),
+                        (float)((double)w[2] + g.hdl[2])};
+  const float d[3] = {pose->f[3] - cen[0], pose->f[7] - cen[1], pose->f[11] - cen[2]};
+  float v[3];
+  normalized(d, v);
+  bool ok = false;
+  if (zd >= 250 && zd <= 600) {
+    const int32_t a = vd.off[slot], b = vd.off[slot + 1];
+    for (int32_t j = a; j < b; ++j) {
+      const float4 n = vd.nrm[j];
+      if (n.w != 0.0f && angle_ok(n.x, n.y, n.z, v, dstar)) { ok = true; break; }
+    }
+  }
+  if (mode == kClassify) {
+    if (vd.view[slot] == 0) vd.view[slot] = view_arg;
+    if (ok) vd.good[slot] = 1;
+  } else if (ok) {
+    atomicMin(&minkey[slot], key);
+  }
+}
+
+__global__ void k_minkey_flags(const unsigned long long* __restrict__ minkey, int64_t V, uint8_t* __restrict__ flags) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < V) flags[s] = minkey[s] != ~0ull;
+}
+
+__global__ void k_minkey_pairs(const uint32_t* __restrict__ slots, const unsigned long long* __restrict__ nsel,
+                               const unsigned long long* __restrict__ minkey, const uint64_t* __restrict__ hash,
+                               uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((unsigned long long)i >= *nsel) return;
+  const uint32_t s = slots[i];
+  keys[i] = minkey[s];
+  vals[i] = hash[s];
+}
+
+struct FwdResult {
+  int found = 0;
+  int minimum = -1;
+  int64_t n = 0;
+  uint64_t* d_list = nullptr;
+};
+
+static int run_forward(dmf_volume* v, const dmf_camera* cam, const float* pose, int mode, int zstart, int zdelta,
+                       int rdelta, int cdelta, int view_arg, FwdResult* res) {
+  DMF_TRY(require_constructed(v));
+  DMF_TRY(check_camera(cam));
+  if (!pose) return fail(DMF_ERR_INVALID, "null pose");
+  if (zdelta <= 0) return fail(DMF_ERR_INVALID, "zdelta must be > 0 (the reference loops forever)");
+  if (rdelta <= 0 || cdelta <= 0) return fail(DMF_ERR_INVALID, "bad pixel stride");
+  PoseX* tab;
+  DMF_TRY(pose_table(v, pose, 1, false, &tab));
+  const int R = (cam->height + rdelta - 1) / rdelta, C = (cam->width + cdelta - 1) / cdelta;
+  const int64_t RC = (int64_t)R * C;
+  void *kb, *sb, *aux;
+  DMF_TRY(scratch(v, kScOut0, sizeof(int32_t) * RC, &kb));
+  DMF_TRY(scratch(v, kScOut1, sizeof(int32_t) * RC, &sb));
+  DMF_TRY(scratch(v, kScHost2, 64, &aux));
+  int* found = (int*)aux;
+  int* kmin = found + 1;
+  unsigned long long* hz = (unsigned long long*)((char*)aux + 16);
+  DMF_HIP(hipMemsetAsync(aux, 0, 64, v->stream));
+  DMF_HIP(hipMemsetAsync(kmin, 0x7f, sizeof(int), v->stream));
+  const CamP cp = cam_params(cam);
+  const Geom g = v->geom();
+  const dim3 grid((unsigned)((RC + 255) / 256));
+  hipLaunchKernelGGL(k_forward, grid, dim3(256), 0, v->stream, g, v->d_occ, v->d_slot_of, cp, tab, zstart, zdelta,
+                     rdelta, cdelta, R, C, (int32_t*)kb, (int32_t*)sb, hz, nullptr);
+  DMF_LAUNCH_CHECK();
+  unsigned long long* minkey = nullptr;
+  if ((mode == kPoints || mode == kGoodPoints) && v->V > 0) {
+    void* mk;
+    DMF_TRY(scratch(v, kScOut2, sizeof(unsigned long long) * v->V, &mk));
+    minkey = (unsigned long long*)mk;
+    DMF_HIP(hipMemsetAsync(minkey, 0xff, sizeof(unsigned long long) * v->V, v->stream));
+  }
+  hipLaunchKernelGGL(k_forward_post, grid, dim3(256), 0, v->stream, g, v->dev(), cp, tab, mode, zstart, zdelta,
+                     rdelta, cdelta, R, C, view_arg, v->dstar, (const int32_t*)kb, (const int32_t*)sb, minkey, kmin,
+                     found);
+  DMF_LAUNCH_CHECK();
+  int hf[2];
+  unsigned long long hzh = 0;
+  DMF_HIP(hipMemcpyAsync(hf, aux, sizeof(hf), hipMemcpyDeviceToHost, v->stream));
+  DMF_HIP(hipMemcpyAsync(&hzh, hz, sizeof(hzh), hipMemcpyDeviceToHost, v->stream));
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  v->hazards += (int64_t)hzh;
+  res->found = hf[0];
+  res->minimum = (hf[1] == 0x7f7f7f7f) ? -1 : zstart + hf[1] * zdelta;
+  res->n = 0;
+  if (minkey) {
+    // slots with a key, ordered by the reference loop key (k, r, c)
+    void *fl, *sel, *ns, *kk2;
+    DMF_TRY(scratch(v, kScOut3, v->V + 16, &fl));
+    DMF_TRY(scratch(v, kScOut0, sizeof(uint32_t) * v->V, &sel));
+    DMF_TRY(scratch(v, kScHost1, 16, &ns));
+    hipLaunchKernelGGL(k_minkey_flags, dim3((unsigned)((v->V + 255) / 256)), dim3(256), 0, v->stream, minkey, v->V,
+                       (uint8_t*)fl);
+    DMF_LAUNCH_CHECK();
+    size_t bytes = 0;
+    auto it = rocprim::counting_iterator<uint32_t>(0);
+    DMF_HIP(rocprim::select(nullptr, bytes, it, (uint8_t*)fl, (uint32_t*)sel, (unsigned long long*)ns, (size_t)v->V,
+                            v->stream));
+    void* tmp;
+    DMF_TRY(scratch(v, kScTmp, bytes, &tmp));
+    DMF_HIP(rocprim::select(tmp, bytes, it, (uint8_t*)fl, (uint32_t*)sel, (unsigned long long*)ns, (size_t)v->V,
+                            v->stream));
+    unsigned long long n = 0;
+    DMF_HIP(hipMemcpyAsync(&n, ns, sizeof(n), hipMemcpyDeviceToHost, v->stream));
+    DMF_HIP(hipStreamSynchronize(v->stream));
+    if (n > 0) {
+      DMF_TRY(scratch(v, kScOut1, sizeof(uint64_t) * n, &kk2));
+      void* vals;
+      DMF_TRY(scratch(v, kScHost0, sizeof(uint64_t) * n, &vals));
+      hipLaunchKernelGGL(k_minkey_pairs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream,
+                         (const uint32_t*)sel, (const unsigned long long*)ns, minkey, v->d_hash, (uint64_t*)kk2,
+                         (uint64_t*)vals);
+      DMF_LAUNCH_CHECK();
+      int end_bit = 1;
+      const unsigned long long maxkey = (unsigned long long)((1000 - zstart) / zdelta + 2) * (unsigned long long)RC;
+      while (end_bit < 64 && (1ull << end_bit) <= maxkey) ++end_bit;
+      DMF_TRY(sort_pairs_u64(v, (uint64_t*)kk2, (uint64_t*)vals, n, end_bit));
+      res->d_list = (uint64_t*)vals;
+      res->n = (int64_t)n;
+    }
+  }
+  return DMF_OK;
+}
+
+static int forward_list_api(dmf_volume* v, const dmf_camera* cam, const float* pose, int mode, int zdelta, int sparse,
+                            uint8_t* found, uint64_t* hashes, int64_t cap, int64_t* n) {
+  const int s = sparse ? 5 : 1;  // RayTracingEngine.hpp:387-392 / 452-457
+  FwdResult res;
+  DMF_TRY(run_forward(v, cam, pose, mode, 10, zdelta, s, s, 1, &res));
+  if (found) *found = res.found ? 1 : 0;
+  if (n) *n = res.n;
+  if (res.n > cap) return fail(DMF_ERR_CAPACITY, "need %lld hashes", (long long)res.n);
+  if (res.n > 0) {
+    if (!hashes) return fail(DMF_ERR_INVALID, "null hashes");
+    DMF_HIP(hipMemcpyAsync(hashes, res.d_list, sizeof(uint64_t) * res.n, hipMemcpyDeviceToHost, v->stream));
+    DMF_HIP(hipStreamSynchronize(v->stream));
+  }
+  return DMF_OK;
+}
+
+// ---------------------------------------------------------------- rayTraceVolume
+// z-buffer over the float-accumulated enumeration (RayTracingEngine.hpp:509-536),
+// then view marking where the voxel's depth equals the pixel minimum (:540-563).
+__global__ void k_zbuffer(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ pose, EnumList el, int64_t n,
+                          int pass, int* __restrict__ zbuf, unsigned long long* __restrict__ hazards) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint32_t en = el.list[e];
+  const uint32_t nyz = (uint32_t)el.nax[1] * (uint32_t)el.nax[2];
+  const uint32_t i = en / nyz, j = (en / el.nax[2]) % el.nax[1], k = en % el.nax[2];
+  const float x = el.axes[i], y = el.axes[el.nax[0] + j], z = el.axes[el.nax[0] + el.nax[1] + k];
+  float t[3];
+  xform(pose->i, (float)((double)x + g.hdl[0]), (float)((double)y + g.hdl[1]), (float)((double)z + g.hdl[2]), t);
+  int r, c;
+  if (!deproject_valid(cam, t[0], t[1], t[2], r, c)) return;
+  const int d = to_int_x86((double)roundf(t[2] * 1000.0f));
+  int* px = &zbuf[(int64_t)r * cam.W + c];
+  if (pass == 0) {
+    if (d == -1) atomicAdd(hazards, 1ull);  // collides with the reference's -1 "unset" marker (:529)
+    atomicMin(px, d);
+  } else if (*px == d) {
+    vd.view[vd.slot_of[lin_index(g, bin_axis(g, 0, x), bin_axis(g, 1, y), bin_axis(g, 2, z))]] = 1;
+  }
+}
+
+__global__ void k_zbuf_out(const int* __restrict__ z, int64_t n, int* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = z[i] == 0x7fffffff ? -1 : z[i];
+}
+
+// ---------------------------------------------------------------- willCollide
+// tests/CameraPathGen.cpp:128-156, one lane per segment.
+__global__ void k_will_collide(Geom g, const uint32_t* __restrict__ occ, const float* __restrict__ A,
+                               const float* __restrict__ B, int64_t n, uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float a[3] = {A[3 * i], A[3 * i + 1], A[3 * i + 2]};
+  const float b[3] = {B[3 * i], B[3 * i + 1], B[3 * i + 2]};
+  const float ab[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+  const double distance = (double)sqrtf(sum3(ab[0] * ab[0], ab[1] * ab[1], ab[2] * ab[2]));
+  const float ba[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  float v[3];
+  normalized(ba, v);
+  bool collided = false;
+  const double lim = distance * 1000;
+  for (int depth = 1; !collided; depth++) {
+    if ((double)depth > lim) break;
+    const float fd = (float)depth;
+    const float px = a[0] + ((v[0] * fd) / 1000.0f);
+    const float py = a[1] + ((v[1] * fd) / 1000.0f);
+    const float pz = a[2] + ((v[2] * fd) / 1000.0f);
+    if (!valid_points(g, px, py, pz)) continue;
+    const int x = bin_axis(g, 0, px), y = bin_axis(g, 1, py), z = bin_axis(g, 2, pz);
+    if (!valid_coords(g, x, y, z)) continue;
+    if (occ_test(occ, lin_index(g, x, y, z))) collided = true;
+  }
+  out[i] = collided ? 1 : 0;
+}
+
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" {
+
+int dmf_reverse_ray_trace_fast(dmf_volume* v, const dmf_camera* cam, const float* poses, int32_t P, int32_t viz,
+                               uint8_t* found, int64_t* counts, uint64_t* hashes, int64_t cap) {
+  DMF_API_BEGIN
+  return reverse_lists(v, cam, poses, P, viz, false, found, counts, hashes, cap);
+  DMF_API_END
+}
+
+int dmf_reverse_ray_trace(dmf_volume* v, const dmf_camera* cam, const float* poses, int32_t P, int32_t viz,
+                          uint8_t* found, int64_t* counts, uint64_t* hashes, int64_t cap) {
+  DMF_API_BEGIN
+  return reverse_lists(v, cam, poses, P, viz, true, found, counts, hashes, cap);
+  DMF_API_END
+}
+
+int dmf_reverse_visibility_device(dmf_volume* v, const dmf_camera* cam, const float* d_poses, int32_t P, int32_t viz,
+                                  uint64_t* d_visible, uint64_t* d_good, uint64_t* d_stats) {
+  DMF_API_BEGIN
+  uint64_t *vis, *good;
+  int64_t words, nelem;
+  DMF_TRY(run_reverse(v, cam, d_poses, P, true, viz, false, &vis, &good, &words, &nelem, nullptr, d_stats));
+  const size_t bytes = sizeof(uint64_t) * (size_t)P * words;
+  if (bytes) {
+    if (d_visible) DMF_HIP(hipMemcpyAsync(d_visible, vis, bytes, hipMemcpyDeviceToDevice, v->stream));
+    if (d_good) DMF_HIP(hipMemcpyAsync(d_good, good, bytes, hipMemcpyDeviceToDevice, v->stream));
+  }
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_ray_trace(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta, int32_t sparse) {
+  DMF_API_BEGIN
+  const int s = sparse ? 5 : 1;  // RayTracingEngine.hpp:274-279
+  FwdResult res;
+  return run_forward(v, cam, pose, kTrace, 10, zdelta, s, s, 1, &res);
+  DMF_API_END
+}
+
+int dmf_ray_trace_and_classify(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta, int32_t view,
+                               int32_t sparse) {
+  DMF_API_BEGIN
+  const int s = sparse ? 5 : 1;  // :321-326
+  FwdResult res;
+  return run_forward(v, cam, pose, kClassify, 10, zdelta, s, s, view, &res);
+  DMF_API_END
+}
+
+int dmf_ray_trace_and_get_minimum(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta,
+                                  int32_t sparse, int32_t* minimum) {
+  DMF_API_BEGIN
+  if (!minimum) return fail(DMF_ERR_INVALID, "null output");
+  const int s = sparse ? 10 : 1;  // :233-238
+  FwdResult res;
+  DMF_TRY(run_forward(v, cam, pose, kMinimum, 5, zdelta, s, s, 1, &res));
+  *minimum = res.minimum;
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_ray_trace_and_get_points(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta,
+                                 int32_t sparse, uint8_t* found, uint64_t* hashes, int64_t cap, int64_t* n) {
+  DMF_API_BEGIN
+  return forward_list_api(v, cam, pose, kPoints, zdelta, sparse, found, hashes, cap, n);
+  DMF_API_END
+}
+
+int dmf_ray_trace_and_get_good_points(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta,
+                                      int32_t sparse, uint8_t* found, uint64_t* hashes, int64_t cap, int64_t* n) {
+  DMF_API_BEGIN
+  return forward_list_api(v, cam, pose, kGoodPoints, zdelta, sparse, found, hashes, cap, n);
+  DMF_API_END
+}
+
+__global__ void k_first_hit_hash(const int32_t* __restrict__ slot, const uint64_t* __restrict__ hash, int64_t n,
+                                 uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = slot[i] >= 0 ? hash[slot[i]] : 0;
+}
+
+int dmf_forward_first_hits(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zstart, int32_t zdelta,
+                           int32_t rdelta, int32_t cdelta, int32_t* k_out, uint64_t* hash_out) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  DMF_TRY(check_camera(cam));
+  if (!pose || !k_out || !hash_out) return fail(DMF_ERR_INVALID, "null argument");
+  if (zdelta <= 0 || rdelta <= 0 || cdelta <= 0) return fail(DMF_ERR_INVALID, "bad strides");
+  PoseX* tab;
+  DMF_TRY(pose_table(v, pose, 1, false, &tab));
+  const int R = (cam->height + rdelta - 1) / rdelta, C = (cam->width + cdelta - 1) / cdelta;
+  const int64_t RC = (int64_t)R * C;
+  void *kb, *sb, *hb, *aux;
+  DMF_TRY(scratch(v, kScOut0, sizeof(int32_t) * RC, &kb));
+  DMF_TRY(scratch(v, kScOut1, sizeof(int32_t) * RC, &sb));
+  DMF_TRY(scratch(v, kScOut2, sizeof(uint64_t) * RC, &hb));
+  DMF_TRY(scratch(v, kScHost2, 64, &aux));
+  DMF_HIP(hipMemsetAsync(aux, 0, 64, v->stream));
+  const dim3 grid((unsigned)((RC + 255) / 256));
+  hipLaunchKernelGGL(k_forward, grid, dim3(256), 0, v->stream, v->geom(), v->d_occ, v->d_slot_of, cam_params(cam), tab,
+                     zstart, zdelta, rdelta, cdelta, R, C, (int32_t*)kb, (int32_t*)sb, (unsigned long long*)aux,
+                     nullptr);
+  DMF_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_first_hit_hash, grid, dim3(256), 0, v->stream, (const int32_t*)sb, v->d_hash, RC,
+                     (uint64_t*)hb);
+  DMF_LAUNCH_CHECK();
+  DMF_HIP(hipMemcpyAsync(k_out, kb, sizeof(int32_t) * RC, hipMemcpyDeviceToHost, v->stream));
+  DMF_HIP(hipMemcpyAsync(hash_out, hb, sizeof(uint64_t) * RC, hipMemcpyDeviceToHost, v->stream));
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_ray_trace_volume(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t* depth_out) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  DMF_TRY(check_camera(cam));
+  if (!pose) return fail(DMF_ERR_INVALID, "null pose");
+  DMF_TRY(ensure_enumeration(v));
+  PoseX* tab;
+  DMF_TRY(pose_table(v, pose, 1, false, &tab));
+  const int64_t HW = (int64_t)cam->height * cam->width;
+  void *zb, *aux;
+  DMF_TRY(scratch(v, kScOut0, sizeof(int) * HW, &zb));
+  DMF_TRY(scratch(v, kScHost2, 64, &aux));
+  DMF_HIP(hipMemsetD32Async((hipDeviceptr_t)zb, 0x7fffffff, HW, v->stream));
+  DMF_HIP(hipMemsetAsync(aux, 0, 64, v->stream));
+  EnumList el{v->d_axes, {v->nax[0], v->nax[1], v->nax[2]}, v->d_enum};
+  const int64_t n = v->nenum;
+  if (n > 0) {
+    const dim3 grid((unsigned)((n + 255) / 256));
+    for (int pass = 0; pass < 2; ++pass) {
+      hipLaunchKernelGGL(k_zbuffer, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab, el, n,
+                         pass, (int*)zb, (unsigned long long*)aux);
+      DMF_LAUNCH_CHECK();
+    }
+  }
+  unsigned long long hz = 0;
+  DMF_HIP(hipMemcpyAsync(&hz, aux, sizeof(hz), hipMemcpyDeviceToHost, v->stream));
+  if (depth_out) {
+    void* ob;
+    DMF_TRY(scratch(v, kScOut1, sizeof(int) * HW, &ob));
+    hipLaunchKernelGGL(k_zbuf_out, dim3((unsigned)((HW + 255) / 256)), dim3(256), 0, v->stream, (const int*)zb, HW,
+                       (int*)ob);
+    DMF_LAUNCH_CHECK();
+    DMF_HIP(hipMemcpyAsync(depth_out, ob, sizeof(int) * HW, hipMemcpyDeviceToHost, v->stream));
+  }
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  v->hazards += (int64_t)hz + v->enum_hazards;
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_will_collide(dmf_volume* v, const float* a, const float* b, int64_t n, uint8_t* collided) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  if (n < 0 || (n > 0 && (!a || !b || !collided))) return fail(DMF_ERR_INVALID, "bad arguments");
+  if (n == 0) return DMF_OK;
+  for (int64_t i = 0; i < 3 * n; ++i)
+    if (!std::isfinite(a[i]) || !std::isfinite(b[i]))
+      return fail(DMF_ERR_INVALID, "non-finite segment endpoint (the reference never terminates)");
+  void *da, *db, *dout;
+  DMF_TRY(scratch(v, kScHost0, sizeof(float) * 3 * n, &da));
+  DMF_TRY(scratch(v, kScHost1, sizeof(float) * 3 * n, &db));
+  DMF_TRY(scratch(v, kScOut0, n, &dout));
+  DMF_HIP(hipMemcpyAsync(da, a, sizeof(float) * 3 * n, hipMemcpyHostToDevice, v->stream));
+  DMF_HIP(hipMemcpyAsync(db, b, sizeof(float) * 3 * n, hipMemcpyHostToDevice, v->stream));
+  hipLaunchKernelGGL(k_will_collide, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream, v->geom(), v->d_occ,
+                     (const float*)da, (const float*)db, n, (uint8_t*)dout);
+  DMF_LAUNCH_CHECK();
+  DMF_HIP(hipMemcpyAsync(collided, dout, n, hipMemcpyDeviceToHost, v->stream));
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  return DMF_OK;
+  DMF_API_END
+}
+
+}  // extern "C"

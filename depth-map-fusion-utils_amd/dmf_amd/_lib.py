@@ -1,0 +1,169 @@
+"""ctypes binding of libdmf.so (include/dmf.h).
+
+The shared library is the product: there is no Python or CPU fallback.  If the
+library is missing or no gfx950 GPU is visible, every compute call raises.
+
+Import order: when PyTorch is used in the same process, import torch BEFORE
+loading this library so both share torch's HIP runtime (same soname
+libamdhip64.so.7); see INTEGRATION.md.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("DMF_LIB", os.path.join(PKG_ROOT, "build", "libdmf.so"))
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+HEADER_PATH = os.path.join(REPO_ROOT, "include", "dmf.h")
+
+DMF_OK = 0
+DMF_ERR_INVALID = 1
+DMF_ERR_STATE = 2
+DMF_ERR_HIP = 3
+DMF_ERR_NOMEM = 4
+DMF_ERR_CAPACITY = 5
+DMF_ERR_RANGE = 6
+DMF_ERR_NO_DEVICE = 7
+
+
+class DmfError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"dmf status {status}: {msg}")
+        self.status = status
+
+
+class dmf_camera(C.Structure):
+    _fields_ = [("K", C.c_float * 9), ("height", C.c_int32), ("width", C.c_int32)]
+
+
+class dmf_volume_info(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("xmin", "xmax", "ymin", "ymax", "zmin", "zmax", "xcenter", "ycenter",
+                                          "zcenter", "xdelta", "ydelta", "zdelta", "voxel_size")] + [
+        ("xdim", C.c_int32), ("ydim", C.c_int32), ("zdim", C.c_int32), ("constructed", C.c_int32),
+        ("hsize", C.c_uint64), ("num_occupied", C.c_int64), ("num_points", C.c_int64), ("hazards", C.c_int64)]
+
+
+class dmf_fuse_params(C.Structure):
+    _fields_ = [("dmin_mm", C.c_int32), ("dmax_mm", C.c_int32), ("l_hit", C.c_int32), ("l_miss", C.c_int32),
+                ("l_min", C.c_int32), ("l_max", C.c_int32)]
+
+
+_vp = C.c_void_p
+_p = C.c_void_p  # raw pointers are passed as integers (numpy .ctypes.data or device addresses)
+_i32 = C.c_int32
+_i64 = C.c_int64
+
+SIGNATURES = {
+    "dmf_abi_version": (C.c_int, []),
+    "dmf_status_string": (C.c_char_p, [C.c_int]),
+    "dmf_last_error": (C.c_char_p, []),
+    "dmf_device_count": (C.c_int, [_p]),
+    "dmf_fuse_params_default": (None, [_p]),
+    "dmf_volume_create": (C.c_int, [_p, _i32]),
+    "dmf_volume_destroy": (C.c_int, [_vp]),
+    "dmf_volume_set_stream": (C.c_int, [_vp, _vp]),
+    "dmf_volume_synchronize": (C.c_int, [_vp]),
+    "dmf_volume_set_dimensions": (C.c_int, [_vp] + [C.c_double] * 6),
+    "dmf_volume_set_resolution": (C.c_int, [_vp] + [C.c_double] * 3),
+    "dmf_volume_set_volume_size": (C.c_int, [_vp, _i32, _i32, _i32]),
+    "dmf_volume_construct": (C.c_int, [_vp]),
+    "dmf_volume_get_info": (C.c_int, [_vp, _p]),
+    "dmf_volume_integrate": (C.c_int, [_vp, _p, _p, _i64, _p, _p]),
+    "dmf_volume_integrate_device": (C.c_int, [_vp, _p, _p, _i64]),
+    "dmf_volume_occupied": (C.c_int, [_vp, _p, _i64, _p]),
+    "dmf_volume_voxel_flags": (C.c_int, [_vp, _p, _p, _i64]),
+    "dmf_volume_reset_flags": (C.c_int, [_vp]),
+    "dmf_volume_voxel_counts": (C.c_int, [_vp, _p, _p, _i64]),
+    "dmf_volume_voxel_points": (C.c_int, [_vp, C.c_uint64, _p, _p, _i64, _p]),
+    "dmf_volume_occupancy": (C.c_int, [_vp, _p]),
+    "dmf_backproject": (C.c_int, [_vp, _p, _p, _p, _p]),
+    "dmf_backproject_device": (C.c_int, [_vp, _p, _p, _p, _i32, _p]),
+    "dmf_reverse_ray_trace_fast": (C.c_int, [_vp, _p, _p, _i32, _i32, _p, _p, _p, _i64]),
+    "dmf_reverse_visibility_device": (C.c_int, [_vp, _p, _p, _i32, _i32, _p, _p, _p]),
+    "dmf_reverse_ray_trace": (C.c_int, [_vp, _p, _p, _i32, _i32, _p, _p, _p, _i64]),
+    "dmf_ray_trace": (C.c_int, [_vp, _p, _p, _i32, _i32]),
+    "dmf_ray_trace_and_classify": (C.c_int, [_vp, _p, _p, _i32, _i32, _i32]),
+    "dmf_ray_trace_and_get_minimum": (C.c_int, [_vp, _p, _p, _i32, _i32, _p]),
+    "dmf_ray_trace_and_get_points": (C.c_int, [_vp, _p, _p, _i32, _i32, _p, _p, _i64, _p]),
+    "dmf_ray_trace_and_get_good_points": (C.c_int, [_vp, _p, _p, _i32, _i32, _p, _p, _i64, _p]),
+    "dmf_forward_first_hits": (C.c_int, [_vp, _p, _p, _i32, _i32, _i32, _i32, _p, _p]),
+    "dmf_ray_trace_volume": (C.c_int, [_vp, _p, _p, _p]),
+    "dmf_will_collide": (C.c_int, [_vp, _p, _p, _i64, _p]),
+    "dmf_fuse_depth": (C.c_int, [_vp, _p, _p, _p, _i32, _p, _p, _p, _p]),
+    "dmf_fuse_depth_device": (C.c_int, [_vp, _p, _p, _p, _i32, _p, _p, _p, _p]),
+    "dmf_fuse_finalize": (C.c_int, [_vp, _p, _p, _p, _p]),
+    "dmf_fuse_finalize_device": (C.c_int, [_vp, _p, _p, _p, _p]),
+    "dmf_device_malloc": (C.c_int, [_vp, _p, C.c_size_t]),
+    "dmf_device_free": (C.c_int, [_vp, _vp]),
+    "dmf_memcpy_h2d": (C.c_int, [_vp, _vp, _p, C.c_size_t]),
+    "dmf_memcpy_d2h": (C.c_int, [_vp, _p, _vp, C.c_size_t]),
+    "dmf_memset_device": (C.c_int, [_vp, _vp, C.c_int, C.c_size_t]),
+}
+
+_lib = None
+
+
+def load(path=None):
+    """Load libdmf.so (raises if it has not been built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise ImportError(f"libdmf.so not found at {path}; run `make -C depth-map-fusion-utils_amd` "
+                          "(or __graft_entry__.build()).  There is no CPU fallback.")
+    L = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status):
+    if status != DMF_OK:
+        L = load()
+        raise DmfError(status, f"{L.dmf_status_string(status).decode()}: {L.dmf_last_error().decode()}")
+    return status
+
+
+def ptr(a):
+    """Raw address of a numpy array (or None)."""
+    if a is None:
+        return None
+    return a.ctypes.data
+
+
+def device_count():
+    n = C.c_int32(0)
+    check(load().dmf_device_count(C.addressof(n)))
+    return n.value
+
+
+def declared_symbols():
+    """Function names declared in include/dmf.h (parsed from the header text)."""
+    import re
+    txt = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"\b(dmf_[a-z0-9_]+)\s*\(", txt)))
+
+
+def make_camera(K, height=480, width=640):
+    cam = dmf_camera()
+    Kf = np.asarray(K, np.float32).reshape(9)
+    for i in range(9):
+        cam.K[i] = float(Kf[i])
+    cam.height = int(height)
+    cam.width = int(width)
+    return cam
+
+
+def default_fuse_params(**kw):
+    p = dmf_fuse_params()
+    load().dmf_fuse_params_default(C.addressof(p))
+    for k, v in kw.items():
+        setattr(p, k, int(v))
+    return p

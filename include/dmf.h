@@ -1,0 +1,201 @@
+/*
+ * dmf.h — C ABI of the MI355X-native voxel ray-tracing / depth-fusion engine.
+ *
+ * The reference (REXJJ/depth-map-fusion-utils) has no FFI layer: its boundary is the
+ * header-only C++ class API of include/Camera.hpp, include/Volume.hpp and
+ * include/RayTracingEngine.hpp.  Every entry point below names the
+ * reference member it replaces (file:line in the reference tree).  The C++ drop-in
+ * classes in depth-map-fusion-utils_amd/compat/ and the Python mirror in dmf_amd/
+ * are thin layers over this ABI; see INTEGRATION.md for the bindings.
+ *
+ * Conventions
+ *  - All calls return an int status (DMF_OK == 0); nothing throws across the ABI.
+ *    dmf_last_error() returns a thread-local message for the last failure.
+ *  - A dmf_volume is one device-resident VoxelVolume plus its HIP stream; use one
+ *    handle per host thread (the reference hot path is single-threaded).
+ *  - Poses are float[12], row-major 3x4 [R|t] (rows 0..2 of Eigen::Affine3f), camera
+ *    -> world, exactly the `transformation` argument of the reference.
+ *  - Voxel ids are the reference hash (x<<40) ^ (y<<20) ^ z (Volume.hpp:143-148).
+ *    "slot" = position of a voxel in occupied_cells_ (first-touch order).
+ *  - Functions without a _device suffix take HOST pointers and synchronise the
+ *    stream before returning; *_device functions take DEVICE pointers, only enqueue
+ *    work on the volume's stream and never synchronise.
+ *  - The engine needs a gfx950 GPU.  There is no CPU fallback: with no usable
+ *    device every compute call fails with DMF_ERR_NO_DEVICE.
+ */
+#ifndef DMF_H_
+#define DMF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DMF_ABI_VERSION 1
+
+enum dmf_status {
+  DMF_OK = 0,
+  DMF_ERR_INVALID = 1,   /* bad argument (null pointer, bad size, bad pose count ...) */
+  DMF_ERR_STATE = 2,     /* volume not constructed / wrong call order              */
+  DMF_ERR_HIP = 3,       /* HIP runtime error (message in dmf_last_error)          */
+  DMF_ERR_NOMEM = 4,     /* device or host allocation failed                       */
+  DMF_ERR_CAPACITY = 5,  /* output buffer too small: required size returned        */
+  DMF_ERR_RANGE = 6,     /* grid too large for a packed field (hash / fixed point) */
+  DMF_ERR_NO_DEVICE = 7  /* no usable GPU                                          */
+};
+
+typedef struct dmf_volume dmf_volume;
+
+/* Camera(vector<float>& K, int height=480, int width=640)  Camera.hpp:23
+ * K row-major 3x3: fx=K[0], cx=K[2], fy=K[4], cy=K[5]  (Camera.hpp:26). */
+typedef struct dmf_camera {
+  float K[9];
+  int32_t height;
+  int32_t width;
+} dmf_camera;
+
+/* VoxelVolume public fields (Volume.hpp:54-60) + engine bookkeeping. */
+typedef struct dmf_volume_info {
+  double xmin, xmax, ymin, ymax, zmin, zmax;
+  double xcenter, ycenter, zcenter;
+  double xdelta, ydelta, zdelta;
+  double voxel_size;
+  int32_t xdim, ydim, zdim;
+  int32_t constructed;
+  uint64_t hsize;
+  int64_t num_occupied;  /* occupied_cells_.size() */
+  int64_t num_points;    /* points binned so far   */
+  int64_t hazards;       /* unguarded out-of-range accesses the reference would make */
+} dmf_volume_info;
+
+/* 3D-DDA log-odds fusion parameters (not in the reference). */
+typedef struct dmf_fuse_params {
+  int32_t dmin_mm;  /* depth accepted iff dmin_mm <= d < dmax_mm */
+  int32_t dmax_mm;
+  int32_t l_hit;    /* milli-logit per hit   (OctoMap default p=0.7  ->  847) */
+  int32_t l_miss;   /* milli-logit per miss  (OctoMap default p=0.4  -> -405) */
+  int32_t l_min;    /* clamp                 (p=0.1192 -> -2000)              */
+  int32_t l_max;    /*                       (p=0.971  ->  3511)              */
+} dmf_fuse_params;
+
+/* ---- library ------------------------------------------------------------ */
+int dmf_abi_version(void);
+const char* dmf_status_string(int status);
+const char* dmf_last_error(void);
+int dmf_device_count(int32_t* count);
+void dmf_fuse_params_default(dmf_fuse_params* p);
+
+/* ---- VoxelVolume  (Volume.hpp:50-255) ------------------------------------ */
+/* VoxelVolume::VoxelVolume()  Volume.hpp:63 — device = HIP device ordinal. */
+int dmf_volume_create(dmf_volume** out, int32_t device);
+/* VoxelVolume::~VoxelVolume()  Volume.hpp:80-87 */
+int dmf_volume_destroy(dmf_volume* v);
+/* All work of this handle is enqueued on `stream` (hipStream_t; NULL = default). */
+int dmf_volume_set_stream(dmf_volume* v, void* hip_stream);
+int dmf_volume_synchronize(dmf_volume* v);
+/* setDimensions  Volume.hpp:89-100 */
+int dmf_volume_set_dimensions(dmf_volume* v, double xmin, double xmax, double ymin, double ymax,
+                              double zmin, double zmax);
+/* setResolution  Volume.hpp:102-107 */
+int dmf_volume_set_resolution(dmf_volume* v, double xdelta, double ydelta, double zdelta);
+/* setVolumeSize  Volume.hpp:109-117 */
+int dmf_volume_set_volume_size(dmf_volume* v, int32_t xdim, int32_t ydim, int32_t zdim);
+/* constructVolume  Volume.hpp:119-128 (dims recomputed by truncation, as the reference) */
+int dmf_volume_construct(dmf_volume* v);
+int dmf_volume_get_info(const dmf_volume* v, dmf_volume_info* out);
+
+/* integratePointCloud(cloud [, normals])  Volume.hpp:172-197 / :199-228.
+ * xyz: n*3 floats (PointXYZRGB x,y,z); normals: n*3 floats or NULL.  Points
+ * outside the grid are skipped (the no-normals reference overload indexes out of
+ * range there — counted in *n_hazard). */
+int dmf_volume_integrate(dmf_volume* v, const float* xyz, const float* normals, int64_t n,
+                         int64_t* n_binned, int64_t* n_hazard);
+int dmf_volume_integrate_device(dmf_volume* v, const float* d_xyz, const float* d_normals, int64_t n);
+
+/* occupied_cells_ (Volume.hpp:54) in insertion order. */
+int dmf_volume_occupied(const dmf_volume* v, uint64_t* hashes, int64_t cap, int64_t* n);
+/* Voxel::view / Voxel::good (Volume.hpp:29-48) per slot. */
+int dmf_volume_voxel_flags(const dmf_volume* v, int32_t* view, uint8_t* good, int64_t cap);
+int dmf_volume_reset_flags(dmf_volume* v);
+/* Voxel::pts.size() / normals.size() per slot. */
+int dmf_volume_voxel_counts(const dmf_volume* v, int64_t* npts, int64_t* nnormals, int64_t cap);
+/* Voxel::pts / Voxel::normals of one voxel (insertion order); *n = #points, -1 if empty. */
+int dmf_volume_voxel_points(const dmf_volume* v, uint64_t hash, float* pts, float* normals, int64_t cap,
+                            int64_t* n);
+/* voxels_[x][y][z] != nullptr as a dense x-major byte grid (xdim*ydim*zdim). */
+int dmf_volume_occupancy(const dmf_volume* v, uint8_t* dense);
+
+/* ---- Camera back-projection  (Camera.hpp:24-31 projectPoint + :39-45 transformPoints) */
+/* depth: H*W uint16 mm, pose: 12 floats -> xyz: H*W*3 floats (world). */
+int dmf_backproject(dmf_volume* v, const dmf_camera* cam, const uint16_t* depth, const float* pose,
+                    float* xyz);
+int dmf_backproject_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth,
+                           const float* d_poses, int32_t P, float* d_xyz);
+
+/* ---- RayTracingEngine  (RayTracingEngine.hpp:27-564) ---------------------- */
+/* reverseRayTraceFast  RayTracingEngine.hpp:136-226, batched over P poses.
+ * found[P]; counts[P]; hashes = the P good lists concatenated in pose order, each in
+ * occupied_cells_ order.  DMF_ERR_CAPACITY (counts filled) if sum(counts) > cap. */
+int dmf_reverse_ray_trace_fast(dmf_volume* v, const dmf_camera* cam, const float* poses, int32_t P,
+                               int32_t viz, uint8_t* found, int64_t* counts, uint64_t* hashes,
+                               int64_t cap);
+/* Device form: per-pose bitmasks over slots, words = ceil(num_occupied/64) per pose,
+ * d_visible / d_good: P*words uint64 (either may be NULL).  d_poses: P*12 floats. */
+int dmf_reverse_visibility_device(dmf_volume* v, const dmf_camera* cam, const float* d_poses, int32_t P,
+                                  int32_t viz, uint64_t* d_visible, uint64_t* d_good,
+                                  uint64_t* d_stats /* [0]+= march samples, [1]+= rays; may be NULL */);
+/* reverseRayTrace  RayTracingEngine.hpp:45-134 (float-accumulated grid enumeration). */
+int dmf_reverse_ray_trace(dmf_volume* v, const dmf_camera* cam, const float* poses, int32_t P, int32_t viz,
+                          uint8_t* found, int64_t* counts, uint64_t* hashes, int64_t cap);
+/* rayTrace  RayTracingEngine.hpp:268-309 */
+int dmf_ray_trace(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta, int32_t sparse);
+/* rayTraceAndClassify  RayTracingEngine.hpp:311-375 */
+int dmf_ray_trace_and_classify(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta,
+                               int32_t view, int32_t sparse);
+/* rayTraceAndGetMinimum  RayTracingEngine.hpp:229-264 (-1 if nothing hit) */
+int dmf_ray_trace_and_get_minimum(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta,
+                                  int32_t sparse, int32_t* minimum);
+/* rayTraceAndGetPoints  RayTracingEngine.hpp:447-494 */
+int dmf_ray_trace_and_get_points(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta,
+                                 int32_t sparse, uint8_t* found, uint64_t* hashes, int64_t cap, int64_t* n);
+/* rayTraceAndGetGoodPoints  RayTracingEngine.hpp:377-445 */
+int dmf_ray_trace_and_get_good_points(dmf_volume* v, const dmf_camera* cam, const float* pose,
+                                      int32_t zdelta, int32_t sparse, uint8_t* found, uint64_t* hashes,
+                                      int64_t cap, int64_t* n);
+/* Per-pixel first hit of the forward march on the (rdelta, cdelta) lattice:
+ * k_out[R*C] depth-plane index (-1 = none), hash_out[R*C]. */
+int dmf_forward_first_hits(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zstart,
+                           int32_t zdelta, int32_t rdelta, int32_t cdelta, int32_t* k_out,
+                           uint64_t* hash_out);
+/* rayTraceVolume  RayTracingEngine.hpp:498-564 (depth_out: H*W int32 z-buffer or NULL). */
+int dmf_ray_trace_volume(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t* depth_out);
+/* willCollide  tests/CameraPathGen.cpp:128-156, for n segment pairs a[i] -> b[i]. */
+int dmf_will_collide(dmf_volume* v, const float* a, const float* b, int64_t n, uint8_t* collided);
+
+/* ---- 3D-DDA log-odds fusion (new capability) ------------------ */
+/* depth: P*H*W uint16 mm, poses: P*12.  hits/misses: xdim*ydim*zdim int32 counters,
+ * ACCUMULATED (caller zeroes).  stats[3] += {cell updates, rays, hits}. */
+int dmf_fuse_depth(dmf_volume* v, const dmf_camera* cam, const uint16_t* depth, const float* poses,
+                   int32_t P, const dmf_fuse_params* prm, int32_t* hits, int32_t* misses, int64_t* stats);
+int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth,
+                          const float* d_poses, int32_t P, const dmf_fuse_params* prm, int32_t* d_hits,
+                          int32_t* d_misses, uint64_t* d_stats);
+/* clamp(hits*l_hit + misses*l_miss, l_min, l_max) -> int16 log-odds grid. */
+int dmf_fuse_finalize(dmf_volume* v, const int32_t* hits, const int32_t* misses, const dmf_fuse_params* prm,
+                      int16_t* logodds);
+int dmf_fuse_finalize_device(dmf_volume* v, const int32_t* d_hits, const int32_t* d_misses,
+                             const dmf_fuse_params* prm, int16_t* d_logodds);
+
+/* ---- device memory helpers for callers without their own allocator ---------- */
+int dmf_device_malloc(dmf_volume* v, void** d_ptr, size_t bytes);
+int dmf_device_free(dmf_volume* v, void* d_ptr);
+int dmf_memcpy_h2d(dmf_volume* v, void* d_dst, const void* h_src, size_t bytes);
+int dmf_memcpy_d2h(dmf_volume* v, void* h_dst, const void* d_src, size_t bytes);
+int dmf_memset_device(dmf_volume* v, void* d_ptr, int value, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DMF_H_ */

@@ -1,0 +1,243 @@
+"""GPU parity: every hot-path entry point through the C ABI vs the CPU oracle.
+
+Bit-exact for every integer/index output (occupied_cells_ order, flags, lists,
+first hits, z-buffer, counters) and for the back-projected float coordinates
+(north_star tolerance is 1e-5; the fp64 + no-FMA restatement is exact, so the
+test demands equality of the float32 bit patterns).
+"""
+import numpy as np
+import pytest
+
+import helpers as Hh
+from helpers import H, K, W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dmf():
+    import dmf_amd
+    return dmf_amd
+
+
+@pytest.fixture(scope="module")
+def cam(dmf):
+    return dmf.Camera(K, H, W)
+
+
+@pytest.fixture(scope="module")
+def engine(dmf, cam):
+    return dmf.RayTracingEngine(cam)
+
+
+@pytest.fixture(scope="module")
+def oeng(oracle):
+    return oracle.Engine(K, H, W)
+
+
+def test_backproject_bitexact(oracle, engine):
+    poses, depth, _ = Hh.frames()
+    vol = Hh.gpu_volume(clouds=[])
+    for i in range(3):
+        g = engine.backproject(vol, depth[i], poses[i])
+        o = oracle.backproject(K, depth[i], poses[i])
+        assert np.array_equal(g.view(np.uint32), o.view(np.uint32))
+        assert np.max(np.abs(g - o)) <= 1e-5
+
+
+def test_backproject_non_orthonormal(oracle, engine):
+    _, depth, _ = Hh.frames()
+    T = Hh.ref_style_poses()[0]
+    vol = Hh.gpu_volume(clouds=[])
+    g = engine.backproject(vol, depth[0], T)
+    o = oracle.backproject(K, depth[0], T)
+    assert np.array_equal(g.view(np.uint32), o.view(np.uint32))
+
+
+@pytest.mark.parametrize("with_normals", [True, False])
+def test_integrate_parity(oracle, with_normals):
+    pts, nn = Hh.cloud()
+    half = pts.shape[0] // 2
+    clouds = [(pts[:half], nn[:half]), (pts[half:], nn[half:])]
+    ov = Hh.oracle_volume(oracle, with_normals=with_normals, clouds=clouds)
+    gv = Hh.gpu_volume(with_normals=with_normals, clouds=clouds)
+    assert np.array_equal(ov.occupied_cells_, gv.occupied_cells_)
+    assert np.array_equal(ov.occupancy_dense(), gv.occupancy_dense())
+    _, _, onp, onn = ov.voxel_table()
+    gnp, gnn = gv.voxel_counts()
+    assert np.array_equal(onp, gnp) and np.array_equal(onn, gnn)
+    occ = ov.occupied_cells_
+    for h in occ[:: max(1, len(occ) // 50)]:
+        x, y, z = int(h) >> 40, (int(h) >> 20) & 0xFFFFF, int(h) & 0xFFFFF
+        op, on = ov.voxel_points(x, y, z)
+        gp, gn = gv.voxel_points(h)
+        assert np.array_equal(op, gp)
+        if with_normals:
+            assert np.array_equal(on, gn)
+    assert gv.info()["num_points"] == int(onp.sum())
+
+
+def test_integrate_points_outside_and_empty(oracle, dmf):
+    gv = Hh.gpu_volume(clouds=[])
+    gv.integratePointCloud(np.zeros((0, 3), np.float32))
+    assert len(gv.occupied_cells_) == 0
+    pts = np.array([[0.6, 0, 0], [-0.5, 0, 0], [0.1, 0.1, 0.1], [0.1, 0.1, 0.1001], [0.49999, 0, 0]], np.float32)
+    nn = np.tile(np.array([[0, 0, 1]], np.float32), (5, 1))
+    ov = Hh.oracle_volume(oracle, clouds=[(pts, nn)])
+    gv.integratePointCloud(pts, nn)
+    assert np.array_equal(ov.occupied_cells_, gv.occupied_cells_)
+
+
+def _flags(v_or, v_gpu):
+    ov, og, _, _ = v_or.voxel_table()
+    gview, ggood = v_gpu.voxel_flags()
+    return ov, og, gview, ggood
+
+
+def test_reverse_fast_parity(oracle, engine, oeng):
+    ov = Hh.oracle_volume(oracle)
+    gv = Hh.gpu_volume()
+    poses = Hh.all_poses()
+    found, lists = engine.reverseRayTraceFastBatch(gv, poses, viz=False)
+    for i, T in enumerate(poses):
+        f, g = oeng.reverseRayTraceFast(ov, T, False)
+        assert f == bool(found[i])
+        assert np.array_equal(g, lists[i]), f"pose {i}: {len(g)} vs {len(lists[i])}"
+    # viz=True flags, single-pose reference signature
+    ov.reset_flags()
+    gv.reset_flags()
+    for T in poses[:4]:
+        f, g = oeng.reverseRayTraceFast(ov, T, True)
+        f2, g2 = engine.reverseRayTraceFast(gv, T, True)
+        assert f == f2 and np.array_equal(g, g2)
+    a, b, c, d = _flags(ov, gv)
+    assert np.array_equal(a, c) and np.array_equal(b, d)
+    assert sum(len(x) for x in lists) > 0
+
+
+def test_reverse_full_parity(oracle, engine, oeng):
+    ov = Hh.oracle_volume(oracle, n=64)
+    gv = Hh.gpu_volume(n=64)
+    for T in Hh.all_poses()[:6]:
+        f, g = oeng.reverseRayTrace(ov, T, True)
+        f2, g2 = engine.reverseRayTrace(gv, T, True)
+        assert f == f2 and np.array_equal(g, g2)
+    a, b, c, d = _flags(ov, gv)
+    assert np.array_equal(a, c) and np.array_equal(b, d)
+
+
+@pytest.mark.parametrize("zstart,zdelta,stride", [(10, 10, 5), (5, 1, 10), (10, 3, 1)])
+def test_forward_first_hits(oracle, engine, oeng, zstart, zdelta, stride):
+    ov = Hh.oracle_volume(oracle)
+    gv = Hh.gpu_volume()
+    for T in Hh.all_poses()[:5]:
+        ko, ho = oeng.forward_first_hits(ov, T, zstart, zdelta, stride, stride)
+        kg, hg = engine.forward_first_hits(gv, T, zstart, zdelta, stride, stride)
+        assert np.array_equal(ko, kg)
+        assert np.array_equal(ho[ko >= 0], hg[kg >= 0])
+
+
+@pytest.mark.parametrize("sparse", [True, False])
+def test_forward_family(oracle, engine, oeng, sparse):
+    ov = Hh.oracle_volume(oracle)
+    gv = Hh.gpu_volume()
+    for T in Hh.all_poses()[:4]:
+        assert oeng.rayTraceAndGetMinimum(ov, T, 1, sparse) == engine.rayTraceAndGetMinimum(gv, T, 1, sparse)
+        f, g = oeng.rayTraceAndGetPoints(ov, T, 10, sparse)
+        f2, g2 = engine.rayTraceAndGetPoints(gv, T, 10, sparse)
+        assert f == f2 and np.array_equal(g, g2)
+        f, g = oeng.rayTraceAndGetGoodPoints(ov, T, 10, sparse)
+        f2, g2 = engine.rayTraceAndGetGoodPoints(gv, T, 10, sparse)
+        assert f == f2 and np.array_equal(g, g2)
+    ov.reset_flags()
+    gv.reset_flags()
+    for i, T in enumerate(Hh.all_poses()[:4]):
+        oeng.rayTraceAndClassify(ov, T, 10, i + 2, sparse)
+        engine.rayTraceAndClassify(gv, T, 10, i + 2, sparse)
+    a, b, c, d = _flags(ov, gv)
+    assert np.array_equal(a, c) and np.array_equal(b, d)
+    ov.reset_flags()
+    gv.reset_flags()
+    for T in Hh.all_poses()[4:8]:
+        oeng.rayTrace(ov, T, 10, sparse)
+        engine.rayTrace(gv, T, 10, sparse)
+    a, b, c, d = _flags(ov, gv)
+    assert np.array_equal(a, c) and np.array_equal(b, d)
+
+
+def test_ray_trace_volume(oracle, engine, oeng):
+    ov = Hh.oracle_volume(oracle, n=64)
+    gv = Hh.gpu_volume(n=64)
+    for T in Hh.all_poses()[:4]:
+        assert np.array_equal(oeng.rayTraceVolume(ov, T), engine.rayTraceVolume(gv, T))
+    a, b, c, d = _flags(ov, gv)
+    assert np.array_equal(a, c)
+
+
+def test_will_collide(oracle, dmf):
+    ov = Hh.oracle_volume(oracle)
+    gv = Hh.gpu_volume()
+    P = Hh.all_poses().reshape(-1, 3, 4)[:, :, 3]
+    a = np.repeat(P, len(P), axis=0)
+    b = np.tile(P, (len(P), 1))
+    g = dmf.will_collide(gv, a, b)
+    o = np.array([oracle.will_collide(ov, a[i], b[i]) for i in range(len(a))])
+    assert np.array_equal(g, o)
+    assert g.any() and not g.all()
+
+
+def test_fuse_parity(oracle, engine):
+    poses, depth, _ = Hh.frames()
+    ov = Hh.oracle_volume(oracle, clouds=[])
+    gv = Hh.gpu_volume(clouds=[])
+    ho, mo, so = oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
+    import dmf_amd
+    prm = dmf_amd.FuseParams(dmin_mm=200, dmax_mm=1000)
+    hg, mg, sg = engine.fuse_depth(gv, depth, poses, prm)
+    assert np.array_equal(so, sg)
+    assert np.array_equal(ho, hg) and np.array_equal(mo, mg)
+    assert np.array_equal(oracle.fuse_finalize(ho, mo), engine.fuse_finalize(gv, hg, mg))
+
+
+def test_fuse_non_orthonormal_and_inside_cameras(oracle, engine):
+    _, depth, _ = Hh.frames()
+    poses = Hh.ref_style_poses()[:3]  # cameras 0.3 m from the surface: inside the grid
+    ov = Hh.oracle_volume(oracle, n=100, clouds=[])  # non power-of-two delta path
+    gv = Hh.gpu_volume(n=100, clouds=[])
+    ho, mo, so = oracle.fuse_depth(ov, K, depth[:3], poses)
+    hg, mg, sg = engine.fuse_depth(gv, depth[:3], poses)
+    assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
+
+
+def test_truncated_dims_and_odd_bounds(oracle, engine, oeng):
+    # float bounds from a cloud's min/max: constructVolume may truncate dims (Volume.hpp:121-123)
+    pts, nn = Hh.cloud()
+    lo, hi = pts.min(0), pts.max(0)
+    bounds = (float(lo[0]), float(hi[0]), float(lo[1]), float(hi[1]), float(lo[2]), float(hi[2]))
+    n = [int((hi[i] - lo[i]) * 125) for i in range(3)]
+    ov = oracle.Volume()
+    ov.setDimensions(*bounds)
+    ov.setVolumeSize(*n)
+    ov.constructVolume()
+    ov.integratePointCloud(pts, nn)
+    import dmf_amd
+    gv = dmf_amd.VoxelVolume()
+    gv.setDimensions(*bounds)
+    gv.setVolumeSize(*n)
+    gv.constructVolume()
+    gv.integratePointCloud(pts, nn)
+    assert ov.dims == gv.dims
+    assert np.array_equal(ov.occupied_cells_, gv.occupied_cells_)
+    for T in Hh.all_poses()[:3]:
+        f, g = oeng.reverseRayTraceFast(ov, T, False)
+        f2, g2 = engine.reverseRayTraceFast(gv, T, False)
+        assert f == f2 and np.array_equal(g, g2)
+
+
+def test_errors_are_loud(dmf, engine):
+    gv = Hh.gpu_volume(clouds=[])
+    with pytest.raises(dmf.DmfError):
+        engine.rayTraceAndGetMinimum(gv, Hh.frames()[0][0], 0, True)  # zdelta 0: reference never ends
+    v = dmf.VoxelVolume()
+    with pytest.raises(dmf.DmfError):
+        v.integratePointCloud(np.zeros((4, 3), np.float32))  # not constructed
