@@ -118,7 +118,7 @@ def main():
     d_poses = torch.from_numpy(np.ascontiguousarray(poses, np.float32)).to(dev)
     counters = torch.zeros(2 * ncell, dtype=torch.int32, device=dev)  # [hits | misses]: one all-reduce
     logodds = torch.empty(ncell, dtype=torch.int16, device=dev)
-    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    stats = torch.zeros(8, dtype=torch.int64, device=dev)
     import ctypes as C
     pcam, pprm = C.addressof(cam), C.addressof(prm)
     hits_p = counters.data_ptr()
@@ -212,6 +212,9 @@ def main():
                        "grid": grid, "image": f"{WIDTH}x{HEIGHT}", "poses_per_gpu": P, "global_poses": P * world,
                        "parallelism": f"pose-sharded dp{world} + RCCL all-reduce(sum) of counters"},
             "mrays_per_s": rays / elapsed / 1e6,
+            "fuse_diagnostics": {"lds_rounds": int(st[4]), "fallback_rounds": int(st[5]),
+                                 "flushed_cell_atomics": int(st[6]),
+                                 "updates_per_flushed_atomic": float(st[0]) / max(float(st[6]), 1.0)},
             "updates_per_ray": updates / max(rays, 1.0),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -93,6 +93,30 @@ int pose_table(dmf_volume* v, const float* poses, int P, bool on_device, PoseX**
   return DMF_OK;
 }
 
+// ---------------------------------------------------------------- striped stats
+int stats_begin(dmf_volume* v, unsigned long long** striped) {
+  void* b;
+  DMF_TRY(scratch(v, kScStats, sizeof(unsigned long long) * kStatSlots * kStatWidth, &b));
+  DMF_HIP(hipMemsetAsync(b, 0, sizeof(unsigned long long) * kStatSlots * kStatWidth, v->stream));
+  *striped = (unsigned long long*)b;
+  return DMF_OK;
+}
+
+__global__ void k_stats_reduce(const unsigned long long* __restrict__ s, int n, unsigned long long* __restrict__ out) {
+  const int c = threadIdx.x;
+  if (c >= n) return;
+  unsigned long long t = 0;
+  for (int k = 0; k < kStatSlots; ++k) t += s[k * kStatWidth + c];
+  out[c] += t;
+}
+
+int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int n) {
+  if (!d_user) return DMF_OK;
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(64), 0, v->stream, striped, n, (unsigned long long*)d_user);
+  DMF_LAUNCH_CHECK();
+  return DMF_OK;
+}
+
 // ---------------------------------------------------------------- rocPRIM glue
 int exclusive_scan_i64(dmf_volume* v, const int64_t* in, int64_t* out, size_t n) {
   size_t bytes = 0;

@@ -49,8 +49,18 @@ int require_constructed(const dmf_volume* v);
 int scratch(dmf_volume* v, int k, size_t bytes, void** out);
 enum ScratchSlot {
   kScPoses = 0, kScHost0, kScHost1, kScHost2, kScOut0, kScOut1, kScOut2, kScOut3, kScTmp, kScSort0,
-  kScSort1, kScSort2, kScSort3, kScCount
+  kScSort1, kScSort2, kScSort3, kScCount, kScStats
 };
+
+// Striped statistics: kernels add into slot (block % kStatSlots) of a zeroed buffer
+// of kStatSlots x kStatWidth counters (one hot address per counter serialises at the
+// memory side); stats_end() sums the slots into the caller's counters.
+constexpr int kStatSlots = 256, kStatWidth = 8;
+int stats_begin(dmf_volume* v, unsigned long long** striped);
+int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int ncounters);
+__device__ inline unsigned long long* stat_slot(unsigned long long* base) {
+  return base ? base + kStatWidth * ((blockIdx.x + blockIdx.y * gridDim.x) & (kStatSlots - 1)) : nullptr;
+}
 
 // Upload P host poses (or take device poses) and build the PoseX table on device.
 int pose_table(dmf_volume* v, const float* poses, int P, bool poses_on_device, PoseX** d_table);

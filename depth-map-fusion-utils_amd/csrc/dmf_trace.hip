@@ -63,6 +63,7 @@ __global__ __launch_bounds__(256) void k_reverse(Geom g, DevVol vd, CamP cam, co
                                                  uint64_t* __restrict__ good_mask, int64_t words,
                                                  unsigned long long* __restrict__ stats, int* __restrict__ found,
                                                  unsigned long long* __restrict__ hazards) {
+  stats = stat_slot(stats);
   const int p = blockIdx.y;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool vis = false, good = false;
@@ -165,20 +166,21 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
   DMF_HIP(hipMemsetAsync(aux, 0, found_bytes + 2 * sizeof(unsigned long long), v->stream));
   uint64_t* vis = (uint64_t*)masks;
   uint64_t* good = vis + P * words;
+  unsigned long long* st = nullptr;
+  if (d_stats) DMF_TRY(stats_begin(v, &st));
   if (nelem > 0) {
     EnumList el{v->d_axes, {v->nax[0], v->nax[1], v->nax[2]}, v->d_enum};
     const dim3 grid((unsigned)((nelem + 255) / 256), (unsigned)P);
     const int depth0 = enumerate ? 1 : 50;  // :81 vs :172
     if (enumerate)
       hipLaunchKernelGGL(k_reverse<true>, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab,
-                         nelem, el, depth0, max_march_steps(v), v->dstar, viz, 0, vis, good, words,
-                         (unsigned long long*)d_stats, found, hz);
+                         nelem, el, depth0, max_march_steps(v), v->dstar, viz, 0, vis, good, words, st, found, hz);
     else
       hipLaunchKernelGGL(k_reverse<false>, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab,
-                         nelem, el, depth0, max_march_steps(v), v->dstar, viz, 1, vis, good, words,
-                         (unsigned long long*)d_stats, found, hz);
+                         nelem, el, depth0, max_march_steps(v), v->dstar, viz, 1, vis, good, words, st, found, hz);
     DMF_LAUNCH_CHECK();
   }
+  if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 2));
   if (found_h) {
     found_h->assign(P, 0);
     unsigned long long hzh = 0;
@@ -225,6 +227,7 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, const uint32_t* __restr
                                                  int32_t* __restrict__ slot_out,
                                                  unsigned long long* __restrict__ hazards,
                                                  unsigned long long* __restrict__ stats) {
+  stats = stat_slot(stats);
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t samples = 0;
   if (idx < (int64_t)R * C) {

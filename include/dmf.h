@@ -145,7 +145,7 @@ int dmf_reverse_ray_trace_fast(dmf_volume* v, const dmf_camera* cam, const float
  * d_visible / d_good: P*words uint64 (either may be NULL).  d_poses: P*12 floats. */
 int dmf_reverse_visibility_device(dmf_volume* v, const dmf_camera* cam, const float* d_poses, int32_t P,
                                   int32_t viz, uint64_t* d_visible, uint64_t* d_good,
-                                  uint64_t* d_stats /* [0]+= march samples, [1]+= rays; may be NULL */);
+                                          uint64_t* d_stats /* 2 counters += {march samples, voxel rays}; may be NULL */);
 /* reverseRayTrace  RayTracingEngine.hpp:45-134 (float-accumulated grid enumeration). */
 int dmf_reverse_ray_trace(dmf_volume* v, const dmf_camera* cam, const float* poses, int32_t P, int32_t viz,
                           uint8_t* found, int64_t* counts, uint64_t* hashes, int64_t cap);
@@ -176,7 +176,9 @@ int dmf_will_collide(dmf_volume* v, const float* a, const float* b, int64_t n, u
 
 /* ---- 3D-DDA log-odds fusion (new capability) ------------------ */
 /* depth: P*H*W uint16 mm, poses: P*12.  hits/misses: xdim*ydim*zdim int32 counters,
- * ACCUMULATED (caller zeroes).  stats[3] += {cell updates, rays, hits}. */
+ * ACCUMULATED (caller zeroes).  stats[3] += {cell updates, rays, hits}.
+ * d_stats (device form, may be NULL): 8 uint64 counters += {cell updates, rays, hits, 0,
+ * LDS aggregation rounds, direct-atomic rounds, flushed cell atomics, 0}. */
 int dmf_fuse_depth(dmf_volume* v, const dmf_camera* cam, const uint16_t* depth, const float* poses,
                    int32_t P, const dmf_fuse_params* prm, int32_t* hits, int32_t* misses, int64_t* stats);
 int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth,

@@ -241,3 +241,17 @@ def test_errors_are_loud(dmf, engine):
     v = dmf.VoxelVolume()
     with pytest.raises(dmf.DmfError):
         v.integratePointCloud(np.zeros((4, 3), np.float32))  # not constructed
+
+
+def test_fuse_kernel_repeatable(oracle, engine):
+    """Counts are exact integers: every repetition must reproduce the oracle exactly
+    (guards the LDS aggregation rounds against races)."""
+    _, depth, _ = Hh.frames()
+    poses = np.concatenate([Hh.ref_style_poses()[:2], Hh.frames()[0][:2]])
+    frames = np.concatenate([depth[:2], depth[2:4]])
+    ov = Hh.oracle_volume(oracle, n=96, clouds=[])
+    ho, mo, so = oracle.fuse_depth(ov, K, frames, poses)
+    gv = Hh.gpu_volume(n=96, clouds=[])
+    for _ in range(5):
+        hg, mg, sg = engine.fuse_depth(gv, frames, poses)
+        assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
