@@ -30,6 +30,7 @@ sys.path[:0] = [ROOT, PKG]
 
 import dmf_amd  # noqa: E402
 from dmf_amd import _lib, scene  # noqa: E402
+from dmf_amd import dist as D  # noqa: E402
 
 GRID = 512
 WIDTH, HEIGHT = 640, 480
@@ -46,7 +47,8 @@ def log(*a):
 def make_inputs(rank, world, P_local, cache_dir="/tmp/dmf_bench_cache"):
     """Rank's shard of a Fibonacci pose sphere (P_local*world poses) + rendered depth."""
     P_total = P_local * world
-    poses = scene.fibonacci_poses(P_total, seed=1234)[rank * P_local:(rank + 1) * P_local]
+    a, b = D.shard_range(P_total, world, rank)
+    poses = scene.fibonacci_poses(P_total, seed=1234)[a:b]
     os.makedirs(cache_dir, exist_ok=True)
     key = os.path.join(cache_dir, f"depth_{WIDTH}x{HEIGHT}_P{P_total}_r{rank}_of{world}.npy")
     if os.path.exists(key):
@@ -137,8 +139,7 @@ def main():
         if record:
             e1.record(stream)
             ev.append((e0, e1))
-        if world > 1:
-            dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+        D.merge_counters(counters)  # RCCL all-reduce(sum) of [hits | misses] when world > 1
         _lib.check(L.dmf_fuse_finalize_device(vol._h, hits_p, miss_p, pprm, logodds.data_ptr()))
 
     for _ in range(args.warmup):
@@ -159,13 +160,8 @@ def main():
     fuse_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if st[3] != 0:
         raise RuntimeError(f"DDA guard tripped {st[3]} times")
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    tot = torch.tensor(st[:3].astype(np.float64), device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    elapsed = float(t.item())
-    updates, rays, hits = (float(x) for x in tot.cpu().numpy())
+    elapsed = D.max_over_ranks(elapsed, device=dev)
+    updates, rays, hits = D.sum_over_ranks(st[:3], device=dev)
 
     # per-launch algorithmic bytes of the dominant kernel (k_fuse), this rank
     upd_launch = float(st[0]) / args.steps

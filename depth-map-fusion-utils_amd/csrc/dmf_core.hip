@@ -649,6 +649,12 @@ void dmf_fuse_params_default(dmf_fuse_params* p) {
   p->l_max = 3511;
 }
 
+int dmf_angle_threshold(float* dstar) {
+  if (!dstar) return fail(DMF_ERR_INVALID, "null output");
+  *dstar = angle_threshold();
+  return DMF_OK;
+}
+
 int dmf_volume_create(dmf_volume** out, int32_t device) {
   DMF_API_BEGIN
   if (!out) return fail(DMF_ERR_INVALID, "null out");
@@ -882,6 +888,22 @@ int dmf_volume_voxel_points(const dmf_volume* v, uint64_t hash, float* pts, floa
       if (tmp[i].w != 0.0f) { nrm[3 * k] = tmp[i].x; nrm[3 * k + 1] = tmp[i].y; nrm[3 * k + 2] = tmp[i].z; ++k; }
     for (; k < cnt; ++k) nrm[3 * k] = nrm[3 * k + 1] = nrm[3 * k + 2] = 0.0f;
   }
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_volume_export(const dmf_volume* v, int32_t* offsets, float* pts, float* normals4, int64_t cap) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  if (cap < v->nbinned && (pts || normals4)) return fail(DMF_ERR_CAPACITY, "need %lld points", (long long)v->nbinned);
+  if (offsets) DMF_HIP(hipMemcpyAsync(offsets, v->d_off, sizeof(int32_t) * (v->V + 1), hipMemcpyDeviceToHost, v->stream));
+  if (v->nbinned > 0) {
+    if (pts)
+      DMF_HIP(hipMemcpyAsync(pts, v->d_csr_pts, sizeof(float) * 3 * v->nbinned, hipMemcpyDeviceToHost, v->stream));
+    if (normals4)
+      DMF_HIP(hipMemcpyAsync(normals4, v->d_csr_nrm, sizeof(float4) * v->nbinned, hipMemcpyDeviceToHost, v->stream));
+  }
+  DMF_HIP(hipStreamSynchronize(v->stream));
   return DMF_OK;
   DMF_API_END
 }

@@ -62,6 +62,7 @@ SIGNATURES = {
     "dmf_last_error": (C.c_char_p, []),
     "dmf_device_count": (C.c_int, [_p]),
     "dmf_fuse_params_default": (None, [_p]),
+    "dmf_angle_threshold": (C.c_int, [_p]),
     "dmf_volume_create": (C.c_int, [_p, _i32]),
     "dmf_volume_destroy": (C.c_int, [_vp]),
     "dmf_volume_set_stream": (C.c_int, [_vp, _vp]),
@@ -79,6 +80,7 @@ SIGNATURES = {
     "dmf_volume_voxel_counts": (C.c_int, [_vp, _p, _p, _i64]),
     "dmf_volume_voxel_points": (C.c_int, [_vp, C.c_uint64, _p, _p, _i64, _p]),
     "dmf_volume_occupancy": (C.c_int, [_vp, _p]),
+    "dmf_volume_export": (C.c_int, [_vp, _p, _p, _p, _i64]),
     "dmf_backproject": (C.c_int, [_vp, _p, _p, _p, _p]),
     "dmf_backproject_device": (C.c_int, [_vp, _p, _p, _p, _i32, _p]),
     "dmf_reverse_ray_trace_fast": (C.c_int, [_vp, _p, _p, _i32, _i32, _p, _p, _p, _i64]),

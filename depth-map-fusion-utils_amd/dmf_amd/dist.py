@@ -1,0 +1,43 @@
+"""Multi-GPU pose sharding: poses are independent given the grid, so
+P poses go to G ranks in contiguous blocks of ceil(P/G); every rank fuses its block
+into its own replica of the int32 [hits | misses] counters and ONE all-reduce(SUM)
+merges them (RCCL over xGMI with backend "nccl"; gloo on CPU).  Counts are exact
+integers, so the merge is associative and bit-identical to a single-rank fusion.
+The clamped int16 log-odds are finalized after the merge on every rank.
+"""
+from __future__ import annotations
+
+
+def shard_range(P_total: int, world: int, rank: int):
+    """[start, stop) of rank's contiguous pose block (ceil(P/G) per rank)."""
+    per = -(-P_total // world)
+    start = min(rank * per, P_total)
+    return start, min(start + per, P_total)
+
+
+def merge_counters(counters, group=None):
+    """All-reduce(SUM) of the packed [hits | misses] int32 counters, in place."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
+    return counters
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """Max of a per-rank scalar (the bench's step time)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(values, device=None):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(x) for x in t.cpu().tolist()]

@@ -86,6 +86,11 @@ const char* dmf_status_string(int status);
 const char* dmf_last_error(void);
 int dmf_device_count(int32_t* count);
 void dmf_fuse_params_default(dmf_fuse_params* p);
+/* The normal test degree(acos(n.v)) in [0,90] (CommonUtilities.hpp:17,
+ * RayTracingEngine.hpp:207-219) is evaluated on the GPU as dstar <= n.v <= 1, with
+ * dstar the smallest float whose host-libm acosf passes (the function the reference
+ * binary calls).  Host-only; no GPU needed. */
+int dmf_angle_threshold(float* dstar);
 
 /* ---- VoxelVolume  (Volume.hpp:50-255) ------------------------------------ */
 /* VoxelVolume::VoxelVolume()  Volume.hpp:63 — device = HIP device ordinal. */
@@ -124,6 +129,12 @@ int dmf_volume_voxel_counts(const dmf_volume* v, int64_t* npts, int64_t* nnormal
 /* Voxel::pts / Voxel::normals of one voxel (insertion order); *n = #points, -1 if empty. */
 int dmf_volume_voxel_points(const dmf_volume* v, uint64_t hash, float* pts, float* normals, int64_t cap,
                             int64_t* n);
+/* Bulk export of every voxel's points/normals (host mirror of voxels_[x][y][z]->pts /
+ * ->normals): offsets[V+1] (points of slot s are [offsets[s], offsets[s+1])), pts
+ * 3 floats per point, normals4 4 floats per point (w = 1 if the point carried a
+ * normal), in occupied_cells_ order and insertion order within a voxel.  cap_points
+ * must be >= num_points (dmf_volume_get_info); any output may be NULL. */
+int dmf_volume_export(const dmf_volume* v, int32_t* offsets, float* pts, float* normals4, int64_t cap_points);
 /* voxels_[x][y][z] != nullptr as a dense x-major byte grid (xdim*ydim*zdim). */
 int dmf_volume_occupancy(const dmf_volume* v, uint8_t* dense);
 

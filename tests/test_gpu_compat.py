@@ -1,0 +1,64 @@
+"""The C++ drop-in headers (compat/Camera.hpp, Volume.hpp, RayTracingEngine.hpp) drive
+the GPU exactly like the reference's own driver tests/Raytracing.cpp does; every
+number the headless driver prints must equal the oracle run of the same sequence."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import helpers as Hh
+from dmf_amd import scene
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "depth-map-fusion-utils_amd", "build", "raytracing_headless")
+
+
+def _run(tmp_path, pts, nrm, poses):
+    cloud = np.concatenate([pts, nrm], axis=1).astype(np.float32)
+    cloud.tofile(tmp_path / "cloud.bin")
+    scene.write_pose_file(tmp_path / "poses.txt", poses)
+    out = subprocess.run([DRIVER, str(tmp_path / "cloud.bin"), str(tmp_path / "poses.txt")], check=True,
+                         capture_output=True, text=True, timeout=600).stdout
+    res = {"sizes": []}
+    for line in out.splitlines():
+        f = line.split()
+        if f[0] == "dims":
+            res["dims"] = tuple(int(x) for x in f[1:4])
+        elif f[0] == "occupied":
+            res["occupied"] = int(f[1])
+        elif f[0] == "found":
+            res["found"], res["good"], res["view_flags"], res["good_flags"] = int(f[1]), int(f[3]), int(f[5]), int(f[7])
+        elif f[0] == "goodlist":
+            res["goodlist"] = np.array([int(x) for x in f[1:]], np.uint64)
+        elif f[0] == "Sizes:":
+            res["sizes"].append(int(f[1]))
+    return res
+
+
+def test_raytracing_driver_matches_oracle(tmp_path, oracle):
+    assert os.path.exists(DRIVER), "build the driver: make -C depth-map-fusion-utils_amd"
+    pts, nrm = Hh.cloud()
+    poses = np.concatenate([Hh.ref_style_poses()[:3], Hh.frames()[0][:3]])
+    got = _run(tmp_path, pts, nrm, poses)
+    # the same sequence on the oracle (tests/Raytracing.cpp:62-92)
+    lo, hi = pts.min(0), pts.max(0)
+    ov = oracle.Volume()
+    ov.setDimensions(float(lo[0]), float(hi[0]), float(lo[1]), float(hi[1]), float(lo[2]), float(hi[2]))
+    ext = [int(np.float32(hi[i] - lo[i]) * np.float32(125)) for i in range(3)]
+    ov.setVolumeSize(*ext)
+    ov.constructVolume()
+    ov.integratePointCloud(pts, nrm)
+    assert got["dims"] == ov.dims
+    assert got["occupied"] == len(ov.occupied_cells_)
+    eng = oracle.Engine(Hh.K)
+    found, good = eng.reverseRayTraceFast(ov, poses[0], True)
+    view, goodf, _, _ = ov.voxel_table()
+    assert got["found"] == int(found)
+    assert np.array_equal(got["goodlist"], good)
+    assert got["view_flags"] == int((view == 1).sum()) and got["good_flags"] == int(goodf.sum())
+    sizes = [len(eng.reverseRayTraceFast(ov, T, False)[1]) for T in poses]
+    assert got["sizes"] == sizes
+    assert sum(sizes) > 0

@@ -255,3 +255,57 @@ def test_fuse_kernel_repeatable(oracle, engine):
     for _ in range(5):
         hg, mg, sg = engine.fuse_depth(gv, frames, poses)
         assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
+
+
+def test_golden_fixture_gpu(dmf):
+    """GPU results against the committed golden vectors (tests/golden/gen_golden.py)."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_v1.npz"))
+    K, poses, depth = z["K"], z["poses"], z["depth"]
+    W, H = int(z["W"]), int(z["H"])
+    cam = dmf.Camera(K, H, W)
+    eng = dmf.RayTracingEngine(cam)
+    pts, nn = [], []
+    vol0 = dmf.VoxelVolume()
+    vol0.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    vol0.setVolumeSize(8, 8, 8)
+    vol0.constructVolume()
+    for i in (0, 1):
+        xyz = eng.backproject(vol0, depth[i], poses[i])
+        if i == 0:
+            assert np.array_equal(xyz.reshape(-1, 3)[z["bp_index"]].view(np.uint32), z["bp_xyz"].view(np.uint32))
+        m = depth[i] > 0
+        pts.append(xyz[m])
+        nn.append(z["normals16"][i][m].astype(np.float32))
+    pts, nn = np.concatenate(pts), np.concatenate(nn)
+    allp = z["all_poses"]
+    for n in (64, 96):
+        v = dmf.VoxelVolume()
+        v.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+        v.setVolumeSize(n, n, n)
+        v.constructVolume()
+        v.integratePointCloud(pts, nn)
+        assert np.array_equal(v.occupied_cells_, z[f"occ{n}"])
+        assert np.array_equal(v.voxel_counts()[0], z[f"npts{n}"])
+        found, lists = eng.reverseRayTraceFastBatch(v, allp, viz=False)
+        assert np.array_equal(found.astype(np.uint8), z[f"rrtf{n}_found"])
+        assert np.array_equal(np.array([len(x) for x in lists]), z[f"rrtf{n}_counts"])
+        assert np.array_equal(np.concatenate(lists), z[f"rrtf{n}_hashes"])
+        k, h = eng.forward_first_hits(v, allp[0], 10, 10, 5, 5)
+        assert np.array_equal(k, z[f"fwd{n}_k"]) and np.array_equal(h[k >= 0], z[f"fwd{n}_h"][k >= 0])
+        assert np.array_equal(np.array([eng.rayTraceAndGetMinimum(v, T) for T in allp], np.int32), z[f"min{n}"])
+        assert np.array_equal(eng.rayTraceAndGetPoints(v, allp[1])[1], z[f"gp{n}"])
+        v.reset_flags()
+        assert np.array_equal(eng.rayTraceVolume(v, allp[2]), z[f"zbuf{n}"])
+        assert np.array_equal(v.voxel_flags()[0], z[f"zbuf{n}_view"])
+        f = dmf.VoxelVolume()
+        f.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+        f.setVolumeSize(n, n, n)
+        f.constructVolume()
+        hits, misses, st = eng.fuse_depth(f, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
+        assert np.array_equal(st, z[f"fuse{n}_stats"])
+        for name, arr in (("hits", hits), ("misses", misses)):
+            nz = np.nonzero(arr)[0]
+            assert np.array_equal(nz, z[f"fuse{n}_{name}_idx"]) and np.array_equal(arr[nz], z[f"fuse{n}_{name}_val"])
+        L = eng.fuse_finalize(f, hits, misses)
+        assert int(L.astype(np.int64).sum()) == int(z[f"fuse{n}_logodds_sum"][0])

@@ -1,0 +1,225 @@
+"""CPU: the oracle against the committed golden vectors, against an independent
+pure-Python restatement (oracle/py_oracle.py), and structural properties of the
+DDA fusion spec.  No GPU."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from oracle import py_oracle as PY
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "golden_v1.npz")
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(GOLD)  # allow_pickle=False (default): our own fixture, data only
+
+
+@pytest.fixture(scope="module")
+def gold_cloud(gold, oracle):
+    import sys
+    sys.path.insert(0, os.path.dirname(GOLD))
+    import gen_golden as G
+    K, poses, depth = gold["K"], gold["poses"], gold["depth"]
+    nrm16 = np.zeros((len(poses),) + gold["normals16"].shape[1:], np.float16)
+    nrm16[:2] = gold["normals16"]
+    return G, K, poses, depth, nrm16
+
+
+def test_golden_regression(gold, gold_cloud, oracle):
+    G, K, poses, depth, nrm16 = gold_cloud
+    out = G.compute(K, poses, depth, nrm16)
+    for k, v in out.items():
+        assert np.array_equal(np.asarray(v), gold[k]), k
+
+
+def test_golden_fixture_nontrivial(gold):
+    assert len(gold["occ64"]) > 1000 and gold["rrtf64_counts"].sum() > 1000
+    assert gold["fuse64_stats"][0] > 1e6 and (gold["min64"] > 0).all()
+    assert (gold["fwd64_k"] >= 0).any() and (gold["zbuf64"] >= 0).any()
+
+
+def _rand_poses(n, seed):
+    from dmf_amd import scene
+    rng = np.random.default_rng(seed)
+    P = scene.fibonacci_poses(n, seed=seed)
+    pts = rng.uniform(-0.3, 0.3, (n, 3)).astype(np.float32)
+    nn = rng.normal(size=(n, 3)).astype(np.float32)
+    nn /= np.linalg.norm(nn, axis=1, keepdims=True)
+    return np.concatenate([P, scene.reference_style_poses(pts, nn)])
+
+
+def test_camera_math_py_vs_cpp(oracle):
+    rng = np.random.default_rng(1)
+    from dmf_amd import scene
+    K = scene.K_640x480
+    for T in _rand_poses(8, 3):
+        for _ in range(50):
+            r, c, d = int(rng.integers(0, 480)), int(rng.integers(0, 640)), int(rng.integers(1, 3000))
+            p = PY.project_point(K, r, c, d)
+            assert np.array_equal(np.array(p, np.float32), oracle.project_point(K, r, c, d))
+            w = PY.transform(T, p)
+            assert np.array_equal(np.array(w, np.float32), oracle.transform_point(T, *[float(x) for x in p]))
+        assert np.array_equal(PY.inverse(T), oracle.inverse_pose(T))
+        for _ in range(50):
+            x, y, z = rng.uniform(-1, 1), rng.uniform(-1, 1), rng.uniform(-0.2, 1.5)
+            assert PY.deproject(K, x, y, z) == oracle.deproject_point(K, x, y, z)
+
+
+def test_degree_and_angle(oracle):
+    for rad in (0.0, 1.0, 1.5707963, 1.5882, 1.58824, 3.14159, 1e12, float("nan")):
+        v = (rad * 180) / 3.14159
+        exp = int(v) if np.isfinite(v) and -2**31 <= v < 2**31 else -2**31
+        assert oracle.degree(rad) == exp
+
+
+def test_angle_threshold_exhaustive(oracle):
+    """libdmf evaluates degree(acosf(d)) in [0,90] as dstar <= d <= 1 on the GPU: check
+    every float of the transition window and the edges against glibc acosf."""
+    from dmf_amd import _lib
+    f = C.c_float()
+    _lib.check(_lib.load().dmf_angle_threshold(C.addressof(f)))
+    dstar = np.float32(f.value)
+    lo, hi = np.float32(-0.0180), np.float32(-0.0170)
+    a, b = lo.view(np.uint32), hi.view(np.uint32)  # negative: a > b
+    ds = np.arange(b, a + 1, dtype=np.uint32).view(np.float32)
+    L = oracle.lib()
+    v = np.array([1, 0, 0], np.float32)
+    n = np.zeros(3, np.float32)
+    bad = 0
+    for d in ds:
+        n[0] = d
+        bad += bool(L.orc_angle_ok(n, v)) != bool(dstar <= d <= np.float32(1.0))
+    assert bad == 0
+    for d in (np.float32(1.0), np.nextafter(np.float32(1.0), np.float32(2)), np.float32(-1.0), np.float32(0.0),
+              np.float32(-0.5), np.float32(0.99999)):
+        n[0] = d
+        assert bool(L.orc_angle_ok(n, v)) == bool(dstar <= d <= np.float32(1.0)), d
+
+
+def test_integrate_and_reverse_py_vs_cpp(oracle, gold):
+    K, poses, depth = gold["K"], gold["poses"], gold["depth"]
+    W, H = int(gold["W"]), int(gold["H"])
+    xyz = oracle.backproject(K, depth[0], poses[0])
+    m = depth[0] > 0
+    nrm = gold["normals16"][0][m].astype(np.float32)
+    pts = xyz[m][::7]
+    nrm = nrm[::7]
+    bounds = (-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    for n in (24, 30):
+        pv = PY.Vol(bounds, (n, n, n))
+        pv.integrate(pts, nrm)
+        ov = oracle.Volume()
+        ov.setDimensions(*bounds)
+        ov.setVolumeSize(n, n, n)
+        ov.constructVolume()
+        ov.integratePointCloud(pts, nrm)
+        assert np.array_equal(np.array(pv.occupied(), np.uint64), ov.occupied_cells_)
+        eng = oracle.Engine(K, H, W)
+        for T in gold["all_poses"][:6]:
+            f1, g1 = PY.reverse_ray_trace_fast(pv, K, H, W, T)
+            f2, g2 = eng.reverseRayTraceFast(ov, T, False)
+            assert f1 == f2 and np.array_equal(np.array(g1, np.uint64), g2)
+
+
+def _fuse_py(K, H, W, depth, poses, bounds, n, dmin, dmax):
+    v = PY.Vol(bounds, (n, n, n))
+    hits = np.zeros(n ** 3, np.int32)
+    misses = np.zeros(n ** 3, np.int32)
+    lin = lambda c: (c[0] * n + c[1]) * n + c[2]
+    upd = 0
+    for p in range(len(poses)):
+        T = poses[p]
+        O = (np.float32(T[3]), np.float32(T[7]), np.float32(T[11]))
+        for r in range(H):
+            for c in range(W):
+                d = int(depth[p, r, c])
+                if not (dmin <= d < dmax):
+                    continue
+                E = PY.transform(T, PY.project_point(K, r, c, d))
+                inside = v.valid_points(E) and v.valid_coords(v.get_voxel(E))
+                missed, hit = PY.dda_cells(v, O, E, inside)
+                for cell in missed:
+                    misses[lin(cell)] += 1
+                if hit is not None:
+                    hits[lin(hit)] += 1
+                upd += len(missed) + (hit is not None)
+    return hits, misses, upd
+
+
+def test_dda_fusion_py_vs_cpp(oracle):
+    """Exact-rational DDA (py_oracle, Fractions) vs the integer-scaled DDA (oracle.cpp)."""
+    from dmf_amd import scene
+    K = scene.K_640x480.copy()
+    K[[0, 2, 4, 5]] *= np.float32(0.0625)  # 40x30 image
+    W, H = 40, 30
+    poses = _rand_poses(3, 11)
+    depth = scene.render_frames(K, W, H, poses, dmin=1, dmax=65535)
+    bounds = (-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    for n in (16, 23):
+        hp, mp, up = _fuse_py(K, H, W, depth, poses, bounds, n, 1, 65535)
+        ov = oracle.Volume()
+        ov.setDimensions(*bounds)
+        ov.setVolumeSize(n, n, n)
+        ov.constructVolume()
+        ho, mo, so = oracle.fuse_depth(ov, K, depth, poses, dmin=1, dmax=65535)
+        assert so[0] == up
+        assert np.array_equal(hp, ho) and np.array_equal(mp, mo)
+
+
+def test_dda_path_properties(oracle):
+    """Every ray's cell path is 6-connected, ends at the endpoint cell (getVoxel of the
+    back-projected point), and hits equal the binned endpoints (integratePointCloud)."""
+    from dmf_amd import scene
+    rng = np.random.default_rng(5)
+    v = PY.Vol((-0.5, 0.5, -0.5, 0.5, -0.5, 0.5), (37, 37, 37))
+    for _ in range(300):
+        O = rng.uniform(-0.9, 0.9, 3).astype(np.float32)
+        E = rng.uniform(-0.6, 0.6, 3).astype(np.float32)
+        inside = v.valid_points(E) and v.valid_coords(v.get_voxel(E))
+        missed, hit = PY.dda_cells(v, O, E, inside)
+        path = missed + ([hit] if hit is not None else [])
+        for a, b in zip(path, path[1:]):
+            assert sum(abs(a[i] - b[i]) for i in range(3)) == 1
+        assert all(v.valid_coords(c) for c in path)
+        if inside:
+            assert hit == v.get_voxel(E)
+    # hits of a fused frame == occupancy of the binned back-projected cloud
+    K = scene.K_640x480.copy()
+    K[[0, 2, 4, 5]] *= np.float32(0.125)
+    W, H = 80, 60
+    poses = scene.fibonacci_poses(2, seed=3)
+    depth = scene.render_frames(K, W, H, poses)
+    ov = oracle.Volume()
+    ov.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    ov.setVolumeSize(40, 40, 40)
+    ov.constructVolume()
+    h, m, st = oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
+    for i in range(2):
+        xyz = oracle.backproject(K, depth[i], poses[i])
+        ov.integratePointCloud(xyz[depth[i] > 0], np.zeros_like(xyz[depth[i] > 0]))
+    assert np.array_equal(h > 0, ov.occupancy_dense().reshape(-1) > 0)
+    assert st[2] == h.sum() and st[0] == h.sum() + m.sum()
+
+
+def test_fusion_is_additive_over_pose_shards(oracle):
+    """Counts are associative: fusing shards and summing == fusing all (multi-GPU merge)."""
+    from dmf_amd import scene
+    K = scene.K_640x480.copy()
+    K[[0, 2, 4, 5]] *= np.float32(0.125)
+    poses = scene.fibonacci_poses(4, seed=9)
+    depth = scene.render_frames(K, 80, 60, poses)
+    def vol():
+        v = oracle.Volume()
+        v.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+        v.setVolumeSize(32, 32, 32)
+        v.constructVolume()
+        return v
+    h, m, _ = oracle.fuse_depth(vol(), K, depth, poses)
+    h1, m1, _ = oracle.fuse_depth(vol(), K, depth[:2], poses[:2])
+    h2, m2, _ = oracle.fuse_depth(vol(), K, depth[2:], poses[2:])
+    assert np.array_equal(h, h1 + h2) and np.array_equal(m, m1 + m2)
+    L = oracle.fuse_finalize(h, m)
+    assert L.min() >= -2000 and L.max() <= 3511
