@@ -15,6 +15,7 @@ torch.distributed.run (one rank per GPU, RCCL over xGMI).  Rank 0 prints ONE JSO
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -118,13 +119,15 @@ def main():
 
     d_depth = torch.from_numpy(depth.view(np.int16)).to(dev)
     d_poses = torch.from_numpy(np.ascontiguousarray(poses, np.float32)).to(dev)
-    counters = torch.zeros(2 * ncell, dtype=torch.int32, device=dev)  # [hits | misses]: one all-reduce
+    nct = C.c_int64()
+    _lib.check(L.dmf_fuse_counter_cells(vol._h, C.addressof(nct)))
+    nct = nct.value  # tiled counter layout
+    counters = torch.zeros(2 * nct, dtype=torch.int32, device=dev)  # [hits | misses]: one all-reduce
     logodds = torch.empty(ncell, dtype=torch.int16, device=dev)
     stats = torch.zeros(8, dtype=torch.int64, device=dev)
-    import ctypes as C
     pcam, pprm = C.addressof(cam), C.addressof(prm)
     hits_p = counters.data_ptr()
-    miss_p = counters.data_ptr() + 4 * ncell
+    miss_p = counters.data_ptr() + 4 * nct
 
     ev = []
 
@@ -179,7 +182,8 @@ def main():
         if os.path.exists(tpath):
             try:
                 tj = json.load(open(tpath))
-                if tj.get("grid") == grid and tj.get("poses") == P:
+                kname = L.dmf_fuse_kernel().decode()
+                if tj.get("grid") == grid and tj.get("poses") == P and tj.get("kernel") == kname:
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -214,7 +218,7 @@ def main():
             "updates_per_ray": updates / max(rays, 1.0),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_fuse", "kernel_ms": fuse_ms,
+                         "kernel": L.dmf_fuse_kernel().decode(), "kernel_ms": fuse_ms,
                          "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "secondary": secondary,

@@ -368,7 +368,7 @@ __global__ void k_first_flags(const int32_t* __restrict__ plin, int64_t n, const
 __global__ void k_assign_slots(Geom g, const int32_t* __restrict__ plin, const int32_t* __restrict__ flag,
                                const int32_t* __restrict__ rank, int64_t n, int64_t V0, int32_t* __restrict__ slot_of,
                                uint64_t* __restrict__ hash, int32_t* __restrict__ view, uint8_t* __restrict__ good,
-                               uint32_t* __restrict__ occ) {
+                               uint32_t* __restrict__ occ, uint32_t* __restrict__ brick, int nby, int nbz) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || !flag[i]) return;
   const int32_t lin = plin[i];
@@ -380,6 +380,9 @@ __global__ void k_assign_slots(Geom g, const int32_t* __restrict__ plin, const i
   view[slot] = 0;
   good[slot] = 0;
   atomicOr(&occ[(uint32_t)lin >> 5], 1u << ((uint32_t)lin & 31));
+  const uint32_t bl = ((uint32_t)(x >> kBrickShift) * (uint32_t)nby + (uint32_t)(y >> kBrickShift)) * (uint32_t)nbz +
+                      (uint32_t)(z >> kBrickShift);
+  atomicOr(&brick[bl >> 5], 1u << (bl & 31));
 }
 
 __global__ void k_point_slots(const int32_t* __restrict__ plin, int64_t n, const int32_t* __restrict__ slot_of,
@@ -484,7 +487,7 @@ static int integrate_impl(dmf_volume* v, const float* d_xyz, const float* d_nrm,
     v->Vcap = cap;
   }
   hipLaunchKernelGGL(k_assign_slots, grd, blk, 0, v->stream, g, (const int32_t*)plin, (const int32_t*)flag,
-                     (const int32_t*)rank, n, V0, v->d_slot_of, v->d_hash, v->d_view, v->d_good, v->d_occ);
+                     (const int32_t*)rank, n, V0, v->d_slot_of, v->d_hash, v->d_view, v->d_good, v->d_occ, v->d_brick, v->nb[1], v->nb[2]);
   DMF_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_point_slots, grd, blk, 0, v->stream, (const int32_t*)plin, n, v->d_slot_of, v->d_pslot + P0);
   DMF_LAUNCH_CHECK();
@@ -591,19 +594,19 @@ dmf::Geom dmf_volume::geom() const {
 
 dmf::DevVol dmf_volume::dev() const {
   DevVol d;
-  d.occ = d_occ; d.slot_of = d_slot_of; d.hash = d_hash; d.off = d_off; d.nrm = d_csr_nrm;
+  d.occ = d_occ; d.brick = d_brick; d.nb[0] = nb[0]; d.nb[1] = nb[1]; d.nb[2] = nb[2]; d.slot_of = d_slot_of; d.hash = d_hash; d.off = d_off; d.nrm = d_csr_nrm;
   d.view = d_view; d.good = d_good; d.V = V;
   return d;
 }
 
 static void free_state(dmf_volume* v) {
   auto f = [&](void* p) { if (p) (void)hipFree(p); };
-  f(v->d_occ); f(v->d_slot_of); f(v->d_hash); f(v->d_view); f(v->d_good);
+  f(v->d_occ); f(v->d_brick); f(v->d_slot_of); f(v->d_hash); f(v->d_view); f(v->d_good);
   f(v->d_pts); f(v->d_pnrm); f(v->d_pslot); f(v->d_off); f(v->d_csr_nrm); f(v->d_csr_pts);
   f(v->d_axes); f(v->d_enum);
   for (auto& s : v->scratch) f(s.first);
   v->scratch.clear();
-  v->d_occ = nullptr; v->d_slot_of = nullptr; v->d_hash = nullptr; v->d_view = nullptr; v->d_good = nullptr;
+  v->d_occ = nullptr; v->d_brick = nullptr; v->d_slot_of = nullptr; v->d_hash = nullptr; v->d_view = nullptr; v->d_good = nullptr;
   v->d_pts = nullptr; v->d_pnrm = nullptr; v->d_pslot = nullptr; v->d_off = nullptr; v->d_csr_nrm = nullptr;
   v->d_csr_pts = nullptr; v->d_axes = nullptr; v->d_enum = nullptr;
   v->V = v->Vcap = v->npts = v->pcap = v->nbinned = v->csr_cap = v->nenum = v->enum_cap = 0;
@@ -742,6 +745,11 @@ int dmf_volume_construct(dmf_volume* v) {
   if (v->ncell >= (size_t)0x7fffffff) return fail(DMF_ERR_RANGE, "more than 2^31-1 cells");
   DMF_HIP(hipMalloc((void**)&v->d_occ, sizeof(uint32_t) * ((v->ncell + 31) / 32 + 1)));
   DMF_HIP(hipMemsetAsync(v->d_occ, 0, sizeof(uint32_t) * ((v->ncell + 31) / 32 + 1), v->stream));
+  const int bs = 1 << kBrickShift;
+  v->nb[0] = (v->xdim + bs - 1) / bs; v->nb[1] = (v->ydim + bs - 1) / bs; v->nb[2] = (v->zdim + bs - 1) / bs;
+  const size_t bwords = ((size_t)v->nb[0] * v->nb[1] * v->nb[2] + 31) / 32 + 1;
+  DMF_HIP(hipMalloc((void**)&v->d_brick, sizeof(uint32_t) * bwords));
+  DMF_HIP(hipMemsetAsync(v->d_brick, 0, sizeof(uint32_t) * bwords, v->stream));
   DMF_HIP(hipMalloc((void**)&v->d_slot_of, sizeof(int32_t) * v->ncell));
   DMF_HIP(hipMemsetD32Async((hipDeviceptr_t)v->d_slot_of, kEmpty, v->ncell, v->stream));
   DMF_HIP(hipMalloc((void**)&v->d_off, sizeof(int32_t)));

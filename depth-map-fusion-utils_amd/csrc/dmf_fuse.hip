@@ -7,10 +7,12 @@
 // endpoints, crossing times compared by cross-multiplication), so GPU and CPU
 // oracle visit the same cells and the int32 hit/miss counts are bit-identical.
 //
-// Launch shape: a 256-lane workgroup owns a 16x16 pixel tile of one frame, each
-// 64-lane wave an 8x8 packet, so the rays of a workgroup start at one camera centre
-// and stay spatially coherent; the production kernel aggregates their cell updates
-// in LDS before touching HBM (k_fuse_lds).
+// The kernel is bound by the memory-side atomic request rate (≈2e10 64-B requests/s
+// chip-wide, MI355X_MICROARCH.md §Global float atomics): one request per distinct
+// 64-B line per wave instruction.  Two measures raise the cell updates per request:
+// LDS aggregation of each 8x8 ray packet's updates (≈8.8 rays share a cell per
+// round) and a tiled counter layout (2x2x4-cell tiles = one 64-B line, ≈5.3 of a
+// round's distinct cells per line instead of ≈3.0 for x-major rows).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -28,40 +30,55 @@ __device__ inline void atomic_add_dev(int32_t* p, int32_t v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave-wide min / max through DPP (row_shr 1,2,4,8 then row_bcast 15/31) and a
-// readlane: no LDS traffic, unlike __shfl_xor (ds_bpermute).
-__device__ inline int wave_min(int v) {
-  constexpr int kId = 0x7fffffff;
-  v = min(v, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xf, 0xf, false));
-  v = min(v, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xf, 0xf, false));
-  v = min(v, __builtin_amdgcn_update_dpp(kId, v, 0x114, 0xf, 0xf, false));
-  v = min(v, __builtin_amdgcn_update_dpp(kId, v, 0x118, 0xf, 0xf, false));
-  v = min(v, __builtin_amdgcn_update_dpp(kId, v, 0x142, 0xa, 0xf, false));
-  v = min(v, __builtin_amdgcn_update_dpp(kId, v, 0x143, 0xc, 0xf, false));
-  return __builtin_amdgcn_readlane(v, 63);
+// Tiled counter layout: 2x2x4-cell tiles (x, y, z), 16 int32 = one 64-B line, tiles
+// x-major over the padded grid; inside a tile ((x&1)*2 + (y&1))*4 + (z&3).
+struct Tiles {
+  uint32_t ny, nz;  // tiles along y and z
+};
+__host__ __device__ inline Tiles tiles_of(const int n[3]) {
+  return Tiles{(uint32_t)(n[1] + 1) >> 1, (uint32_t)(n[2] + 3) >> 2};
 }
-__device__ inline int wave_max(int v) {
-  constexpr int kId = (int)0x80000000;
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x114, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x118, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x142, 0xa, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x143, 0xc, 0xf, false));
-  return __builtin_amdgcn_readlane(v, 63);
+__host__ __device__ inline uint32_t tile_base(const Tiles& t, int tx, int ty, int tz) {
+  return (((uint32_t)tx * t.ny + (uint32_t)ty) * t.nz + (uint32_t)tz) << 4;
+}
+__host__ __device__ inline uint32_t tiled_index(const Tiles& t, int x, int y, int z) {
+  return tile_base(t, x >> 1, y >> 1, z >> 2) | (uint32_t)(((x & 1) << 3) | ((y & 1) << 2) | (z & 3));
+}
+inline size_t tiled_cells(const int n[3]) {
+  return (size_t)((n[0] + 1) >> 1) * (size_t)((n[1] + 1) >> 1) * (size_t)((n[2] + 3) >> 2) * 16;
 }
 
 // Per-ray DDA state after setup (exact integer walk).
+//
+// The oracle compares next-crossing times T_a = h_a * prod_{b != a} |dq_b| in 64 bits.
+// For a pair of moving axes, sign(T_a - T_b) = sign(E_ab) with
+// E_ab = h_a |dq_b| - h_b |dq_a| (T_a - T_b divided by the third axis' |dq|), and
+// because both next crossings lie within one cell interval of the current time,
+// |E_ab| < (2Q + 1) max|dq| <= 2^29 for grids up to 2048 cells per axis: the walk
+// runs on three int32 differences.  A step along axis a adds 2Q|dq_b| to E_ab (and
+// subtracts 2Q|dq_a| from E_ba).  A pair with a non-moving axis holds a constant that
+// never lets that axis win.
 struct Ray {
   int c[3];        // current cell
   int st[3];       // step direction per axis (-1, 0, +1)
-  int32_t lin;     // linear index of c
-  int32_t dl[3];   // linear-index delta per axis step
-  uint64_t T[3];   // next crossing time per axis (scaled, half units)
-  uint64_t In[3];  // crossing-time increment per axis
+  int32_t E01, E02, E12;  // crossing-time differences (see above)
+  int32_t K[3];    // 2Q |dq_a|
   int left;        // remaining cell updates (misses + final), 0 = inactive
   bool end_inside;
 };
+constexpr int32_t kNever = 1 << 30;  // |E| of a pair with a non-moving axis
+
+// One DDA selection (earliest crossing; ties x before y before z): s2 = z, s1 = y, else x.
+__device__ inline void dda_select(int32_t& E01, int32_t& E02, int32_t& E12, int32_t K0, int32_t K1, int32_t K2,
+                                  bool& s0, bool& s1, bool& s2) {
+  const bool b10 = E01 > 0;             // T1 < T0
+  s2 = (b10 ? E12 : E02) > 0;            // T2 < min(T0, T1)
+  s1 = !s2 && b10;
+  s0 = !s2 && !b10;
+  E01 += s0 ? K1 : (s1 ? -K0 : 0);
+  E02 += s0 ? K2 : (s2 ? -K0 : 0);
+  E12 += s1 ? K2 : (s2 ? -K1 : 0);
+}
 
 // Clip O->E to the grid and set up the walk.  Mirrors oracle.cpp dda_ray()
 // operation for operation.  Returns false when the ray misses the grid.
@@ -98,31 +115,28 @@ __device__ inline bool dda_setup(const Geom& g, const float O[3], const float E[
     qs[a] = clampi((int64_t)floor(gs * (double)kQ), cs[a] * kQ, cs[a] * kQ + kQ - 1);
     qe[a] = clampi((int64_t)floor(gx * (double)kQ), ce[a] * kQ, ce[a] * kQ + kQ - 1);
   }
-  uint64_t adq[3];
+  int64_t adq[3], h[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const int64_t dq = qe[a] - qs[a];
-    adq[a] = (uint64_t)(dq < 0 ? -dq : dq);
+    adq[a] = dq < 0 ? -dq : dq;
     R.st[a] = ce[a] > cs[a] ? 1 : (ce[a] < cs[a] ? -1 : 0);
+    // next crossing numerator in half fixed-point units (oracle.cpp dda_ray)
+    h[a] = R.st[a] > 0 ? 2 * ((cs[a] + 1) * kQ - qs[a]) : 2 * (qs[a] - cs[a] * kQ) + 1;
+    R.K[a] = (int32_t)(2 * kQ * adq[a]);
   }
-  // crossing times in half fixed-point units scaled by the other axes' |dq|
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const uint64_t M = (a != 0 && adq[0] ? adq[0] : 1) * (a != 1 && adq[1] ? adq[1] : 1) * (a != 2 && adq[2] ? adq[2] : 1);
-    const int64_t h = R.st[a] > 0 ? 2 * ((cs[a] + 1) * kQ - qs[a]) : 2 * (qs[a] - cs[a] * kQ) + 1;
-    R.T[a] = R.st[a] == 0 ? ~0ull : (uint64_t)h * M;
-    R.In[a] = (uint64_t)(2 * kQ) * M;
-  }
+  auto pair = [&](int a, int b) -> int32_t {
+    if (R.st[a] && R.st[b]) return (int32_t)(h[a] * adq[b] - h[b] * adq[a]);
+    return R.st[a] ? -kNever : (R.st[b] ? kNever : 0);
+  };
+  R.E01 = pair(0, 1);
+  R.E02 = pair(0, 2);
+  R.E12 = pair(1, 2);
   const int nsteps = (int)((ce[0] > cs[0] ? ce[0] - cs[0] : cs[0] - ce[0]) + (ce[1] > cs[1] ? ce[1] - cs[1] : cs[1] - ce[1]) +
                            (ce[2] > cs[2] ? ce[2] - cs[2] : cs[2] - ce[2]));
-  const int32_t sx = g.n[1] * g.n[2], sy = g.n[2];
-  R.dl[0] = R.st[0] * sx;
-  R.dl[1] = R.st[1] * sy;
-  R.dl[2] = R.st[2];
   R.c[0] = (int)cs[0];
   R.c[1] = (int)cs[1];
   R.c[2] = (int)cs[2];
-  R.lin = (int32_t)(cs[0] * sx + cs[1] * sy + cs[2]);
   R.left = nsteps + 1;
   R.end_inside = end_inside;
   return true;
@@ -130,16 +144,11 @@ __device__ inline bool dda_setup(const Geom& g, const float O[3], const float E[
 
 // Advance one cell (earliest crossing; ties x before y before z).
 __device__ inline void dda_advance(Ray& R) {
-  const bool b10 = R.T[1] < R.T[0];
-  const uint64_t m01 = b10 ? R.T[1] : R.T[0];
-  const bool b2 = R.T[2] < m01;
-  if (b2) {
-    R.T[2] += R.In[2]; R.lin += R.dl[2]; R.c[2] += R.st[2];
-  } else if (b10) {
-    R.T[1] += R.In[1]; R.lin += R.dl[1]; R.c[1] += R.st[1];
-  } else {
-    R.T[0] += R.In[0]; R.lin += R.dl[0]; R.c[0] += R.st[0];
-  }
+  bool s0, s1, s2;
+  dda_select(R.E01, R.E02, R.E12, R.K[0], R.K[1], R.K[2], s0, s1, s2);
+  R.c[0] += s0 ? R.st[0] : 0;
+  R.c[1] += s1 ? R.st[1] : 0;
+  R.c[2] += s2 ? R.st[2] : 0;
 }
 
 // Per-pixel ray: back-projection (Camera.hpp:24-45) + binning of the endpoint
@@ -178,6 +187,7 @@ __device__ inline void wave_stats(unsigned long long* stats, unsigned long long 
   }
 }
 
+
 // 16x16 tile of pixels per 256-lane workgroup; each wave an 8x8 packet.
 __device__ inline void tile_pixel(int tile, int tiles_x, int& r, int& c) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -185,8 +195,8 @@ __device__ inline void tile_pixel(int tile, int tiles_x, int& r, int& c) {
   r = (tile / tiles_x) * 16 + (w >> 1) * 8 + (l >> 3);
 }
 
-// Reference variant: one device-scope atomic per cell update.  Bound by the
-// memory-side atomic request rate (profiles/r01_baseline_atomic); kept for A/B.
+// Baseline: one device-scope atomic per cell update (profiles/r01_baseline_atomic);
+// kept as the A/B reference (DMF_FUSE_VARIANT=1).
 __global__ __launch_bounds__(256) void k_fuse_direct(Geom g, CamP cam, const uint16_t* __restrict__ depth,
                                                      const PoseX* __restrict__ poses, int dmin, int dmax, int tiles_x,
                                                      int32_t* __restrict__ hits, int32_t* __restrict__ misses,
@@ -198,569 +208,293 @@ __global__ __launch_bounds__(256) void k_fuse_direct(Geom g, CamP cam, const uin
   bool valid;
   const int upd = pixel_ray(g, cam, depth, poses, blockIdx.y, r, c, dmin, dmax, R, valid);
   const bool hit = R.left > 0 && R.end_inside;
+  const Tiles tl = tiles_of(g.n);
   while (R.left > 1) {
-    atomic_add_dev(&misses[R.lin], 1);
+    atomic_add_dev(&misses[tiled_index(tl, R.c[0], R.c[1], R.c[2])], 1);
     dda_advance(R);
     --R.left;
   }
-  if (R.left == 1) atomic_add_dev(R.end_inside ? &hits[R.lin] : &misses[R.lin], 1);
+  if (R.left == 1) {
+    const uint32_t ti = tiled_index(tl, R.c[0], R.c[1], R.c[2]);
+    atomic_add_dev(R.end_inside ? &hits[ti] : &misses[ti], 1);
+  }
   if (stats) wave_stats(stats, (unsigned long long)upd, valid ? 1ull : 0ull, hit ? 1ull : 0ull);
 }
 
-// LDS-aggregated variant (the production kernel).  The 256 rays of a tile walk in
-// lockstep rounds of kS cell updates.  Each round the workgroup reduces the
-// bounding box of the cells its rays can reach (the packet's slab), counts misses
-// into a dense LDS box with LDS atomics, records every first-touched cell in an LDS
-// list, then flushes ONE device-scope atomic per distinct cell: the global atomic
-// request count drops by the packet's rays-per-cell reuse.  A round
-// whose box exceeds kBox cells falls back to direct atomics.  Counts are exact
-// integers, so the result is bit-identical to k_fuse_direct and to the oracle.
-template <int kS, int kBox, int kFlush, bool kDpp = false, bool kVec = false, bool kExact = false, int kAblate = 0>
-__global__ __launch_bounds__(256) void k_fuse_lds(Geom g, CamP cam, const uint16_t* __restrict__ depth,
-                                                  const PoseX* __restrict__ poses, int dmin, int dmax, int tiles_x,
-                                                  int32_t* __restrict__ hits, int32_t* __restrict__ misses,
-                                                  unsigned long long* __restrict__ stats) {
+// Packed (hi | (0xffff - lo) << 16) extent reduction over the wave: one DPP max
+// chain of v_pk_max_u16 per axis gives both max(hi) and min(lo).  0 = no lane.
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ inline uint32_t pkmax(uint32_t a, uint32_t b) {
+  us2 x = __builtin_bit_cast(us2, a), y = __builtin_bit_cast(us2, b);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
+}
+__device__ inline uint32_t wave_pkmax(uint32_t v) {
+  v = pkmax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+  v = pkmax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+  v = pkmax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+  v = pkmax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+  v = pkmax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = pkmax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ inline int lane_prefix(uint64_t mask) {  // set lanes of mask below this lane
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// q = i / b for 0 <= i < 2^20, 1 <= b < 2^16 from a float reciprocal plus one
+// correction step (the float quotient is within 1 of the true one).
+__device__ inline int small_div(int i, int b, float rb, int& rem) {
+  int q = (int)((float)i * rb);
+  int r = i - q * b;
+  if (r < 0) { --q; r += b; }
+  if (r >= b) { ++q; r -= b; }
+  rem = r;
+  return q;
+}
+
+// Production fusion kernel.  One 64-lane workgroup per 8x8 pixel packet; the wave
+// runs its own rounds (no cross-wave barriers).  Per round:
+//  1. walk: each lane advances its DDA up to kS cell updates on the three int32
+//     crossing-time differences (dda_select: ties x < y < z), recording 2-bit axis
+//     codes; per-axis advance counts are popcounts;
+//  2. box: the exact extents of the round's miss cells, reduced over the wave with
+//     packed DPP maxima, widened to whole counter tiles (2x2x4), define a dense LDS
+//     box stored tile by tile, like the counters in HBM;
+//  3. replay: each lane replays its codes into LDS adds (odd lanes backwards from
+//     their last miss cell, so that neighbouring rays rarely hit one LDS address in
+//     the same instruction); the tiled LDS index moves by an in-tile delta or, when
+//     the step leaves the tile, by the tile stride;
+//  4. flush: an in-order scan of the box: 16 consecutive lanes = one tile = one 64-B
+//     line of the HBM counters, so each wave instruction issues at most 4 atomic
+//     requests, one per tile with a non-zero cell.
+// A round whose box exceeds kBox cells adds its misses to HBM directly.  Hits (one
+// per ray) go straight to HBM.  Counts are exact integers: bit-identical to
+// k_fuse_direct and to the oracle.
+template <int kS, int kBox, bool kShare = true>
+__global__ __launch_bounds__(64) void k_fuse_t(Geom g, CamP cam, const uint16_t* __restrict__ depth,
+                                               const PoseX* __restrict__ poses, int dmin, int dmax, int packets_x,
+                                               int32_t* __restrict__ hits, int32_t* __restrict__ misses,
+                                               unsigned long long* __restrict__ stats) {
+  static_assert(kS <= 15, "2-bit codes of up to 15 advances with a 32-bit field mask");
+  static_assert(kBox % 256 == 0 && kBox <= 65536, "box scanned 256 cells per iteration, 16-bit indices");
   stats = stat_slot(stats);
-  constexpr bool kScan = kFlush == 1, kRows = kFlush == 2;
-  constexpr int kList = kFlush == 1 ? 1 : 256 * kS;
   __shared__ __attribute__((aligned(16))) int box[kBox];
-  __shared__ int list_loc[kList];                  // list: cell loc   | rows: row index
-  __shared__ int32_t list_lin[kList];              // list: global lin | rows: global row base
-  __shared__ uint32_t rowbits[kRows ? kBox / 32 : 1];
-  __shared__ int red[4][6];
-  __shared__ int nlist;
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  for (int i = tid; i < kBox; i += 256) box[i] = 0;
-  if (kRows)
-    for (int i = tid; i < kBox / 32; i += 256) rowbits[i] = 0;
-  int r, c;
-  tile_pixel(blockIdx.x, tiles_x, r, c);
+  // non-zero cells of a round (<= its updates).  kShare: the list lives in the box
+  // itself — entry j is written while scanning cell i >= j, after cells <= i were
+  // read and cleared, and is cleared again after the flush.
+  __shared__ uint32_t nzl_own[kShare ? 1 : 64 * kS];
+  uint32_t* nzl = kShare ? (uint32_t*)box : nzl_own;
+  const int l = threadIdx.x;
+  for (int i = l; i < kBox; i += 64) box[i] = 0;
+  const int r = (blockIdx.x / packets_x) * 8 + (l >> 3), c = (blockIdx.x % packets_x) * 8 + (l & 7);
   Ray R;
   bool valid;
   const int upd = pixel_ray(g, cam, depth, poses, blockIdx.y, r, c, dmin, dmax, R, valid);
   const bool hit = R.left > 0 && R.end_inside;
-  unsigned long long nflush = 0, nround_lds = 0, nround_direct = 0;
-  while (true) {
-    // bounding box of the cells this lane can reach in the next kS updates
-    const int rem = R.left < kS ? R.left : kS;
-    int lo[3], hi[3];
-    if (kExact && rem > 0) {
-      // exact extent: pre-walk the round on a copy of the DDA state (VALU is cheap here)
-      Ray P = R;
-      for (int k = 1; k < rem; ++k) dda_advance(P);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        lo[a] = min(R.c[a], P.c[a]);
-        hi[a] = max(R.c[a], P.c[a]);
-      }
-    } else {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        if (rem > 0) {
-          const int reach = rem - 1;
-          lo[a] = R.c[a] - (R.st[a] < 0 ? reach : 0);
-          hi[a] = R.c[a] + (R.st[a] > 0 ? reach : 0);
-          lo[a] = lo[a] < 0 ? 0 : lo[a];
-          hi[a] = hi[a] >= g.n[a] ? g.n[a] - 1 : hi[a];
-        } else {
-          lo[a] = 0x7fffffff;
-          hi[a] = -1;
-        }
-      }
-    }
-    if (kDpp) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        lo[a] = wave_min(lo[a]);
-        hi[a] = wave_max(hi[a]);
-      }
-    } else {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          lo[a] = min(lo[a], __shfl_xor(lo[a], o, 64));
-          hi[a] = max(hi[a], __shfl_xor(hi[a], o, 64));
-        }
-      }
-    }
-    if (l == 0) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        red[w][a] = lo[a];
-        red[w][3 + a] = hi[a];
-      }
-    }
-    if (tid == 0) nlist = 0;
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      lo[a] = min(min(red[0][a], red[1][a]), min(red[2][a], red[3][a]));
-      hi[a] = max(max(red[0][3 + a], red[1][3 + a]), max(red[2][3 + a], red[3][3 + a]));
-    }
-    if (hi[0] < lo[0]) break;  // no active ray left in the tile (uniform)
-    const int e1 = hi[1] - lo[1] + 1, e2 = hi[2] - lo[2] + 1;
-    const int64_t vol = (int64_t)(hi[0] - lo[0] + 1) * e1 * e2;
-    const bool use_lds = vol <= kBox;
-    if (tid == 0) ++(use_lds ? nround_lds : nround_direct);
-    for (int k = 0; k < rem; ++k) {
-      if (R.left == 1 && R.end_inside) {
-        atomic_add_dev(&hits[R.lin], 1);
-      } else if (use_lds) {
-        const int row = (R.c[0] - lo[0]) * e1 + (R.c[1] - lo[1]);
-        const int loc = row * e2 + (R.c[2] - lo[2]);
-        if (kAblate & 2) {
-          nflush += (unsigned)loc;  // timing ablation: no LDS atomic
-        } else if (kScan) {
-          atomicAdd(&box[loc], 1);
-        } else if (kRows) {
-          if (atomicAdd(&box[loc], 1) == 0) {
-            const uint32_t bit = 1u << (row & 31);
-            if ((atomicOr(&rowbits[row >> 5], bit) & bit) == 0) {
-              const int j = atomicAdd(&nlist, 1);
-              list_loc[j] = row;
-              list_lin[j] = R.lin - R.c[2];
-            }
-          }
-        } else if (atomicAdd(&box[loc], 1) == 0) {
-          const int j = atomicAdd(&nlist, 1);
-          list_loc[j] = loc;
-          list_lin[j] = R.lin;
-        }
-      } else {
-        atomic_add_dev(&misses[R.lin], 1);
-      }
-      if (R.left > 1) dda_advance(R);
-      --R.left;
-    }
-    __syncthreads();
-    if (use_lds) {
-      if (kRows) {
-        // touched rows only; consecutive lanes -> consecutive z of a row -> contiguous atomics
-        const int nr = nlist;
-        const int total = nr * e2;
-        // k = i / e2 by a 33-bit reciprocal: ceil(2^32/e2) (2^32 for e2 = 1); exact for i, e2 <= 2^13
-        const uint64_t magic = (0x100000000ull + (uint64_t)e2 - 1) / (uint64_t)e2;
-        for (int i = tid; i < total; i += 256) {
-          const int k = (int)(((uint64_t)i * magic) >> 32);
-          const int iz = i - k * e2;
-          const int loc = list_loc[k] * e2 + iz;
-          const int cnt = box[loc];
-          if (cnt) {
-            ++nflush;
-            box[loc] = 0;
-            atomic_add_dev(&misses[list_lin[k] + lo[2] + iz], cnt);
-          }
-        }
-        for (int k = tid; k < nr; k += 256) rowbits[list_loc[k] >> 5] = 0;
-      } else if (kScan) {
-        if (kVec) {
-        // in-order box scan, 4 cells per 128-bit LDS read: consecutive lanes -> consecutive
-        // z of a box row -> contiguous device atomics
-        const int nyz = g.n[1] * g.n[2];
-        const int e12 = e1 * e2;
-        const uint64_t m12 = (0x100000000ull + (uint64_t)e12 - 1) / (uint64_t)e12;  // exact /e12, /e2
-        const uint64_t m2 = (0x100000000ull + (uint64_t)e2 - 1) / (uint64_t)e2;     // for i, e <= 2^13
-        int4* box4 = reinterpret_cast<int4*>(box);
-        const int nvec = ((int)vol + 3) >> 2;
-        for (int j = tid; j < nvec; j += 256) {
-          const int4 q = box4[j];
-          if ((q.x | q.y | q.z | q.w) == 0) continue;
-          box4[j] = make_int4(0, 0, 0, 0);
-          const int i0 = 4 * j;
-          int ix = (int)(((uint64_t)i0 * m12) >> 32);
-          const int r2 = i0 - ix * e12;
-          int iy = (int)(((uint64_t)r2 * m2) >> 32);
-          int iz = r2 - iy * e2;
-          const int cnts[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (cnts[t]) {
-              ++nflush;
-              atomic_add_dev(&misses[(lo[0] + ix) * nyz + (lo[1] + iy) * g.n[2] + lo[2] + iz], cnts[t]);
-            }
-            if (++iz == e2) { iz = 0; if (++iy == e1) { iy = 0; ++ix; } }
-          }
-        }
-        } else {
-          const int nyz = g.n[1] * g.n[2];
-          const int e12 = e1 * e2;
-          for (int i = tid; i < (int)vol; i += 256) {
-            const int cnt = box[i];
-            if (cnt) {
-              ++nflush;
-              box[i] = 0;
-                  const int ix = i / e12, rem2 = i - ix * e12, iy = rem2 / e2, iz = rem2 - iy * e2;
-              if (!(kAblate & 1))  // timing ablation: no device atomics in the flush
-                atomic_add_dev(&misses[(lo[0] + ix) * nyz + (lo[1] + iy) * g.n[2] + lo[2] + iz], cnt);
-              else
-                nflush += (unsigned)(ix + iy + iz);
-            }
-          }
-        }
-      } else {
-        const int n = nlist;
-        for (int j = tid; j < n; j += 256) {
-          const int loc = list_loc[j];
-          const int cnt = box[loc];
-          box[loc] = 0;
-          ++nflush;
-          atomic_add_dev(&misses[list_lin[j]], cnt);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (stats) {
-    wave_stats(stats, (unsigned long long)upd, valid ? 1ull : 0ull, hit ? 1ull : 0ull);
-    // aggregation diagnostics: [4] LDS rounds, [5] fallback rounds, [6] flushed cells
-    for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
-    if (l == 0 && nflush) atomicAdd(&stats[6], nflush);
-    if (tid == 0) {
-      if (nround_lds) atomicAdd(&stats[4], nround_lds);
-      if (nround_direct) atomicAdd(&stats[5], nround_direct);
-    }
-  }
-}
-
-// clamp(hits*l_hit + misses*l_miss, l_min, l_max) -> int16, 8 cells per lane
-// (2 x 32 B loads, one 16 B store: a pure HBM stream).
-__global__ __launch_bounds__(256) void k_finalize(const int32_t* __restrict__ hits, const int32_t* __restrict__ misses,
-                                                  int64_t n, int l_hit, int l_miss, int l_min, int l_max,
-                                                  int16_t* __restrict__ out) {
-  const int64_t i8 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (i8 >= n) return;
-  auto f = [&](int32_t h, int32_t m) -> int16_t {
-    int64_t L = (int64_t)h * l_hit + (int64_t)m * l_miss;
-    L = L < l_min ? l_min : (L > l_max ? l_max : L);
-    return (int16_t)L;
-  };
-  if (i8 + 8 <= n) {
-    const int4 h0 = *(const int4*)(hits + i8), h1 = *(const int4*)(hits + i8 + 4);
-    const int4 m0 = *(const int4*)(misses + i8), m1 = *(const int4*)(misses + i8 + 4);
-    union { int16_t s[8]; int4 v; } o;
-    o.s[0] = f(h0.x, m0.x); o.s[1] = f(h0.y, m0.y); o.s[2] = f(h0.z, m0.z); o.s[3] = f(h0.w, m0.w);
-    o.s[4] = f(h1.x, m1.x); o.s[5] = f(h1.y, m1.y); o.s[6] = f(h1.z, m1.z); o.s[7] = f(h1.w, m1.w);
-    *(int4*)(out + i8) = o.v;
-  } else {
-    for (int64_t i = i8; i < n; ++i) out[i] = f(hits[i], misses[i]);
-  }
-}
-
-// Branch-free DDA step over the crossing times only; returns the axis taken
-// (ties x before y before z) as the three selector masks.
-__device__ inline void dda_pick(uint64_t& T0, uint64_t& T1, uint64_t& T2, uint64_t I0, uint64_t I1, uint64_t I2,
-                                bool& s0, bool& s1, bool& s2) {
-  const bool b10 = T1 < T0;
-  const uint64_t m = b10 ? T1 : T0;
-  s2 = T2 < m;
-  s1 = !s2 && b10;
-  s0 = !s2 && !b10;
-  T0 = s0 ? T0 + I0 : T0;
-  T1 = s1 ? T1 + I1 : T1;
-  T2 = s2 ? T2 + I2 : T2;
-}
-
-// Lean LDS-aggregated fusion kernel.  Same rounds / LDS slab box / in-order flush as
-// k_fuse_lds, but inside an LDS round a lane only advances its crossing times and
-// its box-local index (branch-free); the cell coordinates and the grid index are
-// recovered once per round by exact reciprocal division.  Bit-identical counts.
-template <int kS, int kBox>
-__global__ __launch_bounds__(256) void k_fuse_lean(Geom g, CamP cam, const uint16_t* __restrict__ depth,
-                                                   const PoseX* __restrict__ poses, int dmin, int dmax, int tiles_x,
-                                                   int32_t* __restrict__ hits, int32_t* __restrict__ misses,
-                                                   unsigned long long* __restrict__ stats) {
-  stats = stat_slot(stats);
-  __shared__ __attribute__((aligned(16))) int box[kBox];
-  __shared__ int red[4][6];
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  for (int i = tid; i < kBox; i += 256) box[i] = 0;
-  int r, c;
-  tile_pixel(blockIdx.x, tiles_x, r, c);
-  Ray R;
-  bool valid;
-  const int upd = pixel_ray(g, cam, depth, poses, blockIdx.y, r, c, dmin, dmax, R, valid);
-  const bool hit = R.left > 0 && R.end_inside;
-  const int nyz = g.n[1] * g.n[2], nz = g.n[2];
-  uint64_t T0 = R.T[0], T1 = R.T[1], T2 = R.T[2];
-  const uint64_t I0 = R.In[0], I1 = R.In[1], I2 = R.In[2];
-  int c0 = R.c[0], c1 = R.c[1], c2 = R.c[2];
-  int lin = R.lin, left = R.left;
-  unsigned long long nflush = 0, nround_lds = 0, nround_direct = 0;
-  while (true) {
-    const int rem = left < kS ? left : kS;
-    int lo0, lo1, lo2, hi0, hi1, hi2;
-    {
-      const int reach = rem - 1;
-      const bool act = rem > 0;
-      lo0 = act ? max(c0 - (R.st[0] < 0 ? reach : 0), 0) : 0x7fffffff;
-      lo1 = act ? max(c1 - (R.st[1] < 0 ? reach : 0), 0) : 0x7fffffff;
-      lo2 = act ? max(c2 - (R.st[2] < 0 ? reach : 0), 0) : 0x7fffffff;
-      hi0 = act ? min(c0 + (R.st[0] > 0 ? reach : 0), g.n[0] - 1) : -1;
-      hi1 = act ? min(c1 + (R.st[1] > 0 ? reach : 0), g.n[1] - 1) : -1;
-      hi2 = act ? min(c2 + (R.st[2] > 0 ? reach : 0), g.n[2] - 1) : -1;
-    }
-    lo0 = wave_min(lo0); lo1 = wave_min(lo1); lo2 = wave_min(lo2);
-    hi0 = wave_max(hi0); hi1 = wave_max(hi1); hi2 = wave_max(hi2);
-    if (l == 0) {
-      red[w][0] = lo0; red[w][1] = lo1; red[w][2] = lo2;
-      red[w][3] = hi0; red[w][4] = hi1; red[w][5] = hi2;
-    }
-    __syncthreads();
-    lo0 = min(min(red[0][0], red[1][0]), min(red[2][0], red[3][0]));
-    lo1 = min(min(red[0][1], red[1][1]), min(red[2][1], red[3][1]));
-    lo2 = min(min(red[0][2], red[1][2]), min(red[2][2], red[3][2]));
-    hi0 = max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
-    hi1 = max(max(red[0][4], red[1][4]), max(red[2][4], red[3][4]));
-    hi2 = max(max(red[0][5], red[1][5]), max(red[2][5], red[3][5]));
-    if (hi0 < lo0) break;  // no active ray left in the tile (uniform)
-    const int e1 = hi1 - lo1 + 1, e2 = hi2 - lo2 + 1, e12 = e1 * e2;
-    const int64_t vol = (int64_t)(hi0 - lo0 + 1) * e12;
-    const bool use_lds = vol <= kBox;
-    const int nf = rem < left ? rem : rem - 1;  // updates followed by an advance
-    const bool fin = rem == left && rem > 0;    // this round holds the final update
-    if (use_lds) {
-      if (tid == 0) ++nround_lds;
-      const int b0 = R.st[0] * e12, b1 = R.st[1] * e2, b2 = R.st[2];
-      int loc = ((c0 - lo0) * e1 + (c1 - lo1)) * e2 + (c2 - lo2);
-      int ploc = loc;  // last updated (in-box) cell
-      bool s0 = false, s1 = false, s2 = false;
-      for (int k = 0; k < nf; ++k) {
-        atomicAdd(&box[loc], 1);
-        dda_pick(T0, T1, T2, I0, I1, I2, s0, s1, s2);
-        ploc = loc;
-        loc += s2 ? b2 : (s1 ? b1 : b0);
-      }
-      if (rem > 0) {
-        // Recover the cell from an in-box index (exact reciprocal division for loc,
-        // e <= 2^13).  A non-final round ends one advance past its box: decode the
-        // last updated cell and apply that advance to the coordinates.
-        const int dloc = fin ? loc : ploc;
-        const uint64_t m12 = (0x100000000ull + (uint64_t)e12 - 1) / (uint64_t)e12;
-        const uint64_t m2 = (0x100000000ull + (uint64_t)e2 - 1) / (uint64_t)e2;
-        const int ix = (int)(((uint64_t)dloc * m12) >> 32);
-        const int rr = dloc - ix * e12;
-        const int iy = (int)(((uint64_t)rr * m2) >> 32);
-        c0 = lo0 + ix;
-        c1 = lo1 + iy;
-        c2 = lo2 + (rr - iy * e2);
-        if (!fin) {
-          c0 += s0 ? R.st[0] : 0;
-          c1 += s1 ? R.st[1] : 0;
-          c2 += s2 ? R.st[2] : 0;
-        }
-        lin = c0 * nyz + c1 * nz + c2;
-        if (fin) {
-          if (R.end_inside) atomic_add_dev(&hits[lin], 1);
-          else atomicAdd(&box[loc], 1);
-        }
-      }
-    } else {
-      if (tid == 0) ++nround_direct;
-      for (int k = 0; k < nf; ++k) {
-        atomic_add_dev(&misses[lin], 1);
-        bool s0, s1, s2;
-        dda_pick(T0, T1, T2, I0, I1, I2, s0, s1, s2);
-        lin += s2 ? R.dl[2] : (s1 ? R.dl[1] : R.dl[0]);
-        c0 += s0 ? R.st[0] : 0;
-        c1 += s1 ? R.st[1] : 0;
-        c2 += s2 ? R.st[2] : 0;
-      }
-      if (fin) atomic_add_dev(R.end_inside ? &hits[lin] : &misses[lin], 1);
-    }
-    left -= rem;
-    __syncthreads();
-    if (use_lds) {
-      // in-order box scan: consecutive lanes -> consecutive z -> contiguous device atomics
-      for (int i = tid; i < (int)vol; i += 256) {
-        const int cnt = box[i];
-        if (cnt) {
-          ++nflush;
-          box[i] = 0;
-          const int ix = i / e12, rr = i - ix * e12, iy = rr / e2, iz = rr - iy * e2;
-          atomic_add_dev(&misses[(lo0 + ix) * nyz + (lo1 + iy) * nz + lo2 + iz], cnt);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (stats) {
-    wave_stats(stats, (unsigned long long)upd, valid ? 1ull : 0ull, hit ? 1ull : 0ull);
-    for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
-    if (l == 0 && nflush) atomicAdd(&stats[6], nflush);
-    if (tid == 0) {
-      if (nround_lds) atomicAdd(&stats[4], nround_lds);
-      if (nround_direct) atomicAdd(&stats[5], nround_direct);
-    }
-  }
-}
-
-// Single-walk LDS-aggregated fusion kernel (production).  Per round each lane walks
-// its DDA once for up to kS updates, recording the axis of every step as a 2-bit
-// code; the tile's exact slab box is reduced (DPP + LDS); the codes are replayed into
-// box indices held in registers, and the LDS atomics are issued forward on even
-// lanes and backward on odd lanes so that neighbouring rays, which share cells at
-// the same step, rarely hit the same LDS address in one instruction.  In-order box
-// scan flush (contiguous device atomics).  Bit-identical counts.
-template <int kS, int kBox>
-__global__ __launch_bounds__(256) void k_fuse_v2(Geom g, CamP cam, const uint16_t* __restrict__ depth,
-                                                 const PoseX* __restrict__ poses, int dmin, int dmax, int tiles_x,
-                                                 int32_t* __restrict__ hits, int32_t* __restrict__ misses,
-                                                 unsigned long long* __restrict__ stats) {
-  stats = stat_slot(stats);
-  static_assert(kS <= 16, "2-bit step codes are packed into one 32-bit register");
-  __shared__ __attribute__((aligned(16))) int box[kBox];
-  __shared__ int red[4][6];
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  for (int i = tid; i < kBox; i += 256) box[i] = 0;
-  int r, c;
-  tile_pixel(blockIdx.x, tiles_x, r, c);
-  Ray R;
-  bool valid;
-  const int upd = pixel_ray(g, cam, depth, poses, blockIdx.y, r, c, dmin, dmax, R, valid);
-  const bool hit = R.left > 0 && R.end_inside;
-  const int nyz = g.n[1] * g.n[2], nz = g.n[2];
-  uint64_t T0 = R.T[0], T1 = R.T[1], T2 = R.T[2];
-  const uint64_t I0 = R.In[0], I1 = R.In[1], I2 = R.In[2];
+  const Tiles tl = tiles_of(g.n);
+  int32_t E01 = R.E01, E02 = R.E02, E12 = R.E12;
+  const int32_t K0 = R.K[0], K1 = R.K[1], K2 = R.K[2];
+  const int st0 = R.st[0], st1 = R.st[1], st2 = R.st[2];
+  const bool end_inside = R.end_inside;
   int c0 = R.c[0], c1 = R.c[1], c2 = R.c[2];
   int left = R.left;
   const bool odd = (l & 1) != 0;
   unsigned long long nflush = 0, nround_lds = 0, nround_direct = 0;
-  while (true) {
+  while (__builtin_amdgcn_ballot_w64(left > 0)) {
     const int rem = left < kS ? left : kS;
-    const bool fin = rem == left && rem > 0;  // this round holds the ray's final update
-    const int nadv = fin ? rem - 1 : rem;      // DDA advances this round
-    // walk once: 2-bit axis code per advance, end cell of the round
+    const bool fin = rem == left && rem > 0;
+    const int nadv = fin ? rem - 1 : rem;
     uint32_t codes = 0;
-    int e0 = c0, e1c = c1, e2c = c2;
+    if (__builtin_amdgcn_ballot_w64(nadv != kS) == 0) {  // every lane walks kS steps
 #pragma unroll
-    for (int k = 0; k < kS; ++k) {
-      if (k < nadv) {
+      for (int k = 0; k < kS; ++k) {
         bool s0, s1, s2;
-        dda_pick(T0, T1, T2, I0, I1, I2, s0, s1, s2);
+        dda_select(E01, E02, E12, K0, K1, K2, s0, s1, s2);
         codes |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
-        e0 += s0 ? R.st[0] : 0;
-        e1c += s1 ? R.st[1] : 0;
-        e2c += s2 ? R.st[2] : 0;
-      }
-    }
-    // exact extent per axis: monotone walk -> [min, max] of start and last updated cell;
-    // the last advance of a non-final round leaves the round, so use the cell before it
-    int l0 = c0, l1 = c1, l2 = c2;
-    if (!fin && nadv > 0) {
-      const uint32_t last = (codes >> (2 * (nadv - 1))) & 3u;
-      l0 = e0 - (last == 0u ? R.st[0] : 0);
-      l1 = e1c - (last == 1u ? R.st[1] : 0);
-      l2 = e2c - (last == 2u ? R.st[2] : 0);
-    } else {
-      l0 = e0; l1 = e1c; l2 = e2c;
-    }
-    const bool act = rem > 0;
-    int lo0 = act ? min(c0, l0) : 0x7fffffff, hi0 = act ? max(c0, l0) : -1;
-    int lo1 = act ? min(c1, l1) : 0x7fffffff, hi1 = act ? max(c1, l1) : -1;
-    int lo2 = act ? min(c2, l2) : 0x7fffffff, hi2 = act ? max(c2, l2) : -1;
-    lo0 = wave_min(lo0); lo1 = wave_min(lo1); lo2 = wave_min(lo2);
-    hi0 = wave_max(hi0); hi1 = wave_max(hi1); hi2 = wave_max(hi2);
-    if (l == 0) {
-      red[w][0] = lo0; red[w][1] = lo1; red[w][2] = lo2;
-      red[w][3] = hi0; red[w][4] = hi1; red[w][5] = hi2;
-    }
-    __syncthreads();
-    lo0 = min(min(red[0][0], red[1][0]), min(red[2][0], red[3][0]));
-    lo1 = min(min(red[0][1], red[1][1]), min(red[2][1], red[3][1]));
-    lo2 = min(min(red[0][2], red[1][2]), min(red[2][2], red[3][2]));
-    hi0 = max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
-    hi1 = max(max(red[0][4], red[1][4]), max(red[2][4], red[3][4]));
-    hi2 = max(max(red[0][5], red[1][5]), max(red[2][5], red[3][5]));
-    if (hi0 < lo0) break;  // no active ray left in the tile (uniform)
-    const int bx1 = hi1 - lo1 + 1, bx2 = hi2 - lo2 + 1, b12 = bx1 * bx2;
-    const int64_t vol = (int64_t)(hi0 - lo0 + 1) * b12;
-    const bool use_lds = vol <= kBox;
-    const int nmiss = (fin && R.end_inside) ? rem - 1 : rem;  // LDS/miss updates this round
-    if (use_lds) {
-      if (tid == 0) ++nround_lds;
-      const int sx = R.st[0] * b12, sy = R.st[1] * bx2, sz = R.st[2];
-      int loc[kS];
-      int cur = ((c0 - lo0) * bx1 + (c1 - lo1)) * bx2 + (c2 - lo2);
-#pragma unroll
-      for (int k = 0; k < kS; ++k) {
-        loc[k] = cur;
-        const uint32_t cd = (codes >> (2 * k)) & 3u;
-        cur += cd == 2u ? sz : (cd == 1u ? sy : sx);
-      }
-#pragma unroll
-      for (int k = 0; k < kS; ++k) {
-        const int kk = odd ? kS - 1 - k : k;
-        if (kk < nmiss) atomicAdd(&box[loc[kk]], 1);
       }
     } else {
-      if (tid == 0) ++nround_direct;
-      int lin = c0 * nyz + c1 * nz + c2;
-      const int d0 = R.st[0] * nyz, d1 = R.st[1] * nz, d2 = R.st[2];
 #pragma unroll
       for (int k = 0; k < kS; ++k) {
-        if (k < nmiss) atomic_add_dev(&misses[lin], 1);
-        const uint32_t cd = (codes >> (2 * k)) & 3u;
-        lin += cd == 2u ? d2 : (cd == 1u ? d1 : d0);
-      }
-    }
-    if (fin && R.end_inside) atomic_add_dev(&hits[e0 * nyz + e1c * nz + e2c], 1);
-    c0 = e0; c1 = e1c; c2 = e2c;
-    left -= rem;
-    __syncthreads();
-    if (use_lds) {
-      // in-order box scan: consecutive lanes -> consecutive z -> contiguous device atomics
-      for (int i = tid; i < (int)vol; i += 256) {
-        const int cnt = box[i];
-        if (cnt) {
-          ++nflush;
-          box[i] = 0;
-          const int ix = i / b12, rr = i - ix * b12, iy = rr / bx2, iz = rr - iy * bx2;
-          atomic_add_dev(&misses[(lo0 + ix) * nyz + (lo1 + iy) * nz + lo2 + iz], cnt);
+        if (k < nadv) {
+          bool s0, s1, s2;
+          dda_select(E01, E02, E12, K0, K1, K2, s0, s1, s2);
+          codes |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
         }
       }
     }
-    __syncthreads();
+    const uint32_t fmask = (1u << (2 * nadv)) - 1u;
+    const int n2 = __builtin_popcount(codes & fmask & 0xAAAAAAAAu);
+    const int n1 = __builtin_popcount(codes & fmask & 0x55555555u);
+    const int n0 = nadv - n1 - n2;
+    const int e0 = c0 + st0 * n0, e1 = c1 + st1 * n1, e2 = c2 + st2 * n2;
+    const int nm = (fin && end_inside) ? rem - 1 : rem;  // miss updates this round
+    // cell of the last miss update: the end cell, or one advance before it
+    int m0 = e0, m1 = e1, m2 = e2;
+    if (nm > 0 && nadv > 0 && (!fin || end_inside)) {
+      const uint32_t lc = (codes >> (2 * (nadv - 1))) & 3u;
+      m0 -= lc == 0u ? st0 : 0;
+      m1 -= lc == 1u ? st1 : 0;
+      m2 -= lc == 2u ? st2 : 0;
+    }
+    const bool act = nm > 0;
+    const uint32_t px = act ? ((uint32_t)max(c0, m0) | ((0xffffu - (uint32_t)min(c0, m0)) << 16)) : 0u;
+    const uint32_t py = act ? ((uint32_t)max(c1, m1) | ((0xffffu - (uint32_t)min(c1, m1)) << 16)) : 0u;
+    const uint32_t pz = act ? ((uint32_t)max(c2, m2) | ((0xffffu - (uint32_t)min(c2, m2)) << 16)) : 0u;
+    const uint32_t rx = wave_pkmax(px), ry = wave_pkmax(py), rz = wave_pkmax(pz);
+    if (rx != 0u) {
+      // box = whole tiles covering the extents; origin (ax, ay, az) on a tile corner
+      const int ax = (0xffff - (int)(rx >> 16)) & ~1, ay = (0xffff - (int)(ry >> 16)) & ~1,
+                az = (0xffff - (int)(rz >> 16)) & ~3;
+      const int tbx = (((int)(rx & 0xffffu) - ax) >> 1) + 1, tby = (((int)(ry & 0xffffu) - ay) >> 1) + 1,
+                tbz = (((int)(rz & 0xffffu) - az) >> 2) + 1;
+      const int tyz = tby * tbz;
+      const int64_t ncell_box = (int64_t)tbx * tyz * 16;
+      // replay direction and first replayed cell
+      const int sgn = odd ? -1 : 1;
+      int x = odd ? m0 : c0, y = odd ? m1 : c1, z = odd ? m2 : c2;
+      const int gx = sgn * st0, gy = sgn * st1, gz = sgn * st2;
+      int sh = odd ? 2 * (nm - 2) : 0;
+      const int dsh = odd ? -2 : 2;
+      if (ncell_box <= kBox) {
+        ++nround_lds;
+        // Next-step delta per axis: in-tile (x: 8, y: 4, z: 1) or, when the step leaves
+        // the tile, the tile stride minus the in-tile span; x and y alternate between
+        // the two, z crosses every 4th step.  Signed by the replay direction.
+        const int ix = gx * 8, iy = gy * 4, iz = gz;
+        const int jx = gx * (tyz * 16 - 8), jy = gy * (tbz * 16 - 4), jz = gz * 13;
+        const int fz = gz > 0 ? 3 : 0;
+        int qz = z & 3;
+        int nx = ((x & 1) == (gx > 0 ? 1 : 0)) ? jx : ix;
+        int ny = ((y & 1) == (gy > 0 ? 1 : 0)) ? jy : iy;
+        int nzd = qz == fz ? jz : iz;
+        const int tx_ = ix ^ jx, ty_ = iy ^ jy;
+        int cur = ((((x - ax) >> 1) * tby + ((y - ay) >> 1)) * tbz + ((z - az) >> 2)) * 16 +
+                  (((x & 1) << 3) | ((y & 1) << 2) | qz);
+#pragma unroll
+        for (int k = 0; k < kS; ++k) {
+          if (k < nm) atomicAdd(&box[cur], 1);
+          const uint32_t cd = (codes >> (sh & 31)) & 3u;
+          const bool ax0 = cd == 0u, ax1 = cd == 1u, ax2 = cd == 2u;
+          cur += ax2 ? nzd : (ax1 ? ny : nx);
+          nx ^= ax0 ? tx_ : 0;
+          ny ^= ax1 ? ty_ : 0;
+          qz = ax2 ? ((qz + gz) & 3) : qz;
+          nzd = qz == fz ? jz : iz;
+          sh += dsh;
+        }
+        __syncthreads();  // single-wave workgroup: orders the LDS adds before the flush
+        // compact the non-zero cells (box order = tile order) into (index | count << 16)
+        const int nb = (int)ncell_box;
+        int nnz = 0;
+        for (int i0 = 0; i0 < nb; i0 += 256) {
+          int v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + l;
+            v[u] = i < nb ? box[i] : 0;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint64_t b = __builtin_amdgcn_ballot_w64(v[u] != 0);
+            if (v[u]) {
+              const int i = i0 + 64 * u + l;
+              box[i] = 0;
+              nzl[nnz + lane_prefix(b)] = (uint32_t)i | ((uint32_t)v[u] << 16);
+            }
+            nnz += __builtin_popcountll(b);
+          }
+        }
+        __syncthreads();
+        const float rtyz = 1.0f / (float)tyz, rtz = 1.0f / (float)tbz;
+        const int tax = ax >> 1, tay = ay >> 1, taz = az >> 2;
+        for (int e = l; e < nnz; e += 64) {
+          const uint32_t en = nzl[e];
+          const int i = (int)(en & 0xffffu);
+          int rr, tc;
+          const int t = i >> 4;
+          const int ta = small_div(t, tyz, rtyz, rr);
+          const int tb = small_div(rr, tbz, rtz, tc);
+          ++nflush;
+          atomic_add_dev(&misses[tile_base(tl, tax + ta, tay + tb, taz + tc) + (i & 15)], (int)(en >> 16));
+        }
+        if (kShare) {
+          __syncthreads();
+          for (int e = l; e < nnz; e += 64) box[e] = 0;
+        }
+        __syncthreads();
+      } else {
+        ++nround_direct;
+#pragma unroll
+        for (int k = 0; k < kS; ++k) {
+          if (k < nm) atomic_add_dev(&misses[tiled_index(tl, x, y, z)], 1);
+          const uint32_t cd = (codes >> (sh & 31)) & 3u;
+          x += cd == 0u ? gx : 0;
+          y += cd == 1u ? gy : 0;
+          z += cd == 2u ? gz : 0;
+          sh += dsh;
+        }
+      }
+    }
+    if (fin && end_inside) atomic_add_dev(&hits[tiled_index(tl, e0, e1, e2)], 1);
+    c0 = e0; c1 = e1; c2 = e2;
+    left -= rem;
   }
   if (stats) {
     wave_stats(stats, (unsigned long long)upd, valid ? 1ull : 0ull, hit ? 1ull : 0ull);
     for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
-    if (l == 0 && nflush) atomicAdd(&stats[6], nflush);
-    if (tid == 0) {
+    if (l == 0) {
+      if (nflush) atomicAdd(&stats[6], nflush);
       if (nround_lds) atomicAdd(&stats[4], nround_lds);
       if (nround_direct) atomicAdd(&stats[5], nround_direct);
     }
   }
 }
 
-// Timing-only probes (wrong results, DMF_FUSE_VARIANT >= 94): 94 = setup only,
-// 95 = setup + register-only DDA walk (no LDS, no barriers, no atomics).
-template <int kMode>
-__global__ __launch_bounds__(256) void k_fuse_probe(Geom g, CamP cam, const uint16_t* __restrict__ depth,
-                                                    const PoseX* __restrict__ poses, int dmin, int dmax, int tiles_x,
-                                                    int32_t* __restrict__ hits, int32_t* __restrict__ misses,
-                                                    unsigned long long* __restrict__ stats) {
-  stats = stat_slot(stats);
-  int r, c;
-  tile_pixel(blockIdx.x, tiles_x, r, c);
-  Ray R;
-  bool valid;
-  const int upd = pixel_ray(g, cam, depth, poses, blockIdx.y, r, c, dmin, dmax, R, valid);
-  uint64_t T0 = R.T[0], T1 = R.T[1], T2 = R.T[2];
-  int lin = R.lin;
-  if (kMode == 1) {
-    for (int k = 1; k < R.left; ++k) {
-      bool s0, s1, s2;
-      dda_pick(T0, T1, T2, R.In[0], R.In[1], R.In[2], s0, s1, s2);
-      lin += s2 ? R.dl[2] : (s1 ? R.dl[1] : R.dl[0]);
-    }
+// Tiled counters -> clamped int16 log-odds in the reference's x-major voxel order.
+// One lane per 4 consecutive z cells: one 16-B read per counter, one 8-B write.
+__global__ __launch_bounds__(256) void k_finalize(Geom g, const int32_t* __restrict__ hits,
+                                                  const int32_t* __restrict__ misses, int l_hit, int l_miss,
+                                                  int l_min, int l_max, int16_t* __restrict__ out) {
+  const int nz4 = (g.n[2] + 3) >> 2;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t rows = (int64_t)g.n[0] * g.n[1];
+  if (q >= rows * nz4) return;
+  const int64_t row = q / nz4;
+  const int z = (int)(q - row * nz4) * 4;
+  const int x = (int)(row / g.n[1]), y = (int)(row - (int64_t)x * g.n[1]);
+  const uint32_t ti = tiled_index(tiles_of(g.n), x, y, z);
+  const int4 h = *(const int4*)(hits + ti), m = *(const int4*)(misses + ti);
+  auto f = [&](int32_t hv, int32_t mv) -> int16_t {
+    int64_t L = (int64_t)hv * l_hit + (int64_t)mv * l_miss;
+    L = L < l_min ? l_min : (L > l_max ? l_max : L);
+    return (int16_t)L;
+  };
+  const int16_t o[4] = {f(h.x, m.x), f(h.y, m.y), f(h.z, m.z), f(h.w, m.w)};
+  int16_t* dst = out + (row * g.n[2] + z);
+  if (z + 4 <= g.n[2] && ((uintptr_t)dst & 7) == 0) {
+    *(uint2*)dst = *(const uint2*)o;
+  } else {
+    for (int k = 0; k < 4 && z + k < g.n[2]; ++k) dst[k] = o[k];
   }
-  if (lin == -12345 && T0 == 7) hits[0] = 1;  // keep the walk alive
-  if (stats) wave_stats(stats, (unsigned long long)upd, valid ? 1ull : 0ull, 0ull);
 }
 
-// Kernel variant: DMF_FUSE_VARIANT=<n> selects a (round length, LDS box, flush)
-// instantiation for A/B measurements; 1 = one atomic per update (k_fuse_direct).
+// Linear (x-major) <-> tiled counter copies for the host-pointer API and tests.
+template <bool kToLinear>
+__global__ __launch_bounds__(256) void k_counter_layout(Geom g, const int32_t* __restrict__ src,
+                                                        int32_t* __restrict__ dst, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t nyz = (int64_t)g.n[1] * g.n[2];
+  const int x = (int)(i / nyz);
+  const int64_t rr = i - x * nyz;
+  const int y = (int)(rr / g.n[2]), z = (int)(rr - (int64_t)y * g.n[2]);
+  const uint32_t ti = tiled_index(tiles_of(g.n), x, y, z);
+  if (kToLinear) dst[i] = src[ti];
+  else dst[ti] = src[i];
+}
+
+// Kernel variant: DMF_FUSE_VARIANT=<n> selects an instantiation for A/B measurements.
 static int fuse_variant() {
   static const int v = [] {
     const char* e = getenv("DMF_FUSE_VARIANT");
@@ -776,6 +510,8 @@ static int check_fuse(const dmf_volume* v, const dmf_camera* cam, int P, const d
   if (P <= 0 || P > 65535) return fail(DMF_ERR_INVALID, "pose count %d out of range [1,65535]", P);
   if (v->xdim > 2048 || v->ydim > 2048 || v->zdim > 2048)
     return fail(DMF_ERR_RANGE, "fusion grid is limited to 2048 cells per axis (fixed-point DDA)");
+  if (tiled_cells(v->geom().n) > (size_t)UINT32_MAX)
+    return fail(DMF_ERR_RANGE, "fusion grid is limited to 2^32 tiled counter cells");
   return DMF_OK;
 }
 
@@ -784,6 +520,45 @@ static int check_fuse(const dmf_volume* v, const dmf_camera* cam, int P, const d
 using namespace dmf;
 
 extern "C" {
+
+const char* dmf_fuse_kernel(void) {
+  switch (fuse_variant()) {
+    case 1: return "dmf::k_fuse_direct";
+    case 2: return "dmf::k_fuse_t<10, 1536>";
+    case 3: return "dmf::k_fuse_t<12, 2048>";
+    case 4: return "dmf::k_fuse_t<15, 2560>";
+    case 5: return "dmf::k_fuse_t<14, 1536>";
+    case 6: return "dmf::k_fuse_t<15, 3072>";
+    case 7: return "dmf::k_fuse_t<8, 1024>";
+    case 8: return "dmf::k_fuse_t<10, 1280>";
+    case 9: return "dmf::k_fuse_t<6, 768>";
+    case 10: return "dmf::k_fuse_t<10, 1536, false>";
+    case 11: return "dmf::k_fuse_t<12, 1536>";
+    case 12: return "dmf::k_fuse_t<14, 2048>";
+    default: return "dmf::k_fuse_t<10, 1280>";
+  }
+}
+
+int dmf_fuse_counter_cells(const dmf_volume* v, int64_t* n) {
+  DMF_API_BEGIN
+  if (!n) return fail(DMF_ERR_INVALID, "null argument");
+  DMF_TRY(require_constructed(v));
+  *n = (int64_t)tiled_cells(v->geom().n);
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_fuse_counters_to_linear_device(dmf_volume* v, const int32_t* d_tiled, int32_t* d_linear) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  if (!d_tiled || !d_linear) return fail(DMF_ERR_INVALID, "null device buffer");
+  const int64_t n = (int64_t)v->ncell;
+  hipLaunchKernelGGL(k_counter_layout<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream, v->geom(),
+                     d_tiled, d_linear, n);
+  DMF_LAUNCH_CHECK();
+  return DMF_OK;
+  DMF_API_END
+}
 
 int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth, const float* d_poses,
                           int32_t P, const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses,
@@ -794,52 +569,35 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
   PoseX* tab;
   DMF_TRY(pose_table(v, d_poses, P, true, &tab));
   const CamP cp = cam_params(cam);
-  const int tx = (cp.W + 15) / 16, ty = (cp.H + 15) / 16;
-  const dim3 grid((unsigned)(tx * ty), (unsigned)P);
   const Geom g = v->geom();
   unsigned long long* st = nullptr;
   if (d_stats) DMF_TRY(stats_begin(v, &st));
-#define DMF_FUSE_LAUNCH(K)                                                                                     \
-  hipLaunchKernelGGL(K, grid, dim3(256), 0, v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, tx, d_hits, \
+  const int pkx = (cp.W + 7) / 8, pky = (cp.H + 7) / 8;
+  const dim3 gridw((unsigned)(pkx * pky), (unsigned)P);
+#define DMF_FUSE_LAUNCH_T(K)                                                                                    \
+  hipLaunchKernelGGL(K, gridw, dim3(64), 0, v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, \
                      d_misses, st)
   switch (fuse_variant()) {
-    case 1: DMF_FUSE_LAUNCH(k_fuse_direct); break;
-    case 2: DMF_FUSE_LAUNCH((k_fuse_lds<8, 8192, 0>)); break;
-    case 3: DMF_FUSE_LAUNCH((k_fuse_lds<8, 8192, 1>)); break;
-    case 4: DMF_FUSE_LAUNCH((k_fuse_lds<8, 8192, 2>)); break;
-    case 9: DMF_FUSE_LAUNCH((k_fuse_lds<8, 8192, 1, true, false>)); break;
-    case 10: DMF_FUSE_LAUNCH((k_fuse_lds<8, 8192, 1, false, true>)); break;
-    case 11: DMF_FUSE_LAUNCH((k_fuse_lds<8, 8192, 1, true, true>)); break;
-    case 12: DMF_FUSE_LAUNCH((k_fuse_lds<8, 8192, 1, true, false, true>)); break;
-    case 13: DMF_FUSE_LAUNCH((k_fuse_lds<16, 8192, 1, true, false, true>)); break;
-    case 14: DMF_FUSE_LAUNCH((k_fuse_lds<24, 12288, 1, true, false, true>)); break;
-    case 15: DMF_FUSE_LAUNCH((k_fuse_lds<12, 8192, 1, true, false, true>)); break;
-    case 16: DMF_FUSE_LAUNCH((k_fuse_lean<8, 8192>)); break;
-    case 17: DMF_FUSE_LAUNCH((k_fuse_lean<12, 8192>)); break;
-    case 18: DMF_FUSE_LAUNCH((k_fuse_lean<16, 12288>)); break;
-    case 19: DMF_FUSE_LAUNCH((k_fuse_lean<6, 6144>)); break;
-    case 20: DMF_FUSE_LAUNCH((k_fuse_v2<16, 8192>)); break;
-    case 21: DMF_FUSE_LAUNCH((k_fuse_v2<12, 8192>)); break;
-    case 22: DMF_FUSE_LAUNCH((k_fuse_v2<16, 12288>)); break;
-    case 23: DMF_FUSE_LAUNCH((k_fuse_v2<8, 6144>)); break;
-    case 24: DMF_FUSE_LAUNCH((k_fuse_v2<8, 4096>)); break;
-    case 25: DMF_FUSE_LAUNCH((k_fuse_v2<6, 4096>)); break;
-    case 26: DMF_FUSE_LAUNCH((k_fuse_v2<10, 6144>)); break;
-    case 27: DMF_FUSE_LAUNCH((k_fuse_v2<6, 3072>)); break;
-    case 28: DMF_FUSE_LAUNCH((k_fuse_v2<8, 5120>)); break;
-    case 94: DMF_FUSE_LAUNCH((k_fuse_probe<0>)); break;
-    case 95: DMF_FUSE_LAUNCH((k_fuse_probe<1>)); break;
-    // timing-only ablations (wrong results): 91 no flush atomics, 92 no LDS atomics, 93 neither
-    case 91: DMF_FUSE_LAUNCH((k_fuse_lds<16, 8192, 1, true, false, true, 1>)); break;
-    case 92: DMF_FUSE_LAUNCH((k_fuse_lds<16, 8192, 1, true, false, true, 2>)); break;
-    case 93: DMF_FUSE_LAUNCH((k_fuse_lds<16, 8192, 1, true, false, true, 3>)); break;
-    case 5: DMF_FUSE_LAUNCH((k_fuse_lds<12, 8192, 2>)); break;
-    case 6: DMF_FUSE_LAUNCH((k_fuse_lds<6, 6144, 2>)); break;
-    case 7: DMF_FUSE_LAUNCH((k_fuse_lds<16, 12288, 2>)); break;
-    case 8: DMF_FUSE_LAUNCH((k_fuse_lds<10, 10240, 2>)); break;
-    default: DMF_FUSE_LAUNCH((k_fuse_v2<10, 6144>)); break;
+    case 1: {
+      const int tx = (cp.W + 15) / 16, ty = (cp.H + 15) / 16;
+      hipLaunchKernelGGL(k_fuse_direct, dim3((unsigned)(tx * ty), (unsigned)P), dim3(256), 0, v->stream, g, cp,
+                         d_depth, tab, prm->dmin_mm, prm->dmax_mm, tx, d_hits, d_misses, st);
+      break;
+    }
+    case 2: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1536>)); break;
+    case 3: DMF_FUSE_LAUNCH_T((k_fuse_t<12, 2048>)); break;
+    case 4: DMF_FUSE_LAUNCH_T((k_fuse_t<15, 2560>)); break;
+    case 5: DMF_FUSE_LAUNCH_T((k_fuse_t<14, 1536>)); break;
+    case 6: DMF_FUSE_LAUNCH_T((k_fuse_t<15, 3072>)); break;
+    case 7: DMF_FUSE_LAUNCH_T((k_fuse_t<8, 1024>)); break;
+    case 8: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1280>)); break;
+    case 9: DMF_FUSE_LAUNCH_T((k_fuse_t<6, 768>)); break;
+    case 10: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1536, false>)); break;
+    case 11: DMF_FUSE_LAUNCH_T((k_fuse_t<12, 1536>)); break;
+    case 12: DMF_FUSE_LAUNCH_T((k_fuse_t<14, 2048>)); break;
+    default: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1280>)); break;
   }
-#undef DMF_FUSE_LAUNCH
+#undef DMF_FUSE_LAUNCH_T
   DMF_LAUNCH_CHECK();
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
   DMF_LAUNCH_CHECK();
@@ -853,22 +611,39 @@ int dmf_fuse_depth(dmf_volume* v, const dmf_camera* cam, const uint16_t* depth, 
   DMF_TRY(check_fuse(v, cam, P, prm));
   if (!depth || !poses || !hits || !misses) return fail(DMF_ERR_INVALID, "null buffer");
   const size_t HW = (size_t)cam->height * cam->width;
-  void *dd, *dp, *dh, *dm, *ds;
+  const Geom g = v->geom();
+  const size_t nt = tiled_cells(g.n);
+  const int64_t n = (int64_t)v->ncell;
+  void *dd, *dp, *dh, *dm, *ds, *lin;
   DMF_TRY(scratch(v, kScHost1, sizeof(uint16_t) * HW * P, &dd));
   DMF_TRY(scratch(v, kScHost2, sizeof(float) * 12 * P, &dp));
-  DMF_TRY(scratch(v, kScOut0, sizeof(int32_t) * v->ncell, &dh));
-  DMF_TRY(scratch(v, kScOut1, sizeof(int32_t) * v->ncell, &dm));
+  DMF_TRY(scratch(v, kScOut0, sizeof(int32_t) * nt, &dh));
+  DMF_TRY(scratch(v, kScOut1, sizeof(int32_t) * nt, &dm));
   DMF_TRY(scratch(v, kScOut2, sizeof(uint64_t) * 8, &ds));
+  DMF_TRY(scratch(v, kScOut3, sizeof(int32_t) * v->ncell, &lin));
   DMF_HIP(hipMemcpyAsync(dd, depth, sizeof(uint16_t) * HW * P, hipMemcpyHostToDevice, v->stream));
   DMF_HIP(hipMemcpyAsync(dp, poses, sizeof(float) * 12 * P, hipMemcpyHostToDevice, v->stream));
-  DMF_HIP(hipMemcpyAsync(dh, hits, sizeof(int32_t) * v->ncell, hipMemcpyHostToDevice, v->stream));
-  DMF_HIP(hipMemcpyAsync(dm, misses, sizeof(int32_t) * v->ncell, hipMemcpyHostToDevice, v->stream));
+  DMF_HIP(hipMemsetAsync(dh, 0, sizeof(int32_t) * nt, v->stream));
+  DMF_HIP(hipMemsetAsync(dm, 0, sizeof(int32_t) * nt, v->stream));
+  const dim3 lg((unsigned)((n + 255) / 256));
+  // accumulate onto the caller's linear counters
+  DMF_HIP(hipMemcpyAsync(lin, hits, sizeof(int32_t) * v->ncell, hipMemcpyHostToDevice, v->stream));
+  hipLaunchKernelGGL(k_counter_layout<false>, lg, dim3(256), 0, v->stream, g, (const int32_t*)lin, (int32_t*)dh, n);
+  DMF_LAUNCH_CHECK();
+  DMF_HIP(hipMemcpyAsync(lin, misses, sizeof(int32_t) * v->ncell, hipMemcpyHostToDevice, v->stream));
+  hipLaunchKernelGGL(k_counter_layout<false>, lg, dim3(256), 0, v->stream, g, (const int32_t*)lin, (int32_t*)dm, n);
+  DMF_LAUNCH_CHECK();
   DMF_HIP(hipMemsetAsync(ds, 0, sizeof(uint64_t) * 8, v->stream));
   DMF_TRY(dmf_fuse_depth_device(v, cam, (const uint16_t*)dd, (const float*)dp, P, prm, (int32_t*)dh, (int32_t*)dm,
                                 (uint64_t*)ds));
   uint64_t st[4];
-  DMF_HIP(hipMemcpyAsync(hits, dh, sizeof(int32_t) * v->ncell, hipMemcpyDeviceToHost, v->stream));
-  DMF_HIP(hipMemcpyAsync(misses, dm, sizeof(int32_t) * v->ncell, hipMemcpyDeviceToHost, v->stream));
+  hipLaunchKernelGGL(k_counter_layout<true>, lg, dim3(256), 0, v->stream, g, (const int32_t*)dh, (int32_t*)lin, n);
+  DMF_LAUNCH_CHECK();
+  DMF_HIP(hipMemcpyAsync(hits, lin, sizeof(int32_t) * v->ncell, hipMemcpyDeviceToHost, v->stream));
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  hipLaunchKernelGGL(k_counter_layout<true>, lg, dim3(256), 0, v->stream, g, (const int32_t*)dm, (int32_t*)lin, n);
+  DMF_LAUNCH_CHECK();
+  DMF_HIP(hipMemcpyAsync(misses, lin, sizeof(int32_t) * v->ncell, hipMemcpyDeviceToHost, v->stream));
   DMF_HIP(hipMemcpyAsync(st, ds, sizeof(st), hipMemcpyDeviceToHost, v->stream));
   DMF_HIP(hipStreamSynchronize(v->stream));
   if (stats)
@@ -882,9 +657,9 @@ int dmf_fuse_finalize_device(dmf_volume* v, const int32_t* d_hits, const int32_t
   DMF_API_BEGIN
   DMF_TRY(require_constructed(v));
   if (!prm || !d_hits || !d_misses || !d_out) return fail(DMF_ERR_INVALID, "null argument");
-  const int64_t n = (int64_t)v->ncell;
-  const int64_t lanes = (n + 7) / 8;
-  hipLaunchKernelGGL(k_finalize, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, v->stream, d_hits, d_misses, n,
+  const Geom g = v->geom();
+  const int64_t lanes = (int64_t)g.n[0] * g.n[1] * ((g.n[2] + 3) / 4);
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, v->stream, g, d_hits, d_misses,
                      prm->l_hit, prm->l_miss, prm->l_min, prm->l_max, d_out);
   DMF_LAUNCH_CHECK();
   return DMF_OK;
@@ -896,12 +671,24 @@ int dmf_fuse_finalize(dmf_volume* v, const int32_t* hits, const int32_t* misses,
   DMF_API_BEGIN
   DMF_TRY(require_constructed(v));
   if (!prm || !hits || !misses || !out) return fail(DMF_ERR_INVALID, "null argument");
-  void *dh, *dm, *dout;
-  DMF_TRY(scratch(v, kScOut0, sizeof(int32_t) * v->ncell + 32, &dh));
-  DMF_TRY(scratch(v, kScOut1, sizeof(int32_t) * v->ncell + 32, &dm));
+  const Geom g = v->geom();
+  const size_t nt = tiled_cells(g.n);
+  const int64_t n = (int64_t)v->ncell;
+  void *dh, *dm, *dout, *lin;
+  DMF_TRY(scratch(v, kScOut0, sizeof(int32_t) * nt, &dh));
+  DMF_TRY(scratch(v, kScOut1, sizeof(int32_t) * nt, &dm));
   DMF_TRY(scratch(v, kScOut2, sizeof(int16_t) * v->ncell + 32, &dout));
-  DMF_HIP(hipMemcpyAsync(dh, hits, sizeof(int32_t) * v->ncell, hipMemcpyHostToDevice, v->stream));
-  DMF_HIP(hipMemcpyAsync(dm, misses, sizeof(int32_t) * v->ncell, hipMemcpyHostToDevice, v->stream));
+  DMF_TRY(scratch(v, kScOut3, sizeof(int32_t) * v->ncell, &lin));
+  const dim3 lg((unsigned)((n + 255) / 256));
+  DMF_HIP(hipMemsetAsync(dh, 0, sizeof(int32_t) * nt, v->stream));
+  DMF_HIP(hipMemsetAsync(dm, 0, sizeof(int32_t) * nt, v->stream));
+  DMF_HIP(hipMemcpyAsync(lin, hits, sizeof(int32_t) * v->ncell, hipMemcpyHostToDevice, v->stream));
+  hipLaunchKernelGGL(k_counter_layout<false>, lg, dim3(256), 0, v->stream, g, (const int32_t*)lin, (int32_t*)dh, n);
+  DMF_LAUNCH_CHECK();
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  DMF_HIP(hipMemcpyAsync(lin, misses, sizeof(int32_t) * v->ncell, hipMemcpyHostToDevice, v->stream));
+  hipLaunchKernelGGL(k_counter_layout<false>, lg, dim3(256), 0, v->stream, g, (const int32_t*)lin, (int32_t*)dm, n);
+  DMF_LAUNCH_CHECK();
   DMF_TRY(dmf_fuse_finalize_device(v, (const int32_t*)dh, (const int32_t*)dm, prm, (int16_t*)dout));
   DMF_HIP(hipMemcpyAsync(out, dout, sizeof(int16_t) * v->ncell, hipMemcpyDeviceToHost, v->stream));
   DMF_HIP(hipStreamSynchronize(v->stream));

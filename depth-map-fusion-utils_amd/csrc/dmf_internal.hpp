@@ -149,8 +149,13 @@ __device__ inline bool angle_ok(float nx, float ny, float nz, const float v[3], 
 }
 
 // ---------------------------------------------------------------- device state
+// Coarse occupancy: one bit per 8x8x8-cell brick (empty-space skipping in the marches).
+constexpr int kBrickShift = 3;
+
 struct DevVol {
   const uint32_t* occ;     // N-bit occupancy (x-major lin)
+  const uint32_t* brick;   // one bit per brick, x-major over nb[]
+  int nb[3];               // bricks per axis = ceil(n / 8)
   const int32_t* slot_of;  // N: slot or kEmpty
   const uint64_t* hash;    // V: occupied_cells_
   const int32_t* off;      // V+1: CSR offsets into nrm
@@ -180,6 +185,8 @@ struct dmf_volume {
   // device grid
   size_t ncell = 0;
   uint32_t* d_occ = nullptr;
+  uint32_t* d_brick = nullptr;  // one bit per 8^3 brick
+  int32_t nb[3] = {0, 0, 0};
   int32_t* d_slot_of = nullptr;
   // occupied list
   int64_t V = 0, Vcap = 0;

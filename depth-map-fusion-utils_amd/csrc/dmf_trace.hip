@@ -11,6 +11,7 @@
 //    (tests/CameraPathGen.cpp:128-156).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -30,25 +31,79 @@ __device__ inline void wave_add_u64(unsigned long long* dst, unsigned long long 
   if ((threadIdx.x & 63) == 0 && x) atomicAdd(dst, x);
 }
 
+// One sample of the reverse march: pt = c + (v * (float)depth) / 1000.0f per axis
+// (Eigen evaluates the double depth as float; RayTracingEngine.hpp:82, :173).
+__device__ inline void march_sample(const float cen[3], const float v[3], int depth, float p[3]) {
+  const float fd = (float)depth;
+  p[0] = cen[0] + ((v[0] * fd) / 1000.0f);
+  p[1] = cen[1] + ((v[1] * fd) / 1000.0f);
+  p[2] = cen[2] + ((v[2] * fd) / 1000.0f);
+}
+
 // The reverse 1 mm march (RayTracingEngine.hpp:81-103 / :172-200).  Returns true if
 // an occupied voxel other than the centroid's is hit before leaving the volume.
 // `capped` reports a march that never left (v == 0 or NaN: the reference loops
 // forever there) — treated as occluded and counted as a hazard.
-__device__ inline bool reverse_march(const Geom& g, const uint32_t* __restrict__ occ, const float cen[3],
-                                     const float v[3], int cx, int cy, int cz, int depth0, int max_steps,
-                                     int64_t& samples, bool& capped) {
+//
+// kSkip: empty-space skipping over 8^3 bricks, exact.  Each sample coordinate is a
+// monotone function of the step index (RN(v*fd), /1000 and + cen are monotone), so
+// if samples s and j both lie inside one empty brick and inside the volume, every
+// sample between them does too: none can hit an occupied cell, leave the volume or
+// be the centroid cell (an occupied cell).  j is estimated from the brick faces and
+// then verified by evaluating sample j exactly; on failure the march steps normally.
+template <bool kSkip>
+__device__ inline bool reverse_march(const Geom& g, const DevVol& vd, const float cen[3], const float v[3], int cx,
+                                     int cy, int cz, int depth0, int max_steps, int64_t& samples, bool& capped) {
   capped = false;
+  float rv[3] = {0.f, 0.f, 0.f};  // 1000 / v (estimate only)
+  if (kSkip) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) rv[a] = v[a] != 0.0f ? 1000.0f / v[a] : 0.0f;
+  }
+  uint32_t known_full = 0xffffffffu;  // last brick found occupied (or not skippable)
   for (int s = 0; s < max_steps; ++s) {
-    const float fd = (float)(depth0 + s);
-    const float px = cen[0] + ((v[0] * fd) / 1000.0f);
-    const float py = cen[1] + ((v[1] * fd) / 1000.0f);
-    const float pz = cen[2] + ((v[2] * fd) / 1000.0f);
+    float p[3];
+    march_sample(cen, v, depth0 + s, p);
     ++samples;
-    if (!valid_points(g, px, py, pz)) return false;
-    const int a = bin_axis(g, 0, px), b = bin_axis(g, 1, py), c = bin_axis(g, 2, pz);
+    if (!valid_points(g, p[0], p[1], p[2])) return false;
+    const int a = bin_axis(g, 0, p[0]), b = bin_axis(g, 1, p[1]), c = bin_axis(g, 2, p[2]);
     if (a == cx && b == cy && c == cz) continue;  // hash == centroid_hash
     if (!valid_coords(g, a, b, c)) return false;
-    if (occ_test(occ, lin_index(g, a, b, c))) return true;
+    if (occ_test(vd.occ, lin_index(g, a, b, c))) return true;
+    if (kSkip) {
+      const uint32_t bl = ((uint32_t)(a >> kBrickShift) * (uint32_t)vd.nb[1] + (uint32_t)(b >> kBrickShift)) *
+                              (uint32_t)vd.nb[2] + (uint32_t)(c >> kBrickShift);
+      if (bl == known_full) continue;
+      if (((vd.brick[bl >> 5] >> (bl & 31)) & 1u) == 0u) {
+        // last depth still inside the brick along each moving axis (estimate)
+        const int cell[3] = {a, b, c};
+        float fdmax = 3.0e38f;
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+          if (v[ax] == 0.0f) continue;
+          const int lo = (cell[ax] >> kBrickShift) << kBrickShift;
+          const int hi = min(lo + (1 << kBrickShift), g.n[ax]);  // exclusive
+          const float face = (float)(g.mn[ax] + (double)(v[ax] > 0.0f ? hi : lo) * g.dl[ax]);
+          fdmax = fminf(fdmax, (face - cen[ax]) * rv[ax]);
+        }
+        const float jf = floorf(fdmax) - (float)depth0 - 2.0f;
+        if (jf > (float)(s + 1) && jf < (float)max_steps) {
+          const int j = (int)jf;
+          float q[3];
+          march_sample(cen, v, depth0 + j, q);
+          ++samples;
+          if (valid_points(g, q[0], q[1], q[2])) {
+            const int qa = bin_axis(g, 0, q[0]), qb = bin_axis(g, 1, q[1]), qc = bin_axis(g, 2, q[2]);
+            if ((qa >> kBrickShift) == (a >> kBrickShift) && (qb >> kBrickShift) == (b >> kBrickShift) &&
+                (qc >> kBrickShift) == (c >> kBrickShift) && valid_coords(g, qa, qb, qc)) {
+              s = j;  // samples s+1 .. j lie inside the empty brick
+              continue;
+            }
+          }
+        }
+      }
+      known_full = bl;  // occupied brick, or estimate failed: step through it
+    }
   }
   capped = true;
   return true;
@@ -56,7 +111,7 @@ __device__ inline bool reverse_march(const Geom& g, const uint32_t* __restrict__
 
 // kEnum = false: reverseRayTraceFast over occupied_cells_ (element = slot)
 // kEnum = true : reverseRayTrace over the float-accumulated enumeration list
-template <bool kEnum>
+template <bool kEnum, bool kSkip>
 __global__ __launch_bounds__(256) void k_reverse(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses,
                                                  int64_t nelem, EnumList el, int depth0, int max_steps, float dstar,
                                                  int viz, int normal_test, uint64_t* __restrict__ vis_mask,
@@ -101,7 +156,7 @@ __global__ __launch_bounds__(256) void k_reverse(Geom g, DevVol vd, CamP cam, co
       float v[3];
       normalized(d, v);
       bool capped;
-      const bool collided = reverse_march(g, vd.occ, cen, v, bin_axis(g, 0, cen[0]), bin_axis(g, 1, cen[1]),
+      const bool collided = reverse_march<kSkip>(g, vd, cen, v, bin_axis(g, 0, cen[0]), bin_axis(g, 1, cen[1]),
                                           bin_axis(g, 2, cen[2]), depth0, max_steps, samples, capped);
       if (capped) atomicAdd(hazards, 1ull);
       if (!collided) {
@@ -172,12 +227,19 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
     EnumList el{v->d_axes, {v->nax[0], v->nax[1], v->nax[2]}, v->d_enum};
     const dim3 grid((unsigned)((nelem + 255) / 256), (unsigned)P);
     const int depth0 = enumerate ? 1 : 50;  // :81 vs :172
-    if (enumerate)
-      hipLaunchKernelGGL(k_reverse<true>, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab,
-                         nelem, el, depth0, max_march_steps(v), v->dstar, viz, 0, vis, good, words, st, found, hz);
-    else
-      hipLaunchKernelGGL(k_reverse<false>, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab,
-                         nelem, el, depth0, max_march_steps(v), v->dstar, viz, 1, vis, good, words, st, found, hz);
+    static const bool skip = [] {
+      const char* e = getenv("DMF_REVERSE_SKIP");
+      return !(e && e[0] == '0');
+    }();
+#define DMF_REV(E, S, NT)                                                                                        \
+  hipLaunchKernelGGL((k_reverse<E, S>), grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab, \
+                     nelem, el, depth0, max_march_steps(v), v->dstar, viz, NT, vis, good, words, st, found, hz)
+    if (enumerate) {
+      if (skip) DMF_REV(true, true, 0); else DMF_REV(true, false, 0);
+    } else {
+      if (skip) DMF_REV(false, true, 1); else DMF_REV(false, false, 1);
+    }
+#undef DMF_REV
     DMF_LAUNCH_CHECK();
   }
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 2));

@@ -63,6 +63,7 @@ SIGNATURES = {
     "dmf_device_count": (C.c_int, [_p]),
     "dmf_fuse_params_default": (None, [_p]),
     "dmf_angle_threshold": (C.c_int, [_p]),
+    "dmf_fuse_kernel": (C.c_char_p, []),
     "dmf_volume_create": (C.c_int, [_p, _i32]),
     "dmf_volume_destroy": (C.c_int, [_vp]),
     "dmf_volume_set_stream": (C.c_int, [_vp, _vp]),
@@ -98,6 +99,8 @@ SIGNATURES = {
     "dmf_fuse_depth_device": (C.c_int, [_vp, _p, _p, _p, _i32, _p, _p, _p, _p]),
     "dmf_fuse_finalize": (C.c_int, [_vp, _p, _p, _p, _p]),
     "dmf_fuse_finalize_device": (C.c_int, [_vp, _p, _p, _p, _p]),
+    "dmf_fuse_counter_cells": (C.c_int, [_vp, _p]),
+    "dmf_fuse_counters_to_linear_device": (C.c_int, [_vp, _p, _p]),
     "dmf_device_malloc": (C.c_int, [_vp, _p, C.c_size_t]),
     "dmf_device_free": (C.c_int, [_vp, _vp]),
     "dmf_memcpy_h2d": (C.c_int, [_vp, _vp, _p, C.c_size_t]),

@@ -91,6 +91,8 @@ void dmf_fuse_params_default(dmf_fuse_params* p);
  * dstar the smallest float whose host-libm acosf passes (the function the reference
  * binary calls).  Host-only; no GPU needed. */
 int dmf_angle_threshold(float* dstar);
+/* Diagnostic: name of the fusion kernel dmf_fuse_depth* launches (DMF_FUSE_VARIANT). */
+const char* dmf_fuse_kernel(void);
 
 /* ---- VoxelVolume  (Volume.hpp:50-255) ------------------------------------ */
 /* VoxelVolume::VoxelVolume()  Volume.hpp:63 — device = HIP device ordinal. */
@@ -186,16 +188,26 @@ int dmf_ray_trace_volume(dmf_volume* v, const dmf_camera* cam, const float* pose
 int dmf_will_collide(dmf_volume* v, const float* a, const float* b, int64_t n, uint8_t* collided);
 
 /* ---- 3D-DDA log-odds fusion (new capability) ------------------ */
-/* depth: P*H*W uint16 mm, poses: P*12.  hits/misses: xdim*ydim*zdim int32 counters,
- * ACCUMULATED (caller zeroes).  stats[3] += {cell updates, rays, hits}.
- * d_stats (device form, may be NULL): 8 uint64 counters += {cell updates, rays, hits, 0,
- * LDS aggregation rounds, direct-atomic rounds, flushed cell atomics, 0}. */
+/* Host form: depth P*H*W uint16 mm, poses P*12; hits/misses: xdim*ydim*zdim int32 in
+ * the reference's x-major voxel order, ACCUMULATED (caller zeroes).
+ * stats[3] += {cell updates, rays, hits}. */
 int dmf_fuse_depth(dmf_volume* v, const dmf_camera* cam, const uint16_t* depth, const float* poses,
                    int32_t P, const dmf_fuse_params* prm, int32_t* hits, int32_t* misses, int64_t* stats);
+/* Device form.  d_hits / d_misses are fusion counters in the TILED layout (2x2x4-cell
+ * tiles of 16 int32 = one 64-B line, tiles x-major) of
+ * dmf_fuse_counter_cells() elements each, ACCUMULATED; any elementwise sum of them
+ * (e.g. an all-reduce across ranks) stays valid.  d_stats (may be NULL): 8 uint64
+ * counters += {cell updates, rays, hits, 0, LDS rounds, direct rounds, flushed cell
+ * atomics, 0}. */
 int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth,
                           const float* d_poses, int32_t P, const dmf_fuse_params* prm, int32_t* d_hits,
                           int32_t* d_misses, uint64_t* d_stats);
-/* clamp(hits*l_hit + misses*l_miss, l_min, l_max) -> int16 log-odds grid. */
+/* Elements of one tiled counter array (>= xdim*ydim*zdim: dims padded to 2, 2, 4). */
+int dmf_fuse_counter_cells(const dmf_volume* v, int64_t* n);
+/* Tiled counters -> x-major int32 (xdim*ydim*zdim). */
+int dmf_fuse_counters_to_linear_device(dmf_volume* v, const int32_t* d_tiled, int32_t* d_linear);
+/* clamp(hits*l_hit + misses*l_miss, l_min, l_max) -> int16 log-odds grid, x-major.
+ * Host form: linear counters; device form: tiled counters. */
 int dmf_fuse_finalize(dmf_volume* v, const int32_t* hits, const int32_t* misses, const dmf_fuse_params* prm,
                       int16_t* logodds);
 int dmf_fuse_finalize_device(dmf_volume* v, const int32_t* d_hits, const int32_t* d_misses,

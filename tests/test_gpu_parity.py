@@ -126,6 +126,49 @@ def test_reverse_full_parity(oracle, engine, oeng):
     assert np.array_equal(a, c) and np.array_equal(b, d)
 
 
+def test_reverse_sparse_partial_bricks(oracle, engine, oeng):
+    """Empty-space skipping stress: a sparse scatter of occupied cells in a grid whose
+    dims are not multiples of the 8-cell brick and whose deltas are not powers of two;
+    cameras outside and inside the volume.  Lists and view/good flags must be exact."""
+    rng = np.random.default_rng(21)
+    bounds = (-0.45, 0.52, -0.4, 0.47, -0.33, 0.41)
+    dims = (91, 77, 61)
+    pts = rng.uniform([-0.44, -0.39, -0.32], [0.51, 0.46, 0.40], (400, 3)).astype(np.float32)
+    nn = rng.normal(size=(400, 3)).astype(np.float32)
+    nn /= np.linalg.norm(nn, axis=1, keepdims=True)
+    ov = oracle.Volume()
+    ov.setDimensions(*bounds)
+    ov.setVolumeSize(*dims)
+    ov.constructVolume()
+    ov.integratePointCloud(pts, nn)
+    import dmf_amd
+    gv = dmf_amd.VoxelVolume()
+    gv.setDimensions(*bounds)
+    gv.setVolumeSize(*dims)
+    gv.constructVolume()
+    gv.integratePointCloud(pts, nn)
+    assert np.array_equal(ov.occupied_cells_, gv.occupied_cells_)
+    from dmf_amd import scene
+    poses = np.concatenate([scene.fibonacci_poses(10, seed=5), scene.reference_style_poses(pts[:6], nn[:6], 150)])
+    found, lists = engine.reverseRayTraceFastBatch(gv, poses, viz=False)
+    total = 0
+    for i, T in enumerate(poses):
+        f, g = oeng.reverseRayTraceFast(ov, T, False)
+        assert f == bool(found[i]) and np.array_equal(g, lists[i]), f"pose {i}"
+        total += len(g)
+    assert total > 0
+    for T in poses[:5]:
+        f, g = oeng.reverseRayTraceFast(ov, T, True)
+        f2, g2 = engine.reverseRayTraceFast(gv, T, True)
+        assert f == f2 and np.array_equal(g, g2)
+    for T in poses[-3:]:
+        f, g = oeng.reverseRayTrace(ov, T, True)
+        f2, g2 = engine.reverseRayTrace(gv, T, True)
+        assert f == f2 and np.array_equal(g, g2)
+    a, b, c, d = _flags(ov, gv)
+    assert np.array_equal(a, c) and np.array_equal(b, d)
+
+
 @pytest.mark.parametrize("zstart,zdelta,stride", [(10, 10, 5), (5, 1, 10), (10, 3, 1)])
 def test_forward_first_hits(oracle, engine, oeng, zstart, zdelta, stride):
     ov = Hh.oracle_volume(oracle)
@@ -197,6 +240,67 @@ def test_fuse_parity(oracle, engine):
     assert np.array_equal(so, sg)
     assert np.array_equal(ho, hg) and np.array_equal(mo, mg)
     assert np.array_equal(oracle.fuse_finalize(ho, mo), engine.fuse_finalize(gv, hg, mg))
+
+
+def test_fuse_device_tiled_counters(oracle, engine, dmf):
+    """Device form: tiled counters (accumulated over two calls) -> linear via
+    dmf_fuse_counters_to_linear_device, and dmf_fuse_finalize_device from the tiled
+    counters, equal the oracle.  Odd dims exercise the padded tiles."""
+    import ctypes as C
+    from dmf_amd import _lib
+    poses, depth, _ = Hh.frames()
+    dims = (61, 50, 47)
+    ov = oracle.Volume()
+    ov.setDimensions(*Hh.BOUNDS)
+    ov.setVolumeSize(*dims)
+    ov.constructVolume()
+    ho, mo, _ = oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
+    gv = dmf.VoxelVolume()
+    gv.setDimensions(*Hh.BOUNDS)
+    gv.setVolumeSize(*dims)
+    gv.constructVolume()
+    L, h = gv._L, gv._h
+    ncell = int(np.prod(gv.dims))
+    nt = C.c_int64()
+    _lib.check(L.dmf_fuse_counter_cells(h, C.addressof(nt)))
+    nt = nt.value
+    assert nt >= ncell and nt % 16 == 0
+
+    def dmalloc(nbytes):
+        p = C.c_void_p()
+        _lib.check(L.dmf_device_malloc(h, C.addressof(p), nbytes))
+        return p.value
+
+    dd, dp, dh, dm, dl, dlo = (dmalloc(b) for b in (depth.nbytes, poses.astype(np.float32).nbytes, 4 * nt, 4 * nt,
+                                                     4 * ncell, 2 * ncell))
+    try:
+        d16 = np.ascontiguousarray(depth, np.uint16)
+        p32 = np.ascontiguousarray(poses, np.float32)
+        _lib.check(L.dmf_memcpy_h2d(h, dd, d16.ctypes.data, d16.nbytes))
+        _lib.check(L.dmf_memcpy_h2d(h, dp, p32.ctypes.data, p32.nbytes))
+        _lib.check(L.dmf_memset_device(h, dh, 0, 4 * nt))
+        _lib.check(L.dmf_memset_device(h, dm, 0, 4 * nt))
+        prm = dmf.FuseParams(dmin_mm=200, dmax_mm=1000)
+        cam = _lib.make_camera(K, H, W)
+        P = len(poses)
+        half = P // 2
+        _lib.check(L.dmf_fuse_depth_device(h, C.addressof(cam), dd, dp, half, C.addressof(prm), dh, dm, None))
+        _lib.check(L.dmf_fuse_depth_device(h, C.addressof(cam), dd + d16[0].nbytes * half, dp + 48 * half, P - half,
+                                           C.addressof(prm), dh, dm, None))
+        out = {}
+        for name, src in (("hits", dh), ("misses", dm)):
+            a = np.zeros(ncell, np.int32)
+            _lib.check(L.dmf_fuse_counters_to_linear_device(h, src, dl))
+            _lib.check(L.dmf_memcpy_d2h(h, a.ctypes.data, dl, 4 * ncell))
+            out[name] = a
+        assert np.array_equal(out["hits"], ho) and np.array_equal(out["misses"], mo)
+        lg = np.zeros(ncell, np.int16)
+        _lib.check(L.dmf_fuse_finalize_device(h, dh, dm, C.addressof(prm), dlo))
+        _lib.check(L.dmf_memcpy_d2h(h, lg.ctypes.data, dlo, 2 * ncell))
+        assert np.array_equal(lg, oracle.fuse_finalize(ho, mo))
+    finally:
+        for p in (dd, dp, dh, dm, dl, dlo):
+            L.dmf_device_free(h, p)
 
 
 def test_fuse_non_orthonormal_and_inside_cameras(oracle, engine):
