@@ -354,8 +354,15 @@ __global__ __launch_bounds__(64) void k_fuse_t(Geom g, CamP cam, const uint16_t*
       const int sgn = odd ? -1 : 1;
       int x = odd ? m0 : c0, y = odd ? m1 : c1, z = odd ? m2 : c2;
       const int gx = sgn * st0, gy = sgn * st1, gz = sgn * st2;
-      int sh = odd ? 2 * (nm - 2) : 0;
-      const int dsh = odd ? -2 : 2;
+      // Odd lanes replay backwards: bit-reverse the code word (field k -> 15 - k, and
+      // codes 1 <-> 2 swap their bits, so swap them back), then align the code of
+      // advance nm - 2 to field 0.  Field k then holds the k-th replayed advance.
+      uint32_t rc = codes;
+      if (odd) {
+        rc = __builtin_bitreverse32(codes);
+        rc = ((rc & 0x55555555u) << 1) | ((rc & 0xAAAAAAAAu) >> 1);
+        rc = nm >= 2 ? rc >> (2 * (17 - nm)) : 0u;
+      }
       if (ncell_box <= kBox) {
         ++nround_lds;
         // Next-step delta per axis: in-tile (x: 8, y: 4, z: 1) or, when the step leaves
@@ -371,17 +378,19 @@ __global__ __launch_bounds__(64) void k_fuse_t(Geom g, CamP cam, const uint16_t*
         const int tx_ = ix ^ jx, ty_ = iy ^ jy;
         int cur = ((((x - ax) >> 1) * tby + ((y - ay) >> 1)) * tbz + ((z - az) >> 2)) * 16 +
                   (((x & 1) << 3) | ((y & 1) << 2) | qz);
+        const bool full = __builtin_amdgcn_ballot_w64(nm != kS) == 0;  // every lane has kS misses
 #pragma unroll
         for (int k = 0; k < kS; ++k) {
-          if (k < nm) atomicAdd(&box[cur], 1);
-          const uint32_t cd = (codes >> (sh & 31)) & 3u;
-          const bool ax0 = cd == 0u, ax1 = cd == 1u, ax2 = cd == 2u;
-          cur += ax2 ? nzd : (ax1 ? ny : nx);
-          nx ^= ax0 ? tx_ : 0;
-          ny ^= ax1 ? ty_ : 0;
-          qz = ax2 ? ((qz + gz) & 3) : qz;
-          nzd = qz == fz ? jz : iz;
-          sh += dsh;
+          if (full || k < nm) atomicAdd(&box[cur], 1);
+          if (k + 1 < kS) {
+            const uint32_t cd = (rc >> (2 * k)) & 3u;
+            const bool ax0 = cd == 0u, ax1 = cd == 1u, ax2 = cd == 2u;
+            cur += ax2 ? nzd : (ax1 ? ny : nx);
+            nx ^= ax0 ? tx_ : 0;
+            ny ^= ax1 ? ty_ : 0;
+            qz = ax2 ? ((qz + gz) & 3) : qz;
+            nzd = qz == fz ? jz : iz;
+          }
         }
         __syncthreads();  // single-wave workgroup: orders the LDS adds before the flush
         // compact the non-zero cells (box order = tile order) into (index | count << 16)
@@ -396,17 +405,16 @@ __global__ __launch_bounds__(64) void k_fuse_t(Geom g, CamP cam, const uint16_t*
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + l;
             const uint64_t b = __builtin_amdgcn_ballot_w64(v[u] != 0);
-            if (v[u]) {
-              const int i = i0 + 64 * u + l;
-              box[i] = 0;
-              nzl[nnz + lane_prefix(b)] = (uint32_t)i | ((uint32_t)v[u] << 16);
-            }
+            if (i < nb) box[i] = 0;
+            if (v[u]) nzl[nnz + lane_prefix(b)] = (uint32_t)i | ((uint32_t)v[u] << 16);
             nnz += __builtin_popcountll(b);
           }
         }
         __syncthreads();
-        const float rtyz = 1.0f / (float)tyz, rtz = 1.0f / (float)tbz;
+        // approximate reciprocals suffice: small_div corrects the quotient by one
+        const float rtyz = __builtin_amdgcn_rcpf((float)tyz), rtz = __builtin_amdgcn_rcpf((float)tbz);
         const int tax = ax >> 1, tay = ay >> 1, taz = az >> 2;
         for (int e = l; e < nnz; e += 64) {
           const uint32_t en = nzl[e];
@@ -428,11 +436,10 @@ __global__ __launch_bounds__(64) void k_fuse_t(Geom g, CamP cam, const uint16_t*
 #pragma unroll
         for (int k = 0; k < kS; ++k) {
           if (k < nm) atomic_add_dev(&misses[tiled_index(tl, x, y, z)], 1);
-          const uint32_t cd = (codes >> (sh & 31)) & 3u;
+          const uint32_t cd = (rc >> (2 * k)) & 3u;
           x += cd == 0u ? gx : 0;
           y += cd == 1u ? gy : 0;
           z += cd == 2u ? gz : 0;
-          sh += dsh;
         }
       }
     }
@@ -524,18 +531,18 @@ extern "C" {
 const char* dmf_fuse_kernel(void) {
   switch (fuse_variant()) {
     case 1: return "dmf::k_fuse_direct";
-    case 2: return "dmf::k_fuse_t<10, 1536>";
-    case 3: return "dmf::k_fuse_t<12, 2048>";
-    case 4: return "dmf::k_fuse_t<15, 2560>";
-    case 5: return "dmf::k_fuse_t<14, 1536>";
-    case 6: return "dmf::k_fuse_t<15, 3072>";
-    case 7: return "dmf::k_fuse_t<8, 1024>";
-    case 8: return "dmf::k_fuse_t<10, 1280>";
-    case 9: return "dmf::k_fuse_t<6, 768>";
+    case 2: return "dmf::k_fuse_t<10, 1536, true>";
+    case 3: return "dmf::k_fuse_t<12, 2048, true>";
+    case 4: return "dmf::k_fuse_t<15, 2560, true>";
+    case 5: return "dmf::k_fuse_t<14, 1536, true>";
+    case 6: return "dmf::k_fuse_t<15, 3072, true>";
+    case 7: return "dmf::k_fuse_t<8, 1024, true>";
+    case 8: return "dmf::k_fuse_t<10, 1280, true>";
+    case 9: return "dmf::k_fuse_t<6, 768, true>";
     case 10: return "dmf::k_fuse_t<10, 1536, false>";
-    case 11: return "dmf::k_fuse_t<12, 1536>";
-    case 12: return "dmf::k_fuse_t<14, 2048>";
-    default: return "dmf::k_fuse_t<10, 1280>";
+    case 11: return "dmf::k_fuse_t<12, 1536, true>";
+    case 12: return "dmf::k_fuse_t<14, 2048, true>";
+    default: return "dmf::k_fuse_t<10, 1280, true>";
   }
 }
 
