@@ -495,6 +495,7 @@ static int integrate_impl(dmf_volume* v, const float* d_xyz, const float* d_nrm,
   v->npts = P0 + n;
   v->hazards += (int64_t)hz;
   v->enum_valid = false;
+  v->bdist_valid = false;
   // CSR over all points, stable in point order within each slot.
   const int64_t N = v->npts;
   void *keys, *vals;
@@ -572,6 +573,49 @@ static float angle_threshold() {
   return dstar;
 }
 
+
+// ---- brick distance field (empty-space skipping in the reverse march) ---------
+// d(b) = min over occupied bricks q of max_axis |b - q| (L-inf, in bricks), capped.
+// L-inf distance is separable: three 1-D passes d' = min_t max(|t|, d(b + t e_axis)).
+__global__ void k_bdist_init(const uint32_t* __restrict__ brick, int64_t nbr, uint8_t* __restrict__ d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nbr) d[i] = ((brick[i >> 5] >> (i & 31)) & 1u) ? 0 : kBrickDistCap;
+}
+__global__ void k_bdist_pass(int nbx, int nby, int nbz, int axis, const uint8_t* __restrict__ src,
+                             uint8_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nbr = (int64_t)nbx * nby * nbz;
+  if (i >= nbr) return;
+  const int z = (int)(i % nbz), y = (int)((i / nbz) % nby), x = (int)(i / ((int64_t)nbz * nby));
+  const int c = axis == 0 ? x : (axis == 1 ? y : z), n = axis == 0 ? nbx : (axis == 1 ? nby : nbz);
+  const int64_t stride = axis == 0 ? (int64_t)nby * nbz : (axis == 1 ? nbz : 1);
+  int best = src[i];
+  for (int t = 1; t < best && t < kBrickDistCap; ++t) {
+    if (c - t >= 0) best = min(best, max(t, (int)src[i - t * stride]));
+    if (c + t < n) best = min(best, max(t, (int)src[i + t * stride]));
+  }
+  dst[i] = (uint8_t)best;
+}
+
+int ensure_brick_dist(dmf_volume* v) {
+  if (v->bdist_valid) return DMF_OK;
+  const int64_t nbr = (int64_t)v->nb[0] * v->nb[1] * v->nb[2];
+  uint8_t* a = v->d_bdist;
+  uint8_t* b = v->d_bdist + nbr + 64;
+  const dim3 blk(256), grd((unsigned)((nbr + 255) / 256));
+  hipLaunchKernelGGL(k_bdist_init, grd, blk, 0, v->stream, v->d_brick, nbr, a);
+  DMF_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bdist_pass, grd, blk, 0, v->stream, v->nb[0], v->nb[1], v->nb[2], 2, a, b);
+  DMF_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bdist_pass, grd, blk, 0, v->stream, v->nb[0], v->nb[1], v->nb[2], 1, b, a);
+  DMF_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_bdist_pass, grd, blk, 0, v->stream, v->nb[0], v->nb[1], v->nb[2], 0, a, b);
+  DMF_LAUNCH_CHECK();
+  DMF_HIP(hipMemcpyAsync(a, b, (size_t)nbr, hipMemcpyDeviceToDevice, v->stream));
+  v->bdist_valid = true;
+  return DMF_OK;
+}
+
 }  // namespace dmf
 
 using namespace dmf;
@@ -588,29 +632,36 @@ dmf::Geom dmf_volume::geom() const {
     const bool p2 = (m == 0.5) && std::isfinite(dl[a]) && dl[a] > 0;
     g.inv[a] = p2 ? 1.0 / dl[a] : 0.0;
     if (!p2) g.pow2 = 0;
+    float lo = (float)mn[a], hi = (float)mx[a];
+    if (!((double)lo > mn[a])) lo = std::nextafter(lo, INFINITY);
+    if (!((double)hi < mx[a])) hi = std::nextafter(hi, -INFINITY);
+    g.vlo[a] = lo;
+    g.vhi[a] = hi;
   }
   return g;
 }
 
 dmf::DevVol dmf_volume::dev() const {
   DevVol d;
-  d.occ = d_occ; d.brick = d_brick; d.nb[0] = nb[0]; d.nb[1] = nb[1]; d.nb[2] = nb[2]; d.slot_of = d_slot_of; d.hash = d_hash; d.off = d_off; d.nrm = d_csr_nrm;
+  d.occ = d_occ; d.bdist = d_bdist;
+  d.brick = d_brick; d.nb[0] = nb[0]; d.nb[1] = nb[1]; d.nb[2] = nb[2]; d.slot_of = d_slot_of; d.hash = d_hash; d.off = d_off; d.nrm = d_csr_nrm;
   d.view = d_view; d.good = d_good; d.V = V;
   return d;
 }
 
 static void free_state(dmf_volume* v) {
   auto f = [&](void* p) { if (p) (void)hipFree(p); };
-  f(v->d_occ); f(v->d_brick); f(v->d_slot_of); f(v->d_hash); f(v->d_view); f(v->d_good);
+  f(v->d_occ); f(v->d_brick); f(v->d_bdist); f(v->d_slot_of); f(v->d_hash); f(v->d_view); f(v->d_good);
   f(v->d_pts); f(v->d_pnrm); f(v->d_pslot); f(v->d_off); f(v->d_csr_nrm); f(v->d_csr_pts);
   f(v->d_axes); f(v->d_enum);
   for (auto& s : v->scratch) f(s.first);
   v->scratch.clear();
-  v->d_occ = nullptr; v->d_brick = nullptr; v->d_slot_of = nullptr; v->d_hash = nullptr; v->d_view = nullptr; v->d_good = nullptr;
+  v->d_occ = nullptr; v->d_brick = nullptr; v->d_bdist = nullptr; v->bdist_valid = false; v->d_slot_of = nullptr; v->d_hash = nullptr; v->d_view = nullptr; v->d_good = nullptr;
   v->d_pts = nullptr; v->d_pnrm = nullptr; v->d_pslot = nullptr; v->d_off = nullptr; v->d_csr_nrm = nullptr;
   v->d_csr_pts = nullptr; v->d_axes = nullptr; v->d_enum = nullptr;
   v->V = v->Vcap = v->npts = v->pcap = v->nbinned = v->csr_cap = v->nenum = v->enum_cap = 0;
   v->enum_valid = false;
+  v->bdist_valid = false;
   v->constructed = false;
 }
 
@@ -750,6 +801,9 @@ int dmf_volume_construct(dmf_volume* v) {
   const size_t bwords = ((size_t)v->nb[0] * v->nb[1] * v->nb[2] + 31) / 32 + 1;
   DMF_HIP(hipMalloc((void**)&v->d_brick, sizeof(uint32_t) * bwords));
   DMF_HIP(hipMemsetAsync(v->d_brick, 0, sizeof(uint32_t) * bwords, v->stream));
+  // brick distance field + one scratch copy for the separable passes
+  DMF_HIP(hipMalloc((void**)&v->d_bdist, 2 * ((size_t)v->nb[0] * v->nb[1] * v->nb[2] + 64)));
+  v->bdist_valid = false;
   DMF_HIP(hipMalloc((void**)&v->d_slot_of, sizeof(int32_t) * v->ncell));
   DMF_HIP(hipMemsetD32Async((hipDeviceptr_t)v->d_slot_of, kEmpty, v->ncell, v->stream));
   DMF_HIP(hipMalloc((void**)&v->d_off, sizeof(int32_t)));

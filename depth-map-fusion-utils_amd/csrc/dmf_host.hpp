@@ -70,6 +70,7 @@ int check_camera(const dmf_camera* c);
 
 // Lazily (re)build the float-accumulated enumeration list (reverseRayTrace / rayTraceVolume).
 int ensure_enumeration(dmf_volume* v);
+int ensure_brick_dist(dmf_volume* v);
 
 // Device-wide helpers implemented with rocPRIM in dmf_core.hip.
 int exclusive_scan_i64(dmf_volume* v, const int64_t* in, int64_t* out, size_t n);

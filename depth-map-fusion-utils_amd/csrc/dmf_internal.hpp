@@ -32,6 +32,8 @@ struct Geom {
   double inv[3];  // 1/delta when delta is a power of two (then x*inv == x/delta exactly)
   int pow2;       // all three deltas are powers of two
   int n[3];       // xdim_, ydim_, zdim_ after constructVolume truncation
+  float vlo[3];   // smallest float x with (double)x > mn  (validPoints as float compares)
+  float vhi[3];   // largest float x with (double)x < mx
 };
 
 // Camera.hpp:26 fx=K[0], cx=K[2], fy=K[4], cy=K[5] promoted to double.
@@ -151,9 +153,11 @@ __device__ inline bool angle_ok(float nx, float ny, float nz, const float v[3], 
 // ---------------------------------------------------------------- device state
 // Coarse occupancy: one bit per 8x8x8-cell brick (empty-space skipping in the marches).
 constexpr int kBrickShift = 3;
+constexpr int kBrickDistCap = 15;  // brick distance field saturates here
 
 struct DevVol {
   const uint32_t* occ;     // N-bit occupancy (x-major lin)
+  const uint8_t* bdist;    // per brick: L-inf distance in bricks to the nearest occupied brick (0 = occupied), capped
   const uint32_t* brick;   // one bit per brick, x-major over nb[]
   int nb[3];               // bricks per axis = ceil(n / 8)
   const int32_t* slot_of;  // N: slot or kEmpty
@@ -186,6 +190,8 @@ struct dmf_volume {
   size_t ncell = 0;
   uint32_t* d_occ = nullptr;
   uint32_t* d_brick = nullptr;  // one bit per 8^3 brick
+  uint8_t* d_bdist = nullptr;   // brick distance field (DevVol::bdist), valid when bdist_valid
+  bool bdist_valid = false;
   int32_t nb[3] = {0, 0, 0};
   int32_t* d_slot_of = nullptr;
   // occupied list

@@ -193,6 +193,228 @@ __global__ __launch_bounds__(256) void k_reverse(Geom g, DevVol vd, CamP cam, co
   }
 }
 
+// ---- persistent reverse visibility (work queue per wave) -----------------------
+// Same per-(voxel, pose) semantics as k_reverse<kEnum, true>; the march lengths of
+// neighbouring voxels differ by orders of magnitude (outside the frustum: 0 samples,
+// occluded: tens, visible: hundreds), so one lane per voxel leaves most lanes of a
+// wave idle.  Here each wave owns kItems consecutive voxels of one pose and keeps
+// its lanes busy: a lane that finishes records its result bits in LDS and takes the
+// next voxel; refills run when at least kRefill lanes are idle (the setup is
+// divergent code, so it is batched).
+struct RevLane {
+  float cen[3], v[3], rv[3];
+  int cx, cy, cz;
+  int s;                // next sample index
+  uint32_t known_full;  // last brick found occupied / not skippable
+  int item;             // local item index, -1 = idle
+  int32_t slot;
+  float tz;             // camera-frame z of the centroid (z-range test)
+  uint32_t occi, occw;  // cached occupancy word
+};
+
+__device__ inline bool valid_points_f(const Geom& g, const float p[3]) {
+  return p[0] >= g.vlo[0] && p[0] <= g.vhi[0] && p[1] >= g.vlo[1] && p[1] <= g.vhi[1] && p[2] >= g.vlo[2] &&
+         p[2] <= g.vhi[2];
+}
+
+// One sample of the reverse march (RayTracingEngine.hpp:172-200): 0 = continue,
+// 1 = collided, 2 = left the volume (visible), 3 = capped (collided, hazard).
+//
+// validPoints (x > min and x < max in double) is the exact float test
+// vlo <= x <= vhi.  Empty-space skipping: the brick distance field d gives an empty
+// cube of bricks of radius d - 1 around the current brick; every sample coordinate is
+// a monotone function of the step index, so if samples s and j both lie in that cube
+// (and inside the volume) so does every sample between them — none can hit an
+// occupied cell, the centroid's cell (occupied) or leave the volume.  j is estimated
+// from the cube faces and verified by evaluating sample j exactly.
+__device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int depth0, int max_steps,
+                               int64_t& samples) {
+  if (L.s >= max_steps) return 3;
+  float p[3];
+  march_sample(L.cen, L.v, depth0 + L.s, p);
+  ++samples;
+  if (!valid_points_f(g, p)) return 2;
+  const int a = bin_axis(g, 0, p[0]), b = bin_axis(g, 1, p[1]), c = bin_axis(g, 2, p[2]);
+  if (a == L.cx && b == L.cy && c == L.cz) { ++L.s; return 0; }
+  if (!valid_coords(g, a, b, c)) return 2;
+  const uint32_t lin = lin_index(g, a, b, c);
+  if ((lin >> 5) != L.occi) { L.occi = lin >> 5; L.occw = vd.occ[L.occi]; }
+  if ((L.occw >> (lin & 31)) & 1u) return 1;
+  const int ba = a >> kBrickShift, bb = b >> kBrickShift, bc = c >> kBrickShift;
+  const uint32_t bl = ((uint32_t)ba * (uint32_t)vd.nb[1] + (uint32_t)bb) * (uint32_t)vd.nb[2] + (uint32_t)bc;
+  if (bl != L.known_full) {
+    const int d = vd.bdist[bl];
+    if (d > 0) {
+      const int R = d - 1;  // bricks within R of this one are empty
+      const int bx[3] = {ba, bb, bc};
+      int clo[3], chi[3];   // cell range of the empty cube, [clo, chi)
+      float fdmax = 3.0e38f;
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        clo[ax] = max(bx[ax] - R, 0) << kBrickShift;
+        chi[ax] = min((bx[ax] + R + 1) << kBrickShift, g.n[ax]);
+        if (L.v[ax] == 0.0f) continue;
+        const float face = (float)(g.mn[ax] + (double)(L.v[ax] > 0.0f ? chi[ax] : clo[ax]) * g.dl[ax]);
+        fdmax = fminf(fdmax, (face - L.cen[ax]) * L.rv[ax]);
+      }
+      const float jf = floorf(fdmax) - (float)depth0 - 2.0f;
+      if (jf > (float)(L.s + 1) && jf < (float)max_steps) {
+        const int j = (int)jf;
+        float q[3];
+        march_sample(L.cen, L.v, depth0 + j, q);
+        ++samples;
+        if (valid_points_f(g, q)) {
+          const int qa = bin_axis(g, 0, q[0]), qb = bin_axis(g, 1, q[1]), qc = bin_axis(g, 2, q[2]);
+          if (qa >= clo[0] && qa < chi[0] && qb >= clo[1] && qb < chi[1] && qc >= clo[2] && qc < chi[2]) {
+            L.s = j + 1;  // samples s+1 .. j lie inside the empty cube
+            return 0;
+          }
+        }
+      }
+    }
+    L.known_full = bl;  // occupied brick, or the jump failed: step through it
+  }
+  ++L.s;
+  return 0;
+}
+
+template <bool kEnum, int kItems, int kRefill, int kBurst>
+__global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses,
+                                                   int64_t nelem, EnumList el, int depth0, int max_steps, float dstar,
+                                                   int viz, int normal_test, uint64_t* __restrict__ vis_mask,
+                                                   uint64_t* __restrict__ good_mask, int64_t words,
+                                                   unsigned long long* __restrict__ stats, int* __restrict__ found,
+                                                   unsigned long long* __restrict__ hazards) {
+  static_assert(kItems % 64 == 0, "whole mask words per wave");
+  stats = stat_slot(stats);
+  __shared__ uint32_t lvis[4][kItems / 32], lgood[4][kItems / 32];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int i = l; i < kItems / 32; i += 64) { lvis[w][i] = 0; lgood[w][i] = 0; }
+  const int p = blockIdx.y;
+  const int64_t base = ((int64_t)blockIdx.x * 4 + w) * kItems;
+  const int nitems = (int)max<int64_t>(0, min<int64_t>(kItems, nelem - base));
+  const PoseX& T = poses[p];
+  int64_t samples = 0, rays = 0;
+  unsigned long long ncap = 0;
+  bool any_vis = false;
+  RevLane L;
+  L.item = -1;
+  int next = 0;  // wave-uniform queue head
+  __syncthreads();
+  while (true) {
+    const uint64_t idle = __builtin_amdgcn_ballot_w64(L.item < 0);
+    const int nidle = __builtin_popcountll(idle);
+    if (next < nitems && (nidle >= kRefill || nidle == 64)) {
+      if (L.item < 0) {
+        const int it = next + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        if (it < nitems) {
+          const int64_t e = base + it;
+          ++rays;
+          float cen[3];
+          int32_t slot;
+          if (!kEnum) {
+            slot = (int32_t)e;
+            const uint64_t h = vd.hash[e];
+            const int xid = (int)(h >> 40), yid = (int)((h >> 20) & 0xFFFFF), zid = (int)(h & 0xFFFFF);
+            const float x = (float)((double)xid * g.dl[0] + g.mn[0]);
+            const float y = (float)((double)yid * g.dl[1] + g.mn[1]);
+            const float z = (float)((double)zid * g.dl[2] + g.mn[2]);
+            cen[0] = (float)((double)x + g.hdl[0]);
+            cen[1] = (float)((double)y + g.hdl[1]);
+            cen[2] = (float)((double)z + g.hdl[2]);
+          } else {
+            const uint32_t en = el.list[e];
+            const uint32_t nyz = (uint32_t)el.nax[1] * (uint32_t)el.nax[2];
+            const uint32_t i = en / nyz, j = (en / el.nax[2]) % el.nax[1], k = en % el.nax[2];
+            const float x = el.axes[i], y = el.axes[el.nax[0] + j], z = el.axes[el.nax[0] + el.nax[1] + k];
+            slot = vd.slot_of[lin_index(g, bin_axis(g, 0, x), bin_axis(g, 1, y), bin_axis(g, 2, z))];
+            cen[0] = (float)((double)x + g.hdl[0]);
+            cen[1] = (float)((double)y + g.hdl[1]);
+            cen[2] = (float)((double)z + g.hdl[2]);
+          }
+          float t[3];
+          xform(T.i, cen[0], cen[1], cen[2], t);
+          int r, c;
+          if (deproject_valid(cam, t[0], t[1], t[2], r, c)) {
+            const float d[3] = {T.f[3] - cen[0], T.f[7] - cen[1], T.f[11] - cen[2]};
+            normalized(d, L.v);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+              L.cen[a] = cen[a];
+              L.rv[a] = L.v[a] != 0.0f ? 1000.0f / L.v[a] : 0.0f;
+            }
+            L.cx = bin_axis(g, 0, cen[0]);
+            L.cy = bin_axis(g, 1, cen[1]);
+            L.cz = bin_axis(g, 2, cen[2]);
+            L.s = 0;
+            L.known_full = 0xffffffffu;
+            L.occi = 0xffffffffu;
+            L.item = it;
+            L.slot = slot;
+            L.tz = t[2];
+          }
+        }
+      }
+      next += nidle;
+    }
+    if (__builtin_amdgcn_ballot_w64(L.item >= 0) == 0) {
+      if (next >= nitems) break;
+      continue;
+    }
+    // march: up to kBurst samples per busy lane
+    int st = 0;
+#pragma unroll 1
+    for (int b = 0; b < kBurst; ++b) {
+      if (L.item >= 0 && st == 0) st = rev_step(g, vd, L, depth0, max_steps, samples);
+      if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
+    }
+    if (L.item >= 0 && st != 0) {
+      if (st == 3) ++ncap;
+      if (st == 2) {
+        any_vis = true;
+        bool good = false;
+        const double zz = (double)L.tz;
+        if (zz >= kZMin && zz <= kZMax) {
+          if (normal_test) {
+            const int32_t a = vd.off[L.slot], b = vd.off[L.slot + 1];
+            for (int32_t j = a; j < b; ++j) {
+              const float4 n = vd.nrm[j];
+              if (n.w != 0.0f && angle_ok(n.x, n.y, n.z, L.v, dstar)) { good = true; break; }
+            }
+          } else {
+            good = true;
+          }
+        }
+        atomicOr(&lvis[w][L.item >> 5], 1u << (L.item & 31));
+        if (good) atomicOr(&lgood[w][L.item >> 5], 1u << (L.item & 31));
+        if (viz) {
+          vd.view[L.slot] = 1;
+          if (good) vd.good[L.slot] = 1;
+        }
+      }
+      L.item = -1;
+    }
+  }
+  __syncthreads();
+  const int64_t w0 = base >> 6;
+  for (int i = l; i < kItems / 64; i += 64) {
+    if (w0 + i < words) {
+      const uint64_t vb = (uint64_t)lvis[w][2 * i] | ((uint64_t)lvis[w][2 * i + 1] << 32);
+      const uint64_t gb = (uint64_t)lgood[w][2 * i] | ((uint64_t)lgood[w][2 * i + 1] << 32);
+      if (vis_mask) vis_mask[(int64_t)p * words + w0 + i] = vb;
+      if (good_mask) good_mask[(int64_t)p * words + w0 + i] = gb;
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(any_vis) != 0 && l == 0) atomicOr(&found[p], 1);
+  for (int o = 32; o > 0; o >>= 1) ncap += __shfl_down(ncap, o, 64);
+  if (l == 0 && ncap) atomicAdd(hazards, ncap);
+  if (stats) {
+    wave_add_u64(&stats[0], (unsigned long long)samples);
+    wave_add_u64(&stats[1], (unsigned long long)rays);
+  }
+}
+
 static int max_march_steps(const dmf_volume* v) {
   const double dx = v->xmax - v->xmin, dy = v->ymax - v->ymin, dz = v->zmax - v->zmin;
   const double diag_mm = std::sqrt(dx * dx + dy * dy + dz * dz) * 1000.0;
@@ -227,19 +449,43 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
     EnumList el{v->d_axes, {v->nax[0], v->nax[1], v->nax[2]}, v->d_enum};
     const dim3 grid((unsigned)((nelem + 255) / 256), (unsigned)P);
     const int depth0 = enumerate ? 1 : 50;  // :81 vs :172
-    static const bool skip = [] {
-      const char* e = getenv("DMF_REVERSE_SKIP");
-      return !(e && e[0] == '0');
+    static const int rev_kernel = [] {
+      const char* e = getenv("DMF_REVERSE_KERNEL");  // 0 plain, 1 plain + brick skip, >= 2 queue + distance field (2 = default)
+      return e ? atoi(e) : 2;
     }();
 #define DMF_REV(E, S, NT)                                                                                        \
   hipLaunchKernelGGL((k_reverse<E, S>), grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab, \
                      nelem, el, depth0, max_march_steps(v), v->dstar, viz, NT, vis, good, words, st, found, hz)
-    if (enumerate) {
-      if (skip) DMF_REV(true, true, 0); else DMF_REV(true, false, 0);
+#define DMF_REVQ(E, NT)                                                                                           \
+  hipLaunchKernelGGL((k_reverse_q<E, kRevItems, 8, 8>), gridq, dim3(256), 0, v->stream, v->geom(), v->dev(),       \
+                     cam_params(cam), tab, nelem, el, depth0, max_march_steps(v), v->dstar, viz, NT, vis, good, words, \
+                     st, found, hz)
+#define DMF_REVQX(E, NT, IT, RF, BU)                                                                              \
+  hipLaunchKernelGGL((k_reverse_q<E, IT, RF, BU>), dim3((unsigned)((nelem + 4 * IT - 1) / (4 * IT)), (unsigned)P),       \
+                     dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab, nelem, el, depth0,             \
+                     max_march_steps(v), v->dstar, viz, NT, vis, good, words, st, found, hz)
+    constexpr int kRevItems = 512;
+    const dim3 gridq((unsigned)((nelem + 4 * kRevItems - 1) / (4 * kRevItems)), (unsigned)P);
+    if (rev_kernel >= 2) {
+      DMF_TRY(ensure_brick_dist(v));
+      // the queue kernel writes every mask word it owns; words past the last wave stay 0
+      switch (rev_kernel) {
+        case 3: if (enumerate) DMF_REVQX(true, 0, 512, 32, 8); else DMF_REVQX(false, 1, 512, 32, 8); break;
+        case 4: if (enumerate) DMF_REVQX(true, 0, 512, 16, 8); else DMF_REVQX(false, 1, 512, 16, 8); break;
+        case 5: if (enumerate) DMF_REVQX(true, 0, 512, 16, 16); else DMF_REVQX(false, 1, 512, 16, 16); break;
+        case 6: if (enumerate) DMF_REVQX(true, 0, 1024, 16, 8); else DMF_REVQX(false, 1, 1024, 16, 8); break;
+        case 7: if (enumerate) DMF_REVQX(true, 0, 256, 16, 4); else DMF_REVQX(false, 1, 256, 16, 4); break;
+        case 8: if (enumerate) DMF_REVQX(true, 0, 512, 24, 4); else DMF_REVQX(false, 1, 512, 24, 4); break;
+        default: if (enumerate) DMF_REVQ(true, 0); else DMF_REVQ(false, 1); break;
+      }
+    } else if (enumerate) {
+      if (rev_kernel == 1) DMF_REV(true, true, 0); else DMF_REV(true, false, 0);
     } else {
-      if (skip) DMF_REV(false, true, 1); else DMF_REV(false, false, 1);
+      if (rev_kernel == 1) DMF_REV(false, true, 1); else DMF_REV(false, false, 1);
     }
 #undef DMF_REV
+#undef DMF_REVQ
+#undef DMF_REVQX
     DMF_LAUNCH_CHECK();
   }
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 2));
