@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "Algorithms.hpp"
 #include "Camera.hpp"
 #include "RayTracingEngine.hpp"
 #include "Volume.hpp"
@@ -101,12 +102,22 @@ int main(int argc, char** argv) {
   for (auto h : res.second) cout << " " << h;
   cout << "\n";
   // tests/SetCover.cpp:218-240 visibility loop (viz=false, sorted for set_difference)
+  vector<vector<unsigned long long int>> regions_covered;
   for (size_t i = 0; i < camera_locations.size(); i++) {
     vector<unsigned long long int> good_points;
     bool found;
     tie(found, good_points) = engine.reverseRayTraceFast(volume, camera_locations[i], false);
     sort(good_points.begin(), good_points.end());
     cout << "Sizes: " << good_points.size() << "\n";
+    regions_covered.push_back(good_points);
   }
+  // tests/SetCover.cpp:236-239 + include/Algorithms.hpp:38-86
+  auto cameras_selected = setCover(engine, volume, camera_locations, resolution_single_dimension);
+  auto again = Algorithms::greedySetCover(volume, regions_covered);
+  cout << "selected";
+  for (auto s : cameras_selected) cout << " " << s;
+  cout << "\nselected_from_sets";
+  for (auto s : again) cout << " " << s;
+  cout << "\n";
   return 0;
 }

@@ -415,6 +415,113 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
   }
 }
 
+// ---- greedy set cover over per-pose good bitmasks (Algorithms.hpp:38-86) ---------
+// The reference scans the remaining set ids in increasing order and keeps the
+// strictly largest |set \ covered|; with sets as bitmasks over occupied slots that
+// difference size is popcount(good[p] & ~covered).  One iteration = gain, pick,
+// merge; every kernel returns at once after the stop condition.
+struct CoverCtl {
+  int done;
+  int sel;
+  int nsel;
+};
+
+__global__ __launch_bounds__(256) void k_cover_gain(const uint64_t* __restrict__ masks, int64_t words,
+                                                    const uint64_t* __restrict__ covered,
+                                                    const uint8_t* __restrict__ removed,
+                                                    unsigned long long* __restrict__ gain,
+                                                    const CoverCtl* __restrict__ ctl) {
+  if (ctl->done) return;
+  const int p = blockIdx.x;
+  if (removed[p]) {
+    if (threadIdx.x == 0) gain[p] = 0;
+    return;
+  }
+  const uint64_t* m = masks + (int64_t)p * words;
+  unsigned long long c = 0;
+  for (int64_t w = threadIdx.x; w < words; w += blockDim.x) c += __popcll(m[w] & ~covered[w]);
+  __shared__ unsigned long long part[4];
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) gain[p] = part[0] + part[1] + part[2] + part[3];
+}
+
+__global__ __launch_bounds__(256) void k_cover_pick(const unsigned long long* __restrict__ gain, int P, int min_gain,
+                                                    uint8_t* __restrict__ removed, int32_t* __restrict__ selected,
+                                                    CoverCtl* __restrict__ ctl) {
+  if (ctl->done) return;
+  // argmax with ties to the smallest index: key = gain << 32 | (2^32 - 1 - p)
+  unsigned long long best = 0;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const unsigned long long k = (gain[p] << 32) | (unsigned long long)(0xffffffffu - (uint32_t)p);
+    best = k > best ? k : best;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long t = __shfl_down(best, o, 64);
+    best = t > best ? t : best;
+  }
+  __shared__ unsigned long long part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 4; ++i) best = part[i] > best ? part[i] : best;
+    const unsigned long long g = best >> 32;
+    if (g == 0 || g < (unsigned long long)min_gain) {  // selected == -1, or max_points < 5
+      ctl->done = 1;
+    } else {
+      const int p = (int)(0xffffffffu - (uint32_t)(best & 0xffffffffu));
+      ctl->sel = p;
+      selected[ctl->nsel++] = p;
+      removed[p] = 1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cover_merge(const uint64_t* __restrict__ masks, int64_t words,
+                                                     uint64_t* __restrict__ covered, const CoverCtl* __restrict__ ctl) {
+  if (ctl->done) return;
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < words) covered[w] |= masks[(int64_t)ctl->sel * words + w];
+}
+
+static int greedy_cover(dmf_volume* v, const uint64_t* d_masks, int P, int64_t words, int min_gain,
+                        int32_t* selected, int32_t* nselected) {
+  if (P <= 0) { *nselected = 0; return DMF_OK; }
+  void *cov, *aux;
+  const size_t cov_bytes = sizeof(uint64_t) * (size_t)std::max<int64_t>(words, 1);
+  DMF_TRY(scratch(v, kScTmp, cov_bytes, &cov));
+  const size_t gain_off = 64, rem_off = gain_off + sizeof(unsigned long long) * P,
+               sel_off = rem_off + ((size_t)P + 7) / 8 * 8;
+  DMF_TRY(scratch(v, kScCount, sel_off + sizeof(int32_t) * P, &aux));
+  CoverCtl* ctl = (CoverCtl*)aux;
+  unsigned long long* gain = (unsigned long long*)((char*)aux + gain_off);
+  uint8_t* removed = (uint8_t*)aux + rem_off;
+  int32_t* sel = (int32_t*)((char*)aux + sel_off);
+  DMF_HIP(hipMemsetAsync(cov, 0, cov_bytes, v->stream));
+  DMF_HIP(hipMemsetAsync(aux, 0, sel_off, v->stream));
+  const unsigned mb = (unsigned)((words + 255) / 256);
+  for (int it = 0; it < P; it += 8) {
+    for (int k = it; k < std::min(P, it + 8); ++k) {
+      hipLaunchKernelGGL(k_cover_gain, dim3((unsigned)P), dim3(256), 0, v->stream, d_masks, words,
+                         (const uint64_t*)cov, removed, gain, ctl);
+      hipLaunchKernelGGL(k_cover_pick, dim3(1), dim3(256), 0, v->stream, gain, P, min_gain, removed, sel, ctl);
+      if (mb) hipLaunchKernelGGL(k_cover_merge, dim3(mb), dim3(256), 0, v->stream, d_masks, words, (uint64_t*)cov, ctl);
+    }
+    DMF_LAUNCH_CHECK();
+    CoverCtl h;
+    DMF_HIP(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, v->stream));
+    DMF_HIP(hipStreamSynchronize(v->stream));
+    if (h.done) break;
+  }
+  CoverCtl h;
+  DMF_HIP(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, v->stream));
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  if (h.nsel) DMF_HIP(hipMemcpy(selected, sel, sizeof(int32_t) * h.nsel, hipMemcpyDeviceToHost));
+  *nselected = h.nsel;
+  return DMF_OK;
+}
+
 static int max_march_steps(const dmf_volume* v) {
   const double dx = v->xmax - v->xmin, dy = v->ymax - v->ymin, dz = v->zmax - v->zmin;
   const double diag_mm = std::sqrt(dx * dx + dy * dy + dz * dz) * 1000.0;
@@ -835,6 +942,27 @@ int dmf_reverse_visibility_device(dmf_volume* v, const dmf_camera* cam, const fl
     if (d_good) DMF_HIP(hipMemcpyAsync(d_good, good, bytes, hipMemcpyDeviceToDevice, v->stream));
   }
   return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_greedy_set_cover_masks_device(dmf_volume* v, const uint64_t* d_masks, int32_t P, int64_t words,
+                                      int32_t min_gain, int32_t* selected, int32_t* nselected) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  if (!selected || !nselected || (P > 0 && !d_masks)) return fail(DMF_ERR_INVALID, "null argument");
+  if (P < 0 || P > 65535 || words < 0) return fail(DMF_ERR_INVALID, "bad set count / width");
+  return greedy_cover(v, d_masks, P, words, min_gain, selected, nselected);
+  DMF_API_END
+}
+
+int dmf_greedy_set_cover(dmf_volume* v, const dmf_camera* cam, const float* poses, int32_t P, int32_t min_gain,
+                         int32_t* selected, int32_t* nselected) {
+  DMF_API_BEGIN
+  if (!poses || !selected || !nselected) return fail(DMF_ERR_INVALID, "null argument");
+  uint64_t *vis, *good;
+  int64_t words, nelem;
+  DMF_TRY(run_reverse(v, cam, poses, P, false, 0, false, &vis, &good, &words, &nelem, nullptr, nullptr));
+  return greedy_cover(v, good, P, words, min_gain, selected, nselected);
   DMF_API_END
 }
 

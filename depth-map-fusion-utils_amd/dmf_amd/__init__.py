@@ -302,6 +302,17 @@ class RayTracingEngine:
     def reverseRayTraceFastBatch(self, volume, poses, viz=False):
         return self._reverse(volume, poses, viz, volume._L.dmf_reverse_ray_trace_fast)
 
+    # Set-cover consumer (Algorithms.hpp:38-86 greedySetCover over the
+    # reverseRayTraceFast good sets, tests/SetCover.cpp:218-240): selected pose indices.
+    def setCover(self, volume, poses, min_gain=5):
+        poses = np.ascontiguousarray(np.asarray(poses, np.float32).reshape(-1, 12))
+        P = poses.shape[0]
+        sel = np.zeros(max(P, 1), np.int32)
+        n = C.c_int32()
+        check(volume._L.dmf_greedy_set_cover(volume._h, self._c(), ptr(poses), P, int(min_gain), ptr(sel),
+                                             C.addressof(n)))
+        return sel[:n.value]
+
     # reverseRayTrace  RayTracingEngine.hpp:45-134
     def reverseRayTrace(self, volume, transformation, viz, zdelta=1):
         found, lists = self._reverse(volume, _pose(transformation)[None], viz, volume._L.dmf_reverse_ray_trace)

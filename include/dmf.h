@@ -162,6 +162,15 @@ int dmf_reverse_visibility_device(dmf_volume* v, const dmf_camera* cam, const fl
 /* reverseRayTrace  RayTracingEngine.hpp:45-134 (float-accumulated grid enumeration). */
 int dmf_reverse_ray_trace(dmf_volume* v, const dmf_camera* cam, const float* poses, int32_t P, int32_t viz,
                           uint8_t* found, int64_t* counts, uint64_t* hashes, int64_t cap);
+/* Set-cover consumer: Algorithms.hpp:38-86 greedySetCover over the reverseRayTraceFast
+ * good sets of P candidate poses (the loop of tests/SetCover.cpp:218-240).  selected[P]
+ * receives the chosen pose indices in selection order; the reference stops when no set
+ * adds anything or the best adds fewer than min_gain (5) voxels. */
+int dmf_greedy_set_cover(dmf_volume* v, const dmf_camera* cam, const float* poses, int32_t P, int32_t min_gain,
+                         int32_t* selected, int32_t* nselected);
+/* Same over caller bitmasks (P x words uint64, e.g. d_good of dmf_reverse_visibility_device). */
+int dmf_greedy_set_cover_masks_device(dmf_volume* v, const uint64_t* d_masks, int32_t P, int64_t words,
+                                      int32_t min_gain, int32_t* selected, int32_t* nselected);
 /* rayTrace  RayTracingEngine.hpp:268-309 */
 int dmf_ray_trace(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zdelta, int32_t sparse);
 /* rayTraceAndClassify  RayTracingEngine.hpp:311-375 */

@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <iterator>
 #include <unordered_set>
 #include <vector>
 
@@ -822,6 +823,50 @@ void orc_fuse_depth(const orc_volume* vol, const float* K, int H, int W, const u
       }
   }
   if (stats) { stats[0] += upd; stats[1] += rays; stats[2] += nhit; }
+}
+
+// Algorithms.hpp:38-86 greedySetCover (the set-cover consumer of reverseRayTraceFast,
+// tests/SetCover.cpp:218-240): candidate sets given as concatenated SORTED hash
+// lists with per-set counts.  Each iteration scans the remaining ids in increasing
+// order, keeps the strictly largest |set \ covered| (std::set_difference), stops when
+// none is positive (selected == -1) or the best is below min_gain (5 in the
+// reference), merges the difference into the sorted `covered`, removes the id.
+// Returns the number of selected ids written to `selected` (selection order).
+int32_t orc_greedy_set_cover(const uint64_t* hashes, const int64_t* counts, int32_t nsets, int32_t min_gain,
+                             int32_t* selected) {
+  std::vector<std::vector<uint64_t>> sets(nsets);
+  int64_t off = 0;
+  for (int32_t i = 0; i < nsets; ++i) {
+    sets[i].assign(hashes + off, hashes + off + counts[i]);
+    off += counts[i];
+  }
+  std::vector<uint64_t> covered;
+  std::vector<int32_t> ids(nsets);
+  for (int32_t i = 0; i < nsets; ++i) ids[i] = i;
+  int32_t nsel = 0;
+  while (true) {
+    int64_t sel = -1;
+    size_t max_points = 0;
+    for (int32_t x : ids) {
+      std::vector<uint64_t> diff;
+      std::set_difference(sets[x].begin(), sets[x].end(), covered.begin(), covered.end(),
+                          std::inserter(diff, diff.begin()));
+      if (diff.size() > max_points) {
+        max_points = diff.size();
+        sel = x;
+      }
+    }
+    if (sel == -1) break;
+    if ((int64_t)max_points < min_gain) break;
+    std::vector<uint64_t> diff;
+    std::set_difference(sets[sel].begin(), sets[sel].end(), covered.begin(), covered.end(),
+                        std::inserter(diff, diff.begin()));
+    for (uint64_t h : diff) covered.push_back(h);
+    std::sort(covered.begin(), covered.end());
+    selected[nsel++] = (int32_t)sel;
+    ids.erase(std::remove(ids.begin(), ids.end(), (int32_t)sel), ids.end());
+  }
+  return nsel;
 }
 
 // Clamped fixed-point log-odds (milli-logit units) from the exact counts.

@@ -343,6 +343,19 @@ def fuse_depth(vol, K, depth, poses, dmin=1, dmax=65535, hits=None, misses=None)
     return hits, misses, stats
 
 
+def greedy_set_cover(sets, min_gain=5):
+    """Algorithms.hpp:38-86 greedySetCover over sorted hash lists -> selected ids."""
+    sets = [np.sort(np.asarray(x, np.uint64)) for x in sets]
+    counts = np.array([len(x) for x in sets], np.int64)
+    flat = np.concatenate(sets) if len(sets) and counts.sum() else np.zeros(1, np.uint64)
+    out = np.zeros(max(len(sets), 1), np.int32)
+    L = lib()
+    L.orc_greedy_set_cover.restype = C.c_int32
+    L.orc_greedy_set_cover.argtypes = [_u64p, _i64p, C.c_int32, C.c_int32, _i32p]
+    n = L.orc_greedy_set_cover(flat, counts, len(sets), int(min_gain), out)
+    return out[:n]
+
+
 def fuse_finalize(hits, misses, l_hit=847, l_miss=-405, l_min=-2000, l_max=3511):
     out = np.zeros(hits.size, np.int16)
     lib().orc_fuse_finalize(hits.size, np.ascontiguousarray(hits, np.int32),

@@ -35,6 +35,8 @@ def _run(tmp_path, pts, nrm, poses):
             res["goodlist"] = np.array([int(x) for x in f[1:]], np.uint64)
         elif f[0] == "Sizes:":
             res["sizes"].append(int(f[1]))
+        elif f[0] in ("selected", "selected_from_sets"):
+            res[f[0]] = [int(x) for x in f[1:]]
     return res
 
 
@@ -59,6 +61,10 @@ def test_raytracing_driver_matches_oracle(tmp_path, oracle):
     assert got["found"] == int(found)
     assert np.array_equal(got["goodlist"], good)
     assert got["view_flags"] == int((view == 1).sum()) and got["good_flags"] == int(goodf.sum())
-    sizes = [len(eng.reverseRayTraceFast(ov, T, False)[1]) for T in poses]
+    sets = [eng.reverseRayTraceFast(ov, T, False)[1] for T in poses]
+    sizes = [len(x) for x in sets]
     assert got["sizes"] == sizes
     assert sum(sizes) > 0
+    # tests/SetCover.cpp:236-239 greedySetCover on the same good sets
+    exp = [int(x) for x in oracle.greedy_set_cover(sets, 5)]
+    assert got["selected"] == exp and got["selected_from_sets"] == exp and len(exp) > 0

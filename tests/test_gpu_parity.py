@@ -413,3 +413,41 @@ def test_golden_fixture_gpu(dmf):
             assert np.array_equal(nz, z[f"fuse{n}_{name}_idx"]) and np.array_equal(arr[nz], z[f"fuse{n}_{name}_val"])
         L = eng.fuse_finalize(f, hits, misses)
         assert int(L.astype(np.int64).sum()) == int(z[f"fuse{n}_logodds_sum"][0])
+
+
+def test_greedy_set_cover(oracle, engine, oeng, dmf):
+    """Algorithms.hpp:38-86 greedySetCover over the reverseRayTraceFast good sets of all
+    candidate poses (tests/SetCover.cpp:218-240) == oracle restatement (std::set_difference)."""
+    ov = Hh.oracle_volume(oracle)
+    gv = Hh.gpu_volume()
+    from dmf_amd import scene
+    poses = np.concatenate([Hh.all_poses(), scene.fibonacci_poses(20, seed=77)])
+    sets = [oeng.reverseRayTraceFast(ov, T, False)[1] for T in poses]
+    for min_gain in (5, 1, 200):
+        exp = oracle.greedy_set_cover(sets, min_gain)
+        got = engine.setCover(gv, poses, min_gain)
+        assert np.array_equal(exp, got), (min_gain, exp, got)
+    assert len(oracle.greedy_set_cover(sets, 5)) >= 2
+    # device-mask form over the same good sets
+    import ctypes as C
+    from dmf_amd import _lib
+    L, h = gv._L, gv._h
+    P = len(poses)
+    V = len(gv.occupied_cells_)
+    words = (V + 63) // 64
+    masks = np.zeros((P, words), np.uint64)
+    slot = {int(x): i for i, x in enumerate(gv.occupied_cells_)}
+    for p, st in enumerate(sets):
+        for x in st:
+            i = slot[int(x)]
+            masks[p, i // 64] |= np.uint64(1) << np.uint64(i % 64)
+    d = C.c_void_p()
+    _lib.check(L.dmf_device_malloc(h, C.addressof(d), masks.nbytes))
+    try:
+        _lib.check(L.dmf_memcpy_h2d(h, d.value, masks.ctypes.data, masks.nbytes))
+        sel = np.zeros(P, np.int32)
+        n = C.c_int32()
+        _lib.check(L.dmf_greedy_set_cover_masks_device(h, d.value, P, words, 5, sel.ctypes.data, C.addressof(n)))
+        assert np.array_equal(sel[:n.value], oracle.greedy_set_cover(sets, 5))
+    finally:
+        L.dmf_device_free(h, d.value)

@@ -223,3 +223,30 @@ def test_fusion_is_additive_over_pose_shards(oracle):
     assert np.array_equal(h, h1 + h2) and np.array_equal(m, m1 + m2)
     L = oracle.fuse_finalize(h, m)
     assert L.min() >= -2000 and L.max() <= 3511
+
+
+def test_greedy_set_cover_oracle_vs_python(oracle):
+    """oracle.cpp greedySetCover restatement vs a direct Python transcription of
+    Algorithms.hpp:38-86 (sorted lists, strict max in increasing id order, stop < 5)."""
+    rng = np.random.default_rng(3)
+
+    def ref(sets, min_gain=5):
+        covered, ids, out = set(), list(range(len(sets))), []
+        while True:
+            sel, best = -1, 0
+            for x in ids:
+                d = len(set(sets[x]) - covered)
+                if d > best:
+                    best, sel = d, x
+            if sel == -1 or best < min_gain:
+                return out
+            covered |= set(sets[sel])
+            out.append(sel)
+            ids.remove(sel)
+
+    for trial in range(20):
+        n = int(rng.integers(1, 30))
+        universe = int(rng.integers(10, 400))
+        sets = [np.unique(rng.integers(0, universe, int(rng.integers(0, 80)))).astype(np.uint64) for _ in range(n)]
+        for mg in (1, 5):
+            assert list(oracle.greedy_set_cover(sets, mg)) == ref([list(map(int, s)) for s in sets], mg)
