@@ -60,8 +60,9 @@ def make_inputs(rank, world, P_local, cache_dir="/tmp/dmf_bench_cache"):
     return poses, depth
 
 
-def cpu_baseline(K, poses, depth, n_frames, grid):
-    """Oracle (single-threaded CPU restatement) on a bounded sample of the same workload."""
+def cpu_baseline(K, poses, depth, n_frames, grid, threads=1):
+    """Oracle (CPU restatement; threads > 1 = its OpenMP row-parallel variant) on a
+    bounded sample of the same workload."""
     from oracle import oracle as O
     v = O.Volume()
     v.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
@@ -72,9 +73,16 @@ def cpu_baseline(K, poses, depth, n_frames, grid):
     misses = np.zeros(n, np.int32)
     t0 = time.perf_counter()
     _, _, st = O.fuse_depth(v, K, depth[:n_frames], poses[:n_frames], dmin=scene.DEPTH_MIN_MM,
-                            dmax=scene.DEPTH_MAX_MM, hits=hits, misses=misses)
+                            dmax=scene.DEPTH_MAX_MM, hits=hits, misses=misses, threads=threads)
     dt = time.perf_counter() - t0
     return float(st[0]) / dt, float(st[1]) / dt, dt
+
+
+def host_threads():
+    """Threads for the multi-core CPU baseline: the job's CPU share (OMP_NUM_THREADS on
+    the GPU box), not the whole machine that os.cpu_count() reports there."""
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n if n > 0 else (os.cpu_count() or 1), 16))
 
 
 def main():
@@ -132,18 +140,24 @@ def main():
     ev = []
 
     def step(record=False):
+        # events on the engine's stream (torch's current stream): clear | fuse | all-reduce | finalize
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
+        if record:
+            e[0].record(stream)
         counters.zero_()
         if record:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
+            e[1].record(stream)
         _lib.check(L.dmf_fuse_depth_device(vol._h, pcam, d_depth.data_ptr(), d_poses.data_ptr(), P, pprm, hits_p,
                                            miss_p, stats.data_ptr()))
         if record:
-            e1.record(stream)
-            ev.append((e0, e1))
+            e[2].record(stream)
         D.merge_counters(counters)  # RCCL all-reduce(sum) of [hits | misses] when world > 1
+        if record:
+            e[3].record(stream)
         _lib.check(L.dmf_fuse_finalize_device(vol._h, hits_p, miss_p, pprm, logodds.data_ptr()))
+        if record:
+            e[4].record(stream)
+            ev.append(e)
 
     for _ in range(args.warmup):
         step()
@@ -160,7 +174,18 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = stats.cpu().numpy()
-    fuse_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    seg = np.array([[e[i].elapsed_time(e[i + 1]) for i in range(4)] for e in ev])  # ms per segment
+    clear_ms, fuse_ms, allreduce_ms, finalize_ms = (float(x) for x in seg.mean(0))
+    breakdown = {"clear": clear_ms, "fuse": fuse_ms, "allreduce": allreduce_ms, "finalize": finalize_ms,
+                 "compute_only": clear_ms + fuse_ms + finalize_ms}
+    # grid-wide streaming passes, priced separately: clear writes the
+    # 2 tiled int32 counter arrays; finalize reads them and writes int16 log-odds
+    clear_bytes, fin_bytes = 2 * 4 * nct, 10 * ncell
+    streaming = {
+        "clear": {"ms": clear_ms, "bytes": clear_bytes, "GBps": clear_bytes / (clear_ms * 1e-3) / 1e9,
+                  "frac": clear_bytes / (clear_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+        "finalize": {"ms": finalize_ms, "bytes": fin_bytes, "GBps": fin_bytes / (finalize_ms * 1e-3) / 1e9,
+                     "frac": fin_bytes / (finalize_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
     if st[3] != 0:
         raise RuntimeError(f"DDA guard tripped {st[3]} times")
     elapsed = D.max_over_ranks(elapsed, device=dev)
@@ -187,12 +212,18 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        cpu = None
+        cpu = cpu_mt = None
         if args.cpu_frames > 0 and world == 1:
             ups, rps, dt = cpu_baseline(K, poses, depth, args.cpu_frames, grid)
             cpu = {"value": ups, "unit": "ray-voxel updates/s", "cores": 1, "kind": "port",
                    "sample": f"oracle fuse of {args.cpu_frames} of the {P} frames (640x480, {grid}^3), "
                              f"{dt:.1f}s single-threaded; Mrays/s {rps / 1e6:.3f}"}
+            nt = host_threads()
+            nf = min(P, 4 * args.cpu_frames)
+            ups_mt, rps_mt, dt_mt = cpu_baseline(K, poses, depth, nf, grid, threads=nt)
+            cpu_mt = {"value": ups_mt, "unit": "ray-voxel updates/s", "cores": nt, "kind": "port",
+                      "sample": f"oracle fuse (OpenMP rows, atomic counters) of {nf} of the {P} frames, "
+                                f"{dt_mt:.1f}s on {nt} threads; Mrays/s {rps_mt / 1e6:.3f}"}
         ms = elapsed / args.steps * 1e3
         result = {
             "metric": "ray-voxel updates/sec (3D-DDA log-odds fusion, 512^3 grid, 640x480 depth)",
@@ -221,6 +252,9 @@ def main():
                          "kernel": L.dmf_fuse_kernel().decode(), "kernel_ms": fuse_ms,
                          "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
+            "cpu_baseline_multicore": cpu_mt,
+            "step_breakdown_ms": breakdown,
+            "streaming": streaming,
             "secondary": secondary,
         }
     if world > 1:
@@ -267,7 +301,15 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16
     ms = e0.elapsed_time(e1) / reps
     s = st.cpu().numpy() / reps
     bytes_launch = 2.0 * s[0]  # 2 B (int16-equivalent read) per query-only march sample
-    return {"reverse_ray_trace_fast": {
+    # set-cover consumer (Algorithms.hpp:38-86) over the same good sets
+    sel = np.zeros(P, np.int32)
+    nsel = C.c_int32()
+    t0 = time.perf_counter()
+    _lib.check(L.dmf_greedy_set_cover_masks_device(vol._h, good.data_ptr(), P, words, 5, sel.ctypes.data,
+                                                   C.addressof(nsel)))
+    cover_ms = (time.perf_counter() - t0) * 1e3
+    return {"greedy_set_cover": {"candidates": P, "selected": int(nsel.value), "ms": cover_ms},
+            "reverse_ray_trace_fast": {
         "occupied_voxels": int(V), "poses": P, "ms_per_batch": ms,
         "march_samples_per_s": float(s[0]) / (ms * 1e-3), "voxel_rays_per_s": float(s[1]) / (ms * 1e-3),
         "roofline": {"bound": "hbm", "achieved": bytes_launch / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,

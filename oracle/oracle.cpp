@@ -719,7 +719,16 @@ struct FuseGeom {
 
 static inline int64_t clampi(int64_t v, int64_t lo, int64_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+extern "C++" {
+template <bool kAtomic>
+static inline void bump(int32_t* p) {
+  if (kAtomic) __atomic_fetch_add(p, 1, __ATOMIC_RELAXED);
+  else *p += 1;
+}
+
 // Returns number of cell updates (misses + hit) applied for this ray.
+// kAtomic: the counters are shared by threads (orc_fuse_depth_mt).
+template <bool kAtomic = false>
 static int64_t dda_ray(const FuseGeom& g, const float O[3], const float E[3], bool end_inside,
                        int32_t* hits, int32_t* misses, int64_t* nhit) {
   double go[3], ge[3], D[3];
@@ -778,7 +787,7 @@ static int64_t dda_ray(const FuseGeom& g, const float O[3], const float E[3], bo
   int64_t cur[3] = {cs[0], cs[1], cs[2]};
   const int64_t sx = (int64_t)g.n[1] * g.n[2], sy = g.n[2];
   for (int64_t s = 0; s < nsteps; ++s) {
-    misses[cur[0] * sx + cur[1] * sy + cur[2]] += 1;
+    bump<kAtomic>(&misses[cur[0] * sx + cur[1] * sy + cur[2]]);
     int a = 0;
     if (Tm[1] < Tm[a]) a = 1;
     if (Tm[2] < Tm[a]) a = 2;
@@ -786,10 +795,11 @@ static int64_t dda_ray(const FuseGeom& g, const float O[3], const float E[3], bo
     Tm[a] += In[a];
   }
   const int64_t lin = cur[0] * sx + cur[1] * sy + cur[2];
-  if (end_inside) { hits[lin] += 1; ++*nhit; }
-  else misses[lin] += 1;
+  if (end_inside) { bump<kAtomic>(&hits[lin]); ++*nhit; }
+  else bump<kAtomic>(&misses[lin]);
   return nsteps + 1;
 }
+}  // extern "C++"
 
 // stats[0] = cell updates, stats[1] = rays traced (valid depth), stats[2] = hits
 void orc_fuse_depth(const orc_volume* vol, const float* K, int H, int W, const uint16_t* depth,
@@ -821,6 +831,45 @@ void orc_fuse_depth(const orc_volume* vol, const float* K, int H, int W, const u
         ++rays;
         upd += dda_ray(g, O, E, inside, hits, misses, &nhit);
       }
+  }
+  if (stats) { stats[0] += upd; stats[1] += rays; stats[2] += nhit; }
+}
+
+// Same computation, pose/row-parallel over nthreads OpenMP threads with relaxed
+// atomic counter increments (the CPU baseline on all host cores).
+// Counts are integers, so the result equals orc_fuse_depth exactly.
+void orc_fuse_depth_mt(const orc_volume* vol, const float* K, int H, int W, const uint16_t* depth,
+                       const float* poses, int P, int dmin, int dmax, int32_t* hits, int32_t* misses,
+                       int64_t* stats, int nthreads) {
+  FuseGeom g;
+  g.mn[0] = vol->xmin_; g.mn[1] = vol->ymin_; g.mn[2] = vol->zmin_;
+  g.dl[0] = vol->xdelta_; g.dl[1] = vol->ydelta_; g.dl[2] = vol->zdelta_;
+  g.n[0] = vol->xdim_; g.n[1] = vol->ydim_; g.n[2] = vol->zdim_;
+  const Cam cam = make_cam(K, H, W);
+  int64_t upd = 0, rays = 0, nhit = 0;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 4) reduction(+ : upd, rays, nhit)
+  for (int64_t pr = 0; pr < (int64_t)P * H; ++pr) {
+    const int p = (int)(pr / H), r = (int)(pr % H);
+    const Aff A = load_aff(poses + 12 * p);
+    const float O[3] = {A.m[0][3], A.m[1][3], A.m[2][3]};
+    const uint16_t* dp = depth + (size_t)p * H * W;
+    for (int c = 0; c < W; ++c) {
+      const int d = dp[(size_t)r * W + c];
+      if (!(d >= dmin && d < dmax)) continue;
+      float pc[3], E[3];
+      cam.project(r, c, d, pc);
+      xform(A, pc[0], pc[1], pc[2], E);
+      bool inside = vol->valid_points(E[0], E[1], E[2]);
+      if (inside) {
+        int a, b, cc;
+        vol->get_voxel(E[0], E[1], E[2], a, b, cc);
+        inside = vol->valid_coords(a, b, cc);
+      }
+      ++rays;
+      int64_t h = 0;
+      upd += dda_ray<true>(g, O, E, inside, hits, misses, &h);
+      nhit += h;
+    }
   }
   if (stats) { stats[0] += upd; stats[1] += rays; stats[2] += nhit; }
 }

@@ -326,8 +326,9 @@ def will_collide(vol, a, b):
 LOGODDS_DEFAULT = dict(l_hit=847, l_miss=-405, l_min=-2000, l_max=3511)
 
 
-def fuse_depth(vol, K, depth, poses, dmin=1, dmax=65535, hits=None, misses=None):
-    """DESIGN.md §4 3D-DDA fusion of P depth frames.  depth (P,H,W) uint16, poses (P,12)."""
+def fuse_depth(vol, K, depth, poses, dmin=1, dmax=65535, hits=None, misses=None, threads=1):
+    """DESIGN.md §4 3D-DDA fusion of P depth frames.  depth (P,H,W) uint16, poses (P,12).
+    threads > 1: the OpenMP row-parallel variant (same counts)."""
     depth = np.ascontiguousarray(depth, np.uint16)
     if depth.ndim == 2:
         depth = depth[None]
@@ -339,7 +340,13 @@ def fuse_depth(vol, K, depth, poses, dmin=1, dmax=65535, hits=None, misses=None)
     if misses is None:
         misses = np.zeros(n, np.int32)
     stats = np.zeros(3, np.int64)
-    lib().orc_fuse_depth(vol._h, _f32(K, 9), H, W, depth, poses, P, dmin, dmax, hits, misses, stats)
+    if threads > 1:
+        L = lib()
+        L.orc_fuse_depth_mt.restype = None
+        L.orc_fuse_depth_mt.argtypes = list(L.orc_fuse_depth.argtypes) + [C.c_int]
+        L.orc_fuse_depth_mt(vol._h, _f32(K, 9), H, W, depth, poses, P, dmin, dmax, hits, misses, stats, int(threads))
+    else:
+        lib().orc_fuse_depth(vol._h, _f32(K, 9), H, W, depth, poses, P, dmin, dmax, hits, misses, stats)
     return hits, misses, stats
 
 

@@ -250,3 +250,22 @@ def test_greedy_set_cover_oracle_vs_python(oracle):
         sets = [np.unique(rng.integers(0, universe, int(rng.integers(0, 80)))).astype(np.uint64) for _ in range(n)]
         for mg in (1, 5):
             assert list(oracle.greedy_set_cover(sets, mg)) == ref([list(map(int, s)) for s in sets], mg)
+
+
+def test_fuse_mt_equals_single_thread(oracle):
+    """The OpenMP CPU baseline variant gives the same integer counts."""
+    from dmf_amd import scene
+    K = scene.K_640x480.copy()
+    K[[0, 2, 4, 5]] *= np.float32(0.25)
+    poses = scene.fibonacci_poses(3, seed=4)
+    depth = scene.render_frames(K, 160, 120, poses)
+
+    def vol():
+        v = oracle.Volume()
+        v.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+        v.setVolumeSize(48, 48, 48)
+        v.constructVolume()
+        return v
+    h1, m1, s1 = oracle.fuse_depth(vol(), K, depth, poses, dmin=200, dmax=1000)
+    h4, m4, s4 = oracle.fuse_depth(vol(), K, depth, poses, dmin=200, dmax=1000, threads=4)
+    assert np.array_equal(h1, h4) and np.array_equal(m1, m4) and np.array_equal(s1, s4)
