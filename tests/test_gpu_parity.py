@@ -451,3 +451,50 @@ def test_greedy_set_cover(oracle, engine, oeng, dmf):
         assert np.array_equal(sel[:n.value], oracle.greedy_set_cover(sets, 5))
     finally:
         L.dmf_device_free(h, d.value)
+
+
+def test_golden_config1_gpu(dmf):
+    """SURVEY.md §8c-3 config 1 (tests/Raytracing.cpp:61-92 sequence, 640x480, one pose)
+    against tests/golden/golden_config1.npz (gen_golden_config1.py)."""
+    import hashlib
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_config1.npz"))
+    sha = lambda a: np.frombuffer(hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest(), np.uint8)
+    K, pose, depth, q = z["K"], z["pose"], z["depth"], z["normals_q"]
+    eng = dmf.RayTracingEngine(dmf.Camera(K, 480, 640))
+    v0 = dmf.VoxelVolume()
+    v0.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    v0.setVolumeSize(8, 8, 8)
+    v0.constructVolume()
+    xyz = eng.backproject(v0, depth, pose)
+    assert np.array_equal(sha(xyz), z["bp_sha"])
+    m = depth > 0
+    pts = xyz[m]
+    nrm = (q[m].astype(np.float32) / np.float32(127.0)).astype(np.float32)
+    lo, hi = pts.min(0), pts.max(0)
+    v = dmf.VoxelVolume()
+    v.setDimensions(float(lo[0]), float(hi[0]), float(lo[1]), float(hi[1]), float(lo[2]), float(hi[2]))
+    v.setVolumeSize(*[int(np.float32(hi[i] - lo[i]) * np.float32(125)) for i in range(3)])
+    v.constructVolume()
+    v.integratePointCloud(pts, nrm)
+    assert tuple(v.dims) == tuple(z["dims"])
+    assert np.array_equal(v.occupied_cells_, z["occ"])
+    assert np.array_equal(sha(v.voxel_counts()[0].astype(np.int64)), z["npts_sha"])
+    found, good = eng.reverseRayTraceFast(v, pose, True)
+    assert int(found) == int(z["rrtf_found"][0]) and np.array_equal(good, z["rrtf_good"])
+    view, goodf = v.voxel_flags()
+    assert np.array_equal(sha(view.astype(np.int32)), z["rrtf_view_sha"])
+    assert np.array_equal(sha(goodf.astype(np.uint8)), z["rrtf_goodf_sha"])
+    k, h = eng.forward_first_hits(v, pose, 10, 10, 1, 1)
+    assert np.array_equal(sha(k), z["fwd_k_sha"]) and np.array_equal(sha(h), z["fwd_h_sha"])
+    assert eng.rayTraceAndGetMinimum(v, pose) == int(z["minimum"][0])
+    vf = dmf.VoxelVolume()
+    vf.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    vf.setVolumeSize(128, 128, 128)
+    vf.constructVolume()
+    from dmf_amd import scene
+    hits, misses, st = eng.fuse_depth(vf, depth[None], pose[None],
+                                      dmf.FuseParams(dmin_mm=scene.DEPTH_MIN_MM, dmax_mm=scene.DEPTH_MAX_MM))
+    assert np.array_equal(st, z["fuse_stats"])
+    assert np.array_equal(sha(hits), z["fuse_hits_sha"]) and np.array_equal(sha(misses), z["fuse_misses_sha"])
+    assert np.array_equal(sha(eng.fuse_finalize(vf, hits, misses)), z["fuse_logodds_sha"])

@@ -269,3 +269,15 @@ def test_fuse_mt_equals_single_thread(oracle):
     h1, m1, s1 = oracle.fuse_depth(vol(), K, depth, poses, dmin=200, dmax=1000)
     h4, m4, s4 = oracle.fuse_depth(vol(), K, depth, poses, dmin=200, dmax=1000, threads=4)
     assert np.array_equal(h1, h4) and np.array_equal(m1, m4) and np.array_equal(s1, s4)
+
+
+def test_golden_config1_regression(oracle):
+    """The oracle reproduces golden_config1.npz (config 1: 640x480, reference K, one pose)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(GOLD))
+    import gen_golden_config1 as G1
+    z = np.load(os.path.join(os.path.dirname(GOLD), "golden_config1.npz"))
+    out = G1.compute(z["K"], z["pose"], z["depth"], z["normals_q"])
+    for k, v in out.items():
+        assert np.array_equal(np.asarray(v), z[k]), k
+    assert len(z["occ"]) > 1000 and len(z["rrtf_good"]) > 1000 and z["fuse_stats"][0] > 1e6
