@@ -41,3 +41,40 @@ def sum_over_ranks(values, device=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(x) for x in t.cpu().tolist()]
+
+
+# ---- visibility queries (reverseRayTraceFast / set cover), SURVEY.md §8e ----------
+# Queries only read the grid: rank r evaluates its contiguous pose block, the per-pose
+# outputs are gathered in pose order (no data-path collective during the compute), and
+# the idempotent view/good flags merge with an all-reduce(MAX).
+
+def gather_pose_lists(found, lists, group=None):
+    """All ranks' (found[], lists[]) of their pose blocks -> the full pose-ordered
+    (found, lists) on every rank (all_gather_object; shards are contiguous)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return list(found), list(lists)
+    parts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(parts, (list(found), [list(map(int, x)) for x in lists]), group=group)
+    f_all, l_all = [], []
+    for f, l in parts:
+        f_all += f
+        l_all += l
+    return f_all, l_all
+
+
+def merge_flags_max(flags, group=None):
+    """All-reduce(MAX) of a per-voxel flag tensor (view int32 / good uint8 widened), in place."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
+    return flags
+
+
+def sharded_visibility(compute, poses, world, rank, group=None):
+    """compute(pose_block) -> (found[], lists[]) on this rank's block (e.g.
+    RayTracingEngine.reverseRayTraceFastBatch bound to a volume); returns the full
+    pose-ordered results on every rank."""
+    a, b = shard_range(len(poses), world, rank)
+    found, lists = compute(poses[a:b]) if b > a else ([], [])
+    return gather_pose_lists(found, lists, group)

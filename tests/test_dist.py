@@ -71,3 +71,51 @@ def test_sharded_fusion_gloo_world2(tmp_path, oracle):
         assert np.array_equal(c[: n ** 3], h) and np.array_equal(c[n ** 3:], m)
         s = np.load(tmp_path / f"s{r}.npy")
         assert np.array_equal(s[:3], st.astype(np.float64)) and s[3] == 2.0
+
+
+def _vis_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "depth-map-fusion-utils_amd"), os.path.join(root, "tests")]
+    import torch
+    import torch.distributed as dist
+    import helpers as Hh
+    from dmf_amd import dist as D
+    from oracle import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ov = Hh.oracle_volume(oracle, n=64)
+    eng = oracle.Engine(Hh.K)
+    poses = Hh.all_poses()
+
+    def compute(block):
+        res = [eng.reverseRayTraceFast(ov, T, True) for T in block]
+        return [f for f, _ in res], [g for _, g in res]
+    found, lists = D.sharded_visibility(compute, poses, world, rank)
+    view, good, _, _ = ov.voxel_table()
+    flags = torch.from_numpy(np.stack([view.astype(np.int32), good.astype(np.int32)]))
+    D.merge_flags_max(flags)
+    sel = oracle.greedy_set_cover(lists, 5)
+    np.save(os.path.join(out_dir, f"v{rank}.npy"),
+            np.array([len(x) for x in lists] + [int(f) for f in found] + list(sel), np.int64))
+    np.save(os.path.join(out_dir, f"f{rank}.npy"), flags.numpy())
+    dist.destroy_process_group()
+
+
+def test_sharded_visibility_gloo_world2(tmp_path, oracle):
+    """Pose-sharded reverseRayTraceFast (viz) over 2 gloo ranks: gathered lists, MAX-merged
+    flags and the set cover on the gathered lists equal the single-rank run."""
+    import helpers as Hh
+    ov = Hh.oracle_volume(oracle, n=64)
+    eng = oracle.Engine(Hh.K)
+    poses = Hh.all_poses()
+    res = [eng.reverseRayTraceFast(ov, T, True) for T in poses]
+    lists = [g for _, g in res]
+    view, good, _, _ = ov.voxel_table()
+    exp = np.array([len(x) for x in lists] + [int(f) for f, _ in res] + list(oracle.greedy_set_cover(lists, 5)),
+                   np.int64)
+    mp.spawn(_vis_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert np.array_equal(np.load(tmp_path / f"v{r}.npy"), exp)
+        f = np.load(tmp_path / f"f{r}.npy")
+        assert np.array_equal(f[0], view.astype(np.int32)) and np.array_equal(f[1], good.astype(np.int32))
