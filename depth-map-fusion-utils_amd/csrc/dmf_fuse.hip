@@ -458,6 +458,227 @@ __global__ __launch_bounds__(64) void k_fuse_t(Geom g, CamP cam, const uint16_t*
   }
 }
 
+// k_fuse_t with kR rays per lane: the wave owns an 8 x (8 kR) pixel packet; every lane
+// walks and replays its kR rays interleaved (independent dependency chains for the
+// scheduler), and the rays share one LDS box per round (more rays per cell, fewer
+// flushed atomics, the round's reduction amortised over kR times the updates).
+// Odd (lane + ray) parities replay backwards.  Same exact counts as k_fuse_t.
+template <int kS, int kBox, int kR>
+__global__ __launch_bounds__(64) void k_fuse_r(Geom g, CamP cam, const uint16_t* __restrict__ depth,
+                                               const PoseX* __restrict__ poses, int dmin, int dmax, int packets_x,
+                                               int32_t* __restrict__ hits, int32_t* __restrict__ misses,
+                                               unsigned long long* __restrict__ stats) {
+  static_assert(kS <= 15, "2-bit codes of up to 15 advances with a 32-bit field mask");
+  static_assert(kBox % 256 == 0 && kBox <= 65536, "box scanned 256 cells per iteration, 16-bit indices");
+  static_assert(kBox >= 64 * kS * kR, "the non-zero list lives in the box");
+  stats = stat_slot(stats);
+  __shared__ __attribute__((aligned(16))) int box[kBox];
+  uint32_t* nzl = (uint32_t*)box;  // non-zero list written behind the scan (see k_fuse_t)
+  const int l = threadIdx.x;
+  for (int i = l; i < kBox; i += 64) box[i] = 0;
+  const Tiles tl = tiles_of(g.n);
+  int32_t E01[kR], E02[kR], E12[kR], K0[kR], K1[kR], K2[kR];
+  int st0[kR], st1[kR], st2[kR], c0[kR], c1[kR], c2[kR], left[kR];
+  bool end_inside[kR];
+  unsigned long long upd = 0, nvalid = 0, nhit = 0;
+#pragma unroll
+  for (int j = 0; j < kR; ++j) {
+    const int r = (blockIdx.x / packets_x) * (8 * kR) + 8 * j + (l >> 3), c = (blockIdx.x % packets_x) * 8 + (l & 7);
+    Ray R;
+    bool valid;
+    upd += (unsigned long long)pixel_ray(g, cam, depth, poses, blockIdx.y, r, c, dmin, dmax, R, valid);
+    nvalid += valid ? 1 : 0;
+    nhit += (R.left > 0 && R.end_inside) ? 1 : 0;
+    E01[j] = R.E01; E02[j] = R.E02; E12[j] = R.E12;
+    K0[j] = R.K[0]; K1[j] = R.K[1]; K2[j] = R.K[2];
+    st0[j] = R.st[0]; st1[j] = R.st[1]; st2[j] = R.st[2];
+    c0[j] = R.c[0]; c1[j] = R.c[1]; c2[j] = R.c[2];
+    left[j] = R.left;
+    end_inside[j] = R.end_inside;
+  }
+  unsigned long long nflush = 0, nround_lds = 0, nround_direct = 0;
+  while (true) {
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < kR; ++j) any = any || left[j] > 0;
+    if (__builtin_amdgcn_ballot_w64(any) == 0) break;
+    int rem[kR], nadv[kR], nm[kR], e0[kR], e1[kR], e2[kR], m0[kR], m1[kR], m2[kR];
+    bool fin[kR];
+    uint32_t codes[kR];
+    bool allfull = true;
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      rem[j] = left[j] < kS ? left[j] : kS;
+      fin[j] = rem[j] == left[j] && rem[j] > 0;
+      nadv[j] = fin[j] ? rem[j] - 1 : rem[j];
+      codes[j] = 0;
+      allfull = allfull && nadv[j] == kS;
+    }
+    if (__builtin_amdgcn_ballot_w64(!allfull) == 0) {
+#pragma unroll
+      for (int k = 0; k < kS; ++k)
+#pragma unroll
+        for (int j = 0; j < kR; ++j) {
+          bool s0, s1, s2;
+          dda_select(E01[j], E02[j], E12[j], K0[j], K1[j], K2[j], s0, s1, s2);
+          codes[j] |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
+        }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kS; ++k)
+#pragma unroll
+        for (int j = 0; j < kR; ++j)
+          if (k < nadv[j]) {
+            bool s0, s1, s2;
+            dda_select(E01[j], E02[j], E12[j], K0[j], K1[j], K2[j], s0, s1, s2);
+            codes[j] |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
+          }
+    }
+    uint32_t px = 0, py = 0, pz = 0;
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      const uint32_t fmask = (1u << (2 * nadv[j])) - 1u;
+      const int n2 = __builtin_popcount(codes[j] & fmask & 0xAAAAAAAAu);
+      const int n1 = __builtin_popcount(codes[j] & fmask & 0x55555555u);
+      const int n0 = nadv[j] - n1 - n2;
+      e0[j] = c0[j] + st0[j] * n0; e1[j] = c1[j] + st1[j] * n1; e2[j] = c2[j] + st2[j] * n2;
+      nm[j] = (fin[j] && end_inside[j]) ? rem[j] - 1 : rem[j];
+      m0[j] = e0[j]; m1[j] = e1[j]; m2[j] = e2[j];
+      if (nm[j] > 0 && nadv[j] > 0 && (!fin[j] || end_inside[j])) {
+        const uint32_t lc = (codes[j] >> (2 * (nadv[j] - 1))) & 3u;
+        m0[j] -= lc == 0u ? st0[j] : 0;
+        m1[j] -= lc == 1u ? st1[j] : 0;
+        m2[j] -= lc == 2u ? st2[j] : 0;
+      }
+      if (nm[j] > 0) {
+        px = pkmax(px, (uint32_t)max(c0[j], m0[j]) | ((0xffffu - (uint32_t)min(c0[j], m0[j])) << 16));
+        py = pkmax(py, (uint32_t)max(c1[j], m1[j]) | ((0xffffu - (uint32_t)min(c1[j], m1[j])) << 16));
+        pz = pkmax(pz, (uint32_t)max(c2[j], m2[j]) | ((0xffffu - (uint32_t)min(c2[j], m2[j])) << 16));
+      }
+    }
+    const uint32_t rx = wave_pkmax(px), ry = wave_pkmax(py), rz = wave_pkmax(pz);
+    if (rx != 0u) {
+      const int ax = (0xffff - (int)(rx >> 16)) & ~1, ay = (0xffff - (int)(ry >> 16)) & ~1,
+                az = (0xffff - (int)(rz >> 16)) & ~3;
+      const int tbx = (((int)(rx & 0xffffu) - ax) >> 1) + 1, tby = (((int)(ry & 0xffffu) - ay) >> 1) + 1,
+                tbz = (((int)(rz & 0xffffu) - az) >> 2) + 1;
+      const int tyz = tby * tbz;
+      const int64_t ncell_box = (int64_t)tbx * tyz * 16;
+      int x[kR], y[kR], z[kR], gx[kR], gy[kR], gz[kR];
+      uint32_t rc[kR];
+#pragma unroll
+      for (int j = 0; j < kR; ++j) {
+        const bool back = ((l + j) & 1) != 0;
+        const int sgn = back ? -1 : 1;
+        x[j] = back ? m0[j] : c0[j]; y[j] = back ? m1[j] : c1[j]; z[j] = back ? m2[j] : c2[j];
+        gx[j] = sgn * st0[j]; gy[j] = sgn * st1[j]; gz[j] = sgn * st2[j];
+        rc[j] = codes[j];
+        if (back) {
+          uint32_t t = __builtin_bitreverse32(codes[j]);
+          t = ((t & 0x55555555u) << 1) | ((t & 0xAAAAAAAAu) >> 1);
+          rc[j] = nm[j] >= 2 ? t >> (2 * (17 - nm[j])) : 0u;
+        }
+      }
+      if (ncell_box <= kBox) {
+        ++nround_lds;
+        int cur[kR], nx[kR], ny[kR], nzd[kR], qz[kR], ix[kR], iy[kR], jx[kR], jy[kR], jz[kR], fz[kR];
+        bool allm = true;
+#pragma unroll
+        for (int j = 0; j < kR; ++j) {
+          ix[j] = gx[j] * 8; iy[j] = gy[j] * 4;
+          jx[j] = gx[j] * (tyz * 16 - 8); jy[j] = gy[j] * (tbz * 16 - 4); jz[j] = gz[j] * 13;
+          fz[j] = gz[j] > 0 ? 3 : 0;
+          qz[j] = z[j] & 3;
+          nx[j] = ((x[j] & 1) == (gx[j] > 0 ? 1 : 0)) ? jx[j] : ix[j];
+          ny[j] = ((y[j] & 1) == (gy[j] > 0 ? 1 : 0)) ? jy[j] : iy[j];
+          nzd[j] = qz[j] == fz[j] ? jz[j] : gz[j];
+          cur[j] = ((((x[j] - ax) >> 1) * tby + ((y[j] - ay) >> 1)) * tbz + ((z[j] - az) >> 2)) * 16 +
+                   (((x[j] & 1) << 3) | ((y[j] & 1) << 2) | qz[j]);
+          allm = allm && nm[j] == kS;
+        }
+        const bool full = __builtin_amdgcn_ballot_w64(!allm) == 0;
+#pragma unroll
+        for (int k = 0; k < kS; ++k)
+#pragma unroll
+          for (int j = 0; j < kR; ++j) {
+            if (full || k < nm[j]) atomicAdd(&box[cur[j]], 1);
+            if (k + 1 < kS) {
+              const uint32_t cd = (rc[j] >> (2 * k)) & 3u;
+              const bool a0 = cd == 0u, a1 = cd == 1u, a2 = cd == 2u;
+              cur[j] += a2 ? nzd[j] : (a1 ? ny[j] : nx[j]);
+              nx[j] ^= a0 ? (ix[j] ^ jx[j]) : 0;
+              ny[j] ^= a1 ? (iy[j] ^ jy[j]) : 0;
+              qz[j] = a2 ? ((qz[j] + gz[j]) & 3) : qz[j];
+              nzd[j] = qz[j] == fz[j] ? jz[j] : gz[j];
+            }
+          }
+        __syncthreads();  // single-wave workgroup: orders the LDS adds before the flush
+        const int nb = (int)ncell_box;
+        int nnz = 0;
+        for (int i0 = 0; i0 < nb; i0 += 256) {
+          int v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + l;
+            v[u] = i < nb ? box[i] : 0;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + l;
+            const uint64_t b = __builtin_amdgcn_ballot_w64(v[u] != 0);
+            if (i < nb) box[i] = 0;
+            if (v[u]) nzl[nnz + lane_prefix(b)] = (uint32_t)i | ((uint32_t)v[u] << 16);
+            nnz += __builtin_popcountll(b);
+          }
+        }
+        __syncthreads();
+        const float rtyz = __builtin_amdgcn_rcpf((float)tyz), rtz = __builtin_amdgcn_rcpf((float)tbz);
+        const int tax = ax >> 1, tay = ay >> 1, taz = az >> 2;
+        for (int e = l; e < nnz; e += 64) {
+          const uint32_t en = nzl[e];
+          const int i = (int)(en & 0xffffu);
+          int rr, tc;
+          const int t = i >> 4;
+          const int ta = small_div(t, tyz, rtyz, rr);
+          const int tb = small_div(rr, tbz, rtz, tc);
+          ++nflush;
+          atomic_add_dev(&misses[tile_base(tl, tax + ta, tay + tb, taz + tc) + (i & 15)], (int)(en >> 16));
+        }
+        __syncthreads();
+        for (int e = l; e < nnz; e += 64) box[e] = 0;
+        __syncthreads();
+      } else {
+        ++nround_direct;
+#pragma unroll
+        for (int j = 0; j < kR; ++j)
+#pragma unroll
+          for (int k = 0; k < kS; ++k) {
+            if (k < nm[j]) atomic_add_dev(&misses[tiled_index(tl, x[j], y[j], z[j])], 1);
+            const uint32_t cd = (rc[j] >> (2 * k)) & 3u;
+            x[j] += cd == 0u ? gx[j] : 0;
+            y[j] += cd == 1u ? gy[j] : 0;
+            z[j] += cd == 2u ? gz[j] : 0;
+          }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      if (fin[j] && end_inside[j]) atomic_add_dev(&hits[tiled_index(tl, e0[j], e1[j], e2[j])], 1);
+      c0[j] = e0[j]; c1[j] = e1[j]; c2[j] = e2[j];
+      left[j] -= rem[j];
+    }
+  }
+  if (stats) {
+    wave_stats(stats, upd, nvalid, nhit);
+    for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
+    if (l == 0) {
+      if (nflush) atomicAdd(&stats[6], nflush);
+      if (nround_lds) atomicAdd(&stats[4], nround_lds);
+      if (nround_direct) atomicAdd(&stats[5], nround_direct);
+    }
+  }
+}
+
 // Tiled counters -> clamped int16 log-odds in the reference's x-major voxel order.
 // One lane per 4 consecutive z cells: one 16-B read per counter, one 8-B write.
 __global__ __launch_bounds__(256) void k_finalize(Geom g, const int32_t* __restrict__ hits,
@@ -542,7 +763,13 @@ const char* dmf_fuse_kernel(void) {
     case 10: return "dmf::k_fuse_t<10, 1536, false>";
     case 11: return "dmf::k_fuse_t<12, 1536, true>";
     case 12: return "dmf::k_fuse_t<14, 2048, true>";
-    default: return "dmf::k_fuse_t<10, 1280, true>";
+    case 20: return "dmf::k_fuse_r<10, 2560, 2>";
+    case 21: return "dmf::k_fuse_r<8, 2048, 2>";
+    case 22: return "dmf::k_fuse_r<10, 2048, 2>";
+    case 23: return "dmf::k_fuse_r<6, 2048, 3>";
+    case 24: return "dmf::k_fuse_r<10, 1280, 1>";
+    case 25: return "dmf::k_fuse_t<10, 1280, true>";
+    default: return "dmf::k_fuse_r<10, 1280, 1>";
   }
 }
 
@@ -581,6 +808,9 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
   if (d_stats) DMF_TRY(stats_begin(v, &st));
   const int pkx = (cp.W + 7) / 8, pky = (cp.H + 7) / 8;
   const dim3 gridw((unsigned)(pkx * pky), (unsigned)P);
+#define DMF_FUSE_LAUNCH_R(K, NR)                                                                               \
+  hipLaunchKernelGGL(K, dim3((unsigned)(pkx * ((cp.H + 8 * (NR) - 1) / (8 * (NR)))), (unsigned)P), dim3(64), 0,        \
+                     v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, d_misses, st)
 #define DMF_FUSE_LAUNCH_T(K)                                                                                    \
   hipLaunchKernelGGL(K, gridw, dim3(64), 0, v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, \
                      d_misses, st)
@@ -602,9 +832,16 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
     case 10: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1536, false>)); break;
     case 11: DMF_FUSE_LAUNCH_T((k_fuse_t<12, 1536>)); break;
     case 12: DMF_FUSE_LAUNCH_T((k_fuse_t<14, 2048>)); break;
-    default: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1280>)); break;
+    case 20: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 2560, 2>), 2); break;
+    case 21: DMF_FUSE_LAUNCH_R((k_fuse_r<8, 2048, 2>), 2); break;
+    case 22: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 2048, 2>), 2); break;
+    case 23: DMF_FUSE_LAUNCH_R((k_fuse_r<6, 2048, 3>), 3); break;
+    case 24: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 1280, 1>), 1); break;
+    case 25: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1280>)); break;
+    default: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 1280, 1>), 1); break;
   }
 #undef DMF_FUSE_LAUNCH_T
+#undef DMF_FUSE_LAUNCH_R
   DMF_LAUNCH_CHECK();
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
   DMF_LAUNCH_CHECK();
