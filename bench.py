@@ -287,8 +287,13 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16
     def run():
         _lib.check(L.dmf_reverse_visibility_device(vol._h, C.addressof(cam), d_poses.data_ptr(), P, 0, None,
                                                    good.data_ptr(), st.data_ptr()))
-    run()
+    f0 = torch.cuda.Event(enable_timing=True)
+    f1 = torch.cuda.Event(enable_timing=True)
+    f0.record(stream)
+    run()  # first call after integration also builds the brick distance field
+    f1.record(stream)
     torch.cuda.synchronize(dev)
+    first_ms = f0.elapsed_time(f1)
     st.zero_()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
@@ -301,6 +306,31 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16
     ms = e0.elapsed_time(e1) / reps
     s = st.cpu().numpy() / reps
     bytes_launch = 2.0 * s[0]  # 2 B (int16-equivalent read) per query-only march sample
+    # forward depth-plane march (RayTracingEngine.hpp:280-308 semantics), dense 640x480,
+    # all P poses in one launch: first occupied sample per pixel
+    kbuf = torch.empty(P * H * W, dtype=torch.int32, device=dev)
+    sbuf = torch.empty(P * H * W, dtype=torch.int32, device=dev)
+    fst = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def fwd():
+        _lib.check(L.dmf_forward_first_hits_device(vol._h, C.addressof(cam), d_poses.data_ptr(), P, 10, 10, 1, 1,
+                                                   kbuf.data_ptr(), sbuf.data_ptr(), fst.data_ptr()))
+    fwd()
+    torch.cuda.synchronize(dev)
+    fst.zero_()
+    g0 = torch.cuda.Event(enable_timing=True)
+    g1 = torch.cuda.Event(enable_timing=True)
+    g0.record(stream)
+    fwd()
+    g1.record(stream)
+    torch.cuda.synchronize(dev)
+    fwd_ms = g0.elapsed_time(g1)
+    fwd_samples = float(fst.cpu().numpy()[0])
+    forward = {"rays": P * H * W, "ms_per_batch": fwd_ms, "march_samples_per_s": fwd_samples / (fwd_ms * 1e-3),
+               "mrays_per_s": P * H * W / (fwd_ms * 1e-3) / 1e6,
+               "roofline": {"bound": "hbm", "achieved": 2.0 * fwd_samples / (fwd_ms * 1e-3) / 1e9,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": 2.0 * fwd_samples / (fwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
     # set-cover consumer (Algorithms.hpp:38-86) over the same good sets
     sel = np.zeros(P, np.int32)
     nsel = C.c_int32()
@@ -309,8 +339,10 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16
                                                    C.addressof(nsel)))
     cover_ms = (time.perf_counter() - t0) * 1e3
     return {"greedy_set_cover": {"candidates": P, "selected": int(nsel.value), "ms": cover_ms},
+            "forward_first_hits": forward,
             "reverse_ray_trace_fast": {
         "occupied_voxels": int(V), "poses": P, "ms_per_batch": ms,
+        "first_call_ms": first_ms, "note": "first call after integration includes the brick distance field build",
         "march_samples_per_s": float(s[0]) / (ms * 1e-3), "voxel_rays_per_s": float(s[1]) / (ms * 1e-3),
         "roofline": {"bound": "hbm", "achieved": bytes_launch / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": bytes_launch / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}}

@@ -2,6 +2,7 @@
 // (Volume.hpp:172-228) and depth back-projection (Camera.hpp:24-45) on gfx950.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -368,7 +369,8 @@ __global__ void k_first_flags(const int32_t* __restrict__ plin, int64_t n, const
 __global__ void k_assign_slots(Geom g, const int32_t* __restrict__ plin, const int32_t* __restrict__ flag,
                                const int32_t* __restrict__ rank, int64_t n, int64_t V0, int32_t* __restrict__ slot_of,
                                uint64_t* __restrict__ hash, int32_t* __restrict__ view, uint8_t* __restrict__ good,
-                               uint32_t* __restrict__ occ, uint32_t* __restrict__ brick, int nby, int nbz) {
+                               uint32_t* __restrict__ occ, uint32_t* __restrict__ brick, int nby, int nbz,
+                               int bsh) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || !flag[i]) return;
   const int32_t lin = plin[i];
@@ -380,8 +382,7 @@ __global__ void k_assign_slots(Geom g, const int32_t* __restrict__ plin, const i
   view[slot] = 0;
   good[slot] = 0;
   atomicOr(&occ[(uint32_t)lin >> 5], 1u << ((uint32_t)lin & 31));
-  const uint32_t bl = ((uint32_t)(x >> kBrickShift) * (uint32_t)nby + (uint32_t)(y >> kBrickShift)) * (uint32_t)nbz +
-                      (uint32_t)(z >> kBrickShift);
+  const uint32_t bl = ((uint32_t)(x >> bsh) * (uint32_t)nby + (uint32_t)(y >> bsh)) * (uint32_t)nbz + (uint32_t)(z >> bsh);
   atomicOr(&brick[bl >> 5], 1u << (bl & 31));
 }
 
@@ -487,7 +488,7 @@ static int integrate_impl(dmf_volume* v, const float* d_xyz, const float* d_nrm,
     v->Vcap = cap;
   }
   hipLaunchKernelGGL(k_assign_slots, grd, blk, 0, v->stream, g, (const int32_t*)plin, (const int32_t*)flag,
-                     (const int32_t*)rank, n, V0, v->d_slot_of, v->d_hash, v->d_view, v->d_good, v->d_occ, v->d_brick, v->nb[1], v->nb[2]);
+                     (const int32_t*)rank, n, V0, v->d_slot_of, v->d_hash, v->d_view, v->d_good, v->d_occ, v->d_brick, v->nb[1], v->nb[2], v->brick_shift);
   DMF_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_point_slots, grd, blk, 0, v->stream, (const int32_t*)plin, n, v->d_slot_of, v->d_pslot + P0);
   DMF_LAUNCH_CHECK();
@@ -577,11 +578,11 @@ static float angle_threshold() {
 // ---- brick distance field (empty-space skipping in the reverse march) ---------
 // d(b) = min over occupied bricks q of max_axis |b - q| (L-inf, in bricks), capped.
 // L-inf distance is separable: three 1-D passes d' = min_t max(|t|, d(b + t e_axis)).
-__global__ void k_bdist_init(const uint32_t* __restrict__ brick, int64_t nbr, uint8_t* __restrict__ d) {
+__global__ void k_bdist_init(const uint32_t* __restrict__ brick, int64_t nbr, int cap, uint8_t* __restrict__ d) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nbr) d[i] = ((brick[i >> 5] >> (i & 31)) & 1u) ? 0 : kBrickDistCap;
+  if (i < nbr) d[i] = ((brick[i >> 5] >> (i & 31)) & 1u) ? 0 : (uint8_t)cap;
 }
-__global__ void k_bdist_pass(int nbx, int nby, int nbz, int axis, const uint8_t* __restrict__ src,
+__global__ void k_bdist_pass(int nbx, int nby, int nbz, int axis, int cap, const uint8_t* __restrict__ src,
                              uint8_t* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nbr = (int64_t)nbx * nby * nbz;
@@ -590,7 +591,7 @@ __global__ void k_bdist_pass(int nbx, int nby, int nbz, int axis, const uint8_t*
   const int c = axis == 0 ? x : (axis == 1 ? y : z), n = axis == 0 ? nbx : (axis == 1 ? nby : nbz);
   const int64_t stride = axis == 0 ? (int64_t)nby * nbz : (axis == 1 ? nbz : 1);
   int best = src[i];
-  for (int t = 1; t < best && t < kBrickDistCap; ++t) {
+  for (int t = 1; t < best && t < cap; ++t) {
     if (c - t >= 0) best = min(best, max(t, (int)src[i - t * stride]));
     if (c + t < n) best = min(best, max(t, (int)src[i + t * stride]));
   }
@@ -603,13 +604,13 @@ int ensure_brick_dist(dmf_volume* v) {
   uint8_t* a = v->d_bdist;
   uint8_t* b = v->d_bdist + nbr + 64;
   const dim3 blk(256), grd((unsigned)((nbr + 255) / 256));
-  hipLaunchKernelGGL(k_bdist_init, grd, blk, 0, v->stream, v->d_brick, nbr, a);
+  hipLaunchKernelGGL(k_bdist_init, grd, blk, 0, v->stream, v->d_brick, nbr, v->brick_cap, a);
   DMF_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bdist_pass, grd, blk, 0, v->stream, v->nb[0], v->nb[1], v->nb[2], 2, a, b);
+  hipLaunchKernelGGL(k_bdist_pass, grd, blk, 0, v->stream, v->nb[0], v->nb[1], v->nb[2], 2, v->brick_cap, a, b);
   DMF_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bdist_pass, grd, blk, 0, v->stream, v->nb[0], v->nb[1], v->nb[2], 1, b, a);
+  hipLaunchKernelGGL(k_bdist_pass, grd, blk, 0, v->stream, v->nb[0], v->nb[1], v->nb[2], 1, v->brick_cap, b, a);
   DMF_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bdist_pass, grd, blk, 0, v->stream, v->nb[0], v->nb[1], v->nb[2], 0, a, b);
+  hipLaunchKernelGGL(k_bdist_pass, grd, blk, 0, v->stream, v->nb[0], v->nb[1], v->nb[2], 0, v->brick_cap, a, b);
   DMF_LAUNCH_CHECK();
   DMF_HIP(hipMemcpyAsync(a, b, (size_t)nbr, hipMemcpyDeviceToDevice, v->stream));
   v->bdist_valid = true;
@@ -643,7 +644,7 @@ dmf::Geom dmf_volume::geom() const {
 
 dmf::DevVol dmf_volume::dev() const {
   DevVol d;
-  d.occ = d_occ; d.bdist = d_bdist;
+  d.occ = d_occ; d.bdist = d_bdist; d.bsh = brick_shift;
   d.brick = d_brick; d.nb[0] = nb[0]; d.nb[1] = nb[1]; d.nb[2] = nb[2]; d.slot_of = d_slot_of; d.hash = d_hash; d.off = d_off; d.nrm = d_csr_nrm;
   d.view = d_view; d.good = d_good; d.V = V;
   return d;
@@ -796,7 +797,13 @@ int dmf_volume_construct(dmf_volume* v) {
   if (v->ncell >= (size_t)0x7fffffff) return fail(DMF_ERR_RANGE, "more than 2^31-1 cells");
   DMF_HIP(hipMalloc((void**)&v->d_occ, sizeof(uint32_t) * ((v->ncell + 31) / 32 + 1)));
   DMF_HIP(hipMemsetAsync(v->d_occ, 0, sizeof(uint32_t) * ((v->ncell + 31) / 32 + 1), v->stream));
-  const int bs = 1 << kBrickShift;
+  {
+    const char* e = getenv("DMF_BRICK_SHIFT");  // experiments only; default 8^3 bricks
+    v->brick_shift = e ? std::max(0, std::min(5, atoi(e))) : kBrickShiftDefault;
+    const char* c = getenv("DMF_BRICK_CAP");
+    v->brick_cap = c ? std::max(1, std::min(255, atoi(c))) : kBrickDistCapDefault;
+  }
+  const int bs = 1 << v->brick_shift;
   v->nb[0] = (v->xdim + bs - 1) / bs; v->nb[1] = (v->ydim + bs - 1) / bs; v->nb[2] = (v->zdim + bs - 1) / bs;
   const size_t bwords = ((size_t)v->nb[0] * v->nb[1] * v->nb[2] + 31) / 32 + 1;
   DMF_HIP(hipMalloc((void**)&v->d_brick, sizeof(uint32_t) * bwords));

@@ -71,8 +71,8 @@ __device__ inline bool reverse_march(const Geom& g, const DevVol& vd, const floa
     if (!valid_coords(g, a, b, c)) return false;
     if (occ_test(vd.occ, lin_index(g, a, b, c))) return true;
     if (kSkip) {
-      const uint32_t bl = ((uint32_t)(a >> kBrickShift) * (uint32_t)vd.nb[1] + (uint32_t)(b >> kBrickShift)) *
-                              (uint32_t)vd.nb[2] + (uint32_t)(c >> kBrickShift);
+      const uint32_t bl = ((uint32_t)(a >> vd.bsh) * (uint32_t)vd.nb[1] + (uint32_t)(b >> vd.bsh)) *
+                              (uint32_t)vd.nb[2] + (uint32_t)(c >> vd.bsh);
       if (bl == known_full) continue;
       if (((vd.brick[bl >> 5] >> (bl & 31)) & 1u) == 0u) {
         // last depth still inside the brick along each moving axis (estimate)
@@ -81,8 +81,8 @@ __device__ inline bool reverse_march(const Geom& g, const DevVol& vd, const floa
 #pragma unroll
         for (int ax = 0; ax < 3; ++ax) {
           if (v[ax] == 0.0f) continue;
-          const int lo = (cell[ax] >> kBrickShift) << kBrickShift;
-          const int hi = min(lo + (1 << kBrickShift), g.n[ax]);  // exclusive
+          const int lo = (cell[ax] >> vd.bsh) << vd.bsh;
+          const int hi = min(lo + (1 << vd.bsh), g.n[ax]);  // exclusive
           const float face = (float)(g.mn[ax] + (double)(v[ax] > 0.0f ? hi : lo) * g.dl[ax]);
           fdmax = fminf(fdmax, (face - cen[ax]) * rv[ax]);
         }
@@ -94,8 +94,8 @@ __device__ inline bool reverse_march(const Geom& g, const DevVol& vd, const floa
           ++samples;
           if (valid_points(g, q[0], q[1], q[2])) {
             const int qa = bin_axis(g, 0, q[0]), qb = bin_axis(g, 1, q[1]), qc = bin_axis(g, 2, q[2]);
-            if ((qa >> kBrickShift) == (a >> kBrickShift) && (qb >> kBrickShift) == (b >> kBrickShift) &&
-                (qc >> kBrickShift) == (c >> kBrickShift) && valid_coords(g, qa, qb, qc)) {
+            if ((qa >> vd.bsh) == (a >> vd.bsh) && (qb >> vd.bsh) == (b >> vd.bsh) &&
+                (qc >> vd.bsh) == (c >> vd.bsh) && valid_coords(g, qa, qb, qc)) {
               s = j;  // samples s+1 .. j lie inside the empty brick
               continue;
             }
@@ -240,7 +240,7 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   const uint32_t lin = lin_index(g, a, b, c);
   if ((lin >> 5) != L.occi) { L.occi = lin >> 5; L.occw = vd.occ[L.occi]; }
   if ((L.occw >> (lin & 31)) & 1u) return 1;
-  const int ba = a >> kBrickShift, bb = b >> kBrickShift, bc = c >> kBrickShift;
+  const int ba = a >> vd.bsh, bb = b >> vd.bsh, bc = c >> vd.bsh;
   const uint32_t bl = ((uint32_t)ba * (uint32_t)vd.nb[1] + (uint32_t)bb) * (uint32_t)vd.nb[2] + (uint32_t)bc;
   if (bl != L.known_full) {
     const int d = vd.bdist[bl];
@@ -251,8 +251,8 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
       float fdmax = 3.0e38f;
 #pragma unroll
       for (int ax = 0; ax < 3; ++ax) {
-        clo[ax] = max(bx[ax] - R, 0) << kBrickShift;
-        chi[ax] = min((bx[ax] + R + 1) << kBrickShift, g.n[ax]);
+        clo[ax] = max(bx[ax] - R, 0) << vd.bsh;
+        chi[ax] = min((bx[ax] + R + 1) << vd.bsh, g.n[ax]);
         if (L.v[ax] == 0.0f) continue;
         const float face = (float)(g.mn[ax] + (double)(L.v[ax] > 0.0f ? chi[ax] : clo[ax]) * g.dl[ax]);
         fdmax = fminf(fdmax, (face - L.cen[ax]) * L.rv[ax]);
@@ -644,6 +644,10 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, const uint32_t* __restr
                                                  unsigned long long* __restrict__ stats) {
   stats = stat_slot(stats);
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // grid.y = pose index of a batched launch (one pose: grid.y = 1)
+  pose += blockIdx.y;
+  k_out += (int64_t)blockIdx.y * R * C;
+  slot_out += (int64_t)blockIdx.y * R * C;
   int64_t samples = 0;
   if (idx < (int64_t)R * C) {
     const int r = (int)(idx / C) * rdelta, c = (int)(idx % C) * cdelta;
@@ -1013,6 +1017,33 @@ __global__ void k_first_hit_hash(const int32_t* __restrict__ slot, const uint64_
                                  uint64_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = slot[i] >= 0 ? hash[slot[i]] : 0;
+}
+
+int dmf_forward_first_hits_device(dmf_volume* v, const dmf_camera* cam, const float* d_poses, int32_t P,
+                                  int32_t zstart, int32_t zdelta, int32_t rdelta, int32_t cdelta, int32_t* d_k,
+                                  int32_t* d_slot, uint64_t* d_stats) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  DMF_TRY(check_camera(cam));
+  if (!d_poses || !d_k || !d_slot) return fail(DMF_ERR_INVALID, "null argument");
+  if (P <= 0 || P > 65535) return fail(DMF_ERR_INVALID, "pose count %d out of range [1,65535]", P);
+  if (zdelta <= 0 || rdelta <= 0 || cdelta <= 0) return fail(DMF_ERR_INVALID, "bad strides");
+  PoseX* tab;
+  DMF_TRY(pose_table(v, d_poses, P, true, &tab));
+  const int R = (cam->height + rdelta - 1) / rdelta, C = (cam->width + cdelta - 1) / cdelta;
+  const int64_t RC = (int64_t)R * C;
+  void* aux;
+  DMF_TRY(scratch(v, kScHost2, 64, &aux));
+  DMF_HIP(hipMemsetAsync(aux, 0, 64, v->stream));
+  unsigned long long* st = nullptr;
+  if (d_stats) DMF_TRY(stats_begin(v, &st));
+  hipLaunchKernelGGL(k_forward, dim3((unsigned)((RC + 255) / 256), (unsigned)P), dim3(256), 0, v->stream, v->geom(),
+                     v->d_occ, v->d_slot_of, cam_params(cam), tab, zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot,
+                     (unsigned long long*)aux, st);
+  DMF_LAUNCH_CHECK();
+  if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 1));
+  return DMF_OK;
+  DMF_API_END
 }
 
 int dmf_forward_first_hits(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zstart, int32_t zdelta,

@@ -191,6 +191,11 @@ int dmf_ray_trace_and_get_good_points(dmf_volume* v, const dmf_camera* cam, cons
 int dmf_forward_first_hits(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t zstart,
                            int32_t zdelta, int32_t rdelta, int32_t cdelta, int32_t* k_out,
                            uint64_t* hash_out);
+/* Batched device form for P poses: d_k / d_slot P*R*C int32 (first-hit depth-plane index
+ * and occupied slot, -1 = none); d_stats (may be NULL) += {march samples}. */
+int dmf_forward_first_hits_device(dmf_volume* v, const dmf_camera* cam, const float* d_poses, int32_t P,
+                                  int32_t zstart, int32_t zdelta, int32_t rdelta, int32_t cdelta, int32_t* d_k,
+                                  int32_t* d_slot, uint64_t* d_stats);
 /* rayTraceVolume  RayTracingEngine.hpp:498-564 (depth_out: H*W int32 z-buffer or NULL). */
 int dmf_ray_trace_volume(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t* depth_out);
 /* willCollide  tests/CameraPathGen.cpp:128-156, for n segment pairs a[i] -> b[i]. */

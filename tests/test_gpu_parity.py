@@ -498,3 +498,35 @@ def test_golden_config1_gpu(dmf):
     assert np.array_equal(st, z["fuse_stats"])
     assert np.array_equal(sha(hits), z["fuse_hits_sha"]) and np.array_equal(sha(misses), z["fuse_misses_sha"])
     assert np.array_equal(sha(eng.fuse_finalize(vf, hits, misses)), z["fuse_logodds_sha"])
+
+
+def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
+    """dmf_forward_first_hits_device over P poses in one launch == the oracle per pose."""
+    import ctypes as C
+    from dmf_amd import _lib
+    ov = Hh.oracle_volume(oracle, n=100)
+    gv = Hh.gpu_volume(n=100)
+    poses = Hh.all_poses()[:5].astype(np.float32)
+    P, rd, cd = len(poses), 3, 2
+    R, Cc = (H + rd - 1) // rd, (W + cd - 1) // cd
+    L, h = gv._L, gv._h
+
+    def dmalloc(nbytes):
+        p = C.c_void_p()
+        _lib.check(L.dmf_device_malloc(h, C.addressof(p), nbytes))
+        return p.value
+    dp, dk, ds = dmalloc(poses.nbytes), dmalloc(4 * P * R * Cc), dmalloc(4 * P * R * Cc)
+    try:
+        _lib.check(L.dmf_memcpy_h2d(h, dp, poses.ctypes.data, poses.nbytes))
+        cam = _lib.make_camera(K, H, W)
+        _lib.check(L.dmf_forward_first_hits_device(h, C.addressof(cam), dp, P, 10, 10, rd, cd, dk, ds, None))
+        k = np.zeros(P * R * Cc, np.int32)
+        _lib.check(L.dmf_memcpy_d2h(h, k.ctypes.data, dk, k.nbytes))
+        k = k.reshape(P, -1)
+        for p in range(P):
+            ko, _ = oeng.forward_first_hits(ov, poses[p], 10, 10, rd, cd)
+            assert np.array_equal(k[p], np.asarray(ko).reshape(-1)), p
+        assert (k >= 0).any()
+    finally:
+        for p_ in (dp, dk, ds):
+            L.dmf_device_free(h, p_)
