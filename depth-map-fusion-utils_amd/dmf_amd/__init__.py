@@ -26,7 +26,7 @@ import numpy as np
 from . import _lib
 from ._lib import DmfError, check, load, ptr
 
-__all__ = ["Camera", "VoxelVolume", "RayTracingEngine", "DmfError", "degree", "FuseParams"]
+__all__ = ["Camera", "VoxelVolume", "RayTracingEngine", "OccupancyGrid", "DmfError", "degree", "FuseParams"]
 
 
 def degree(radian):
@@ -426,3 +426,79 @@ def will_collide(volume, a, b):
     out = np.zeros(a.shape[0], np.uint8)
     check(volume._L.dmf_will_collide(volume._h, ptr(a), ptr(b), a.shape[0], ptr(out)))
     return out.astype(bool)
+
+
+class OccupancyGrid:
+    """OccupancyGrid.hpp:50-318 on the GPU (dmf_ogrid_*): same setup sequence
+    (setDimensions, setResolution, setK, construct), updateStates(cloud, normals) and the
+    download calls.  updateStates gives the deterministic single-threaded result."""
+
+    def __init__(self, device=0):
+        self._L = load()
+        h = C.c_void_p()
+        check(self._L.dmf_ogrid_create(C.addressof(h), int(device)))
+        self._h = h
+        self._b = None
+        self._r = None
+        self.k_ = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.dmf_ogrid_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def setDimensions(self, xmin, xmax, ymin, ymax, zmin, zmax):
+        self._b = np.array([xmin, xmax, ymin, ymax, zmin, zmax], np.float64)
+
+    def setResolution(self, x, y, z):
+        self._r = (float(np.float32(x)), float(np.float32(y)), float(np.float32(z)))
+
+    def setK(self, k):
+        self.k_ = int(k)
+
+    def construct(self):
+        check(self._L.dmf_ogrid_setup(self._h, ptr(self._b), *self._r, self.k_))
+        return True
+
+    @property
+    def dims(self):
+        d = np.zeros(3, np.int32)
+        check(self._L.dmf_ogrid_get_dims(self._h, ptr(d)))
+        return tuple(int(x) for x in d)
+
+    def updateStates(self, cloud, normals):
+        """cloud (n,3) xyz; normals (m,6) x y z nx ny nz (PointNormal)."""
+        cloud = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
+        normals = np.ascontiguousarray(normals, np.float32).reshape(-1, 6)
+        check(self._L.dmf_ogrid_update_states(self._h, ptr(cloud), cloud.shape[0], ptr(normals), normals.shape[0]))
+        return True
+
+    def state(self):
+        n = int(np.prod(self.dims))
+        nrm, cen = np.zeros(3 * n, np.float32), np.zeros(3 * n, np.float32)
+        cnt, fl = np.zeros(n, np.int32), np.zeros(n, np.uint8)
+        check(self._L.dmf_ogrid_state(self._h, ptr(nrm), ptr(cen), ptr(cnt), ptr(fl)))
+        return nrm.reshape(-1, 3), cen.reshape(-1, 3), cnt, fl
+
+    def _download(self, mode):
+        n = C.c_int64()
+        st = self._L.dmf_ogrid_download(self._h, mode, None, 0, C.addressof(n))
+        if st not in (0, _lib.DMF_ERR_CAPACITY):
+            check(st)
+        out = np.zeros(6 * max(n.value, 1), np.float32)
+        check(self._L.dmf_ogrid_download(self._h, mode, ptr(out), n.value, C.addressof(n)))
+        return out[:6 * n.value].reshape(-1, 6)
+
+    def downloadCloud(self):
+        """(n, 6) centroid xyz + normal of occupied voxels, x-major (:166-193)."""
+        return self._download(0)
+
+    def downloadHQCloud(self):
+        """as downloadCloud for voxels with count > 100 (:283-318)."""
+        return self._download(1)

@@ -104,6 +104,15 @@ SIGNATURES = {
     "dmf_fuse_finalize_device": (C.c_int, [_vp, _p, _p, _p, _p]),
     "dmf_fuse_counter_cells": (C.c_int, [_vp, _p]),
     "dmf_fuse_counters_to_linear_device": (C.c_int, [_vp, _p, _p]),
+    "dmf_ogrid_create": (C.c_int, [_p, _i32]),
+    "dmf_ogrid_destroy": (C.c_int, [_vp]),
+    "dmf_ogrid_set_stream": (C.c_int, [_vp, _vp]),
+    "dmf_ogrid_setup": (C.c_int, [_vp, _p, C.c_float, C.c_float, C.c_float, _i32]),
+    "dmf_ogrid_get_dims": (C.c_int, [_vp, _p]),
+    "dmf_ogrid_update_states": (C.c_int, [_vp, _p, _i64, _p, _i64]),
+    "dmf_ogrid_update_states_device": (C.c_int, [_vp, _p, _i64, _p, _i64]),
+    "dmf_ogrid_state": (C.c_int, [_vp, _p, _p, _p, _p]),
+    "dmf_ogrid_download": (C.c_int, [_vp, _i32, _p, _i64, _p]),
     "dmf_device_malloc": (C.c_int, [_vp, _p, C.c_size_t]),
     "dmf_device_free": (C.c_int, [_vp, _vp]),
     "dmf_memcpy_h2d": (C.c_int, [_vp, _vp, _p, C.c_size_t]),

@@ -227,6 +227,30 @@ int dmf_fuse_finalize(dmf_volume* v, const int32_t* hits, const int32_t* misses,
 int dmf_fuse_finalize_device(dmf_volume* v, const int32_t* d_hits, const int32_t* d_misses,
                              const dmf_fuse_params* prm, int16_t* d_logodds);
 
+/* ---- OccupancyGrid  (include/OccupancyGrid.hpp:50-318) ----------------------- */
+/* The reference's second fusion path.  updateStates is computed in the deterministic
+ * single-threaded order (the reference's OpenMP loops race); state is dense, x-major,
+ * persistent across calls. */
+typedef struct dmf_ogrid dmf_ogrid;
+int dmf_ogrid_create(dmf_ogrid** out, int32_t device);
+int dmf_ogrid_destroy(dmf_ogrid* g);
+int dmf_ogrid_set_stream(dmf_ogrid* g, void* hip_stream);
+/* setDimensions(bounds[6]) + setResolution(float x3) + setK + construct (:323-352). */
+int dmf_ogrid_setup(dmf_ogrid* g, const double* bounds, float xres, float yres, float zres, int32_t k);
+int dmf_ogrid_get_dims(const dmf_ogrid* g, int32_t* dims);
+/* updateStates(cloud, normals) (:99-164): cloud n_cloud x 3 floats, normals n_normals x 6
+ * floats (x, y, z, nx, ny, nz).  Host and device-pointer forms. */
+int dmf_ogrid_update_states(dmf_ogrid* g, const float* cloud, int64_t n_cloud, const float* normals,
+                            int64_t n_normals);
+int dmf_ogrid_update_states_device(dmf_ogrid* g, const float* d_cloud, int64_t n_cloud, const float* d_normals,
+                                   int64_t n_normals);
+/* Dense state copies (any may be NULL): normal / centroid 3 floats per voxel, count,
+ * flags (bit 0 occupied, bit 1 normal_found). */
+int dmf_ogrid_state(const dmf_ogrid* g, float* normal, float* centroid, int32_t* count, uint8_t* flags);
+/* mode 0 downloadCloud (:166-193), 1 downloadHQCloud (count > 100, :283-318): occupied
+ * voxels in x-major order as (cx, cy, cz, nx, ny, nz).  DMF_ERR_CAPACITY (n set) if n > cap. */
+int dmf_ogrid_download(dmf_ogrid* g, int32_t mode, float* out, int64_t cap, int64_t* n);
+
 /* ---- device memory helpers for callers without their own allocator ---------- */
 int dmf_device_malloc(dmf_volume* v, void** d_ptr, size_t bytes);
 int dmf_device_free(dmf_volume* v, void* d_ptr);

@@ -918,6 +918,126 @@ int32_t orc_greedy_set_cover(const uint64_t* hashes, const int64_t* counts, int3
   return nsel;
 }
 
+// ---- OccupancyGrid (include/OccupancyGrid.hpp:50-318), sequential semantics -------
+// The reference runs updateStates' loops under OpenMP with racy read-modify-writes;
+// the deterministic result it approximates is the single-threaded order restated here
+// (points in cloud order, offsets i, j, k from -K..K).  Dense per-voxel state in the
+// reference's x-major order.
+struct orc_ogrid {
+  double xmin_ = 0, xmax_ = 0, ymin_ = 0, ymax_ = 0, zmin_ = 0, zmax_ = 0;
+  double xres_ = 0, yres_ = 0, zres_ = 0;
+  int xdim_ = 0, ydim_ = 0, zdim_ = 0, k_ = 0;
+  std::vector<float> normal, centroid;  // 3 per voxel
+  std::vector<int32_t> count;
+  std::vector<uint8_t> occupied, normal_found;
+  size_t idx(int x, int y, int z) const { return ((size_t)x * ydim_ + y) * zdim_ + z; }
+  bool valid_coords(int x, int y, int z) const {  // :399-402
+    return x < xdim_ && y < ydim_ && z < zdim_ && x >= 0 && y >= 0 && z >= 0;
+  }
+  void coords(const float p[3], int& x, int& y, int& z) const {  // :373-379
+    x = (int)std::floor(((double)p[0] - xmin_) / xres_);
+    y = (int)std::floor(((double)p[1] - ymin_) / yres_);
+    z = (int)std::floor(((double)p[2] - zmin_) / zres_);
+  }
+};
+
+orc_ogrid* orc_ogrid_new() { return new orc_ogrid(); }
+void orc_ogrid_free(orc_ogrid* g) { delete g; }
+void orc_ogrid_setup(orc_ogrid* g, const double* bounds, float xr, float yr, float zr, int k) {
+  g->xmin_ = bounds[0]; g->xmax_ = bounds[1]; g->ymin_ = bounds[2];  // :323-336
+  g->ymax_ = bounds[3]; g->zmin_ = bounds[4]; g->zmax_ = bounds[5];
+  g->xres_ = xr; g->yres_ = yr; g->zres_ = zr;                       // :338-343 (float params)
+  g->k_ = k;                                                          // setK
+  g->xdim_ = (int)((g->xmax_ - g->xmin_) / g->xres_);                 // :345-352 construct
+  g->ydim_ = (int)((g->ymax_ - g->ymin_) / g->yres_);
+  g->zdim_ = (int)((g->zmax_ - g->zmin_) / g->zres_);
+  const size_t n = (size_t)g->xdim_ * g->ydim_ * g->zdim_;
+  g->normal.assign(3 * n, 0.f); g->centroid.assign(3 * n, 0.f);
+  g->count.assign(n, 0); g->occupied.assign(n, 0); g->normal_found.assign(n, 0);
+}
+void orc_ogrid_dims(const orc_ogrid* g, int32_t* d) { d[0] = g->xdim_; d[1] = g->ydim_; d[2] = g->zdim_; }
+
+// :88-98 projectPointToVector (float; the double ball_radius is applied as float)
+static void project_to_vector(const float pt[3], const float np[3], const float n[3], float out[3]) {
+  const float br = (float)0.015;
+  float a[3], b[3], ap[3], ab[3];
+  for (int i = 0; i < 3; ++i) {
+    const float d = n[i] * br;
+    a[i] = np[i] - d;
+    b[i] = np[i] + d;
+  }
+  for (int i = 0; i < 3; ++i) { ap[i] = a[i] - pt[i]; ab[i] = a[i] - b[i]; }
+  const float s = sum3(ap[0] * ab[0], ap[1] * ab[1], ap[2] * ab[2]) / sum3(ab[0] * ab[0], ab[1] * ab[1], ab[2] * ab[2]);
+  for (int i = 0; i < 3; ++i) out[i] = a[i] - s * ab[i];
+}
+
+// :99-164 updateStates(cloud, normals): cloud = n_cloud x 3 floats, normals = n_nrm x 6
+// floats (x, y, z, nx, ny, nz).
+void orc_ogrid_update(orc_ogrid* g, const float* cloud, int64_t n_cloud, const float* pn, int64_t n_nrm) {
+  const int K = g->k_;
+  for (int64_t p = 0; p < n_nrm; ++p) {
+    const float* q = pn + 6 * p;
+    int x, y, z;
+    g->coords(q, x, y, z);
+    for (int i = -K; i <= K; ++i)
+      for (int j = -K; j <= K; ++j)
+        for (int k = -K; k <= K; ++k) {
+          if (!g->valid_coords(x + i, y + j, z + k)) continue;
+          const size_t v = g->idx(x + i, y + j, z + k);
+          float s[3] = {g->normal[3 * v] + q[3], g->normal[3 * v + 1] + q[4], g->normal[3 * v + 2] + q[5]};
+          normalized(s, &g->normal[3 * v]);
+          g->normal_found[v] = 1;
+        }
+  }
+  for (int64_t p = 0; p < n_cloud; ++p) {
+    const float* pt = cloud + 3 * p;
+    int x, y, z;
+    g->coords(pt, x, y, z);
+    for (int i = -K; i <= K; ++i)
+      for (int j = -K; j <= K; ++j)
+        for (int k = -K; k <= K; ++k) {
+          if (!g->valid_coords(x + i, y + j, z + k)) continue;
+          const size_t v = g->idx(x + i, y + j, z + k);
+          if (!g->normal_found[v]) continue;
+          const float c[3] = {(float)(g->xmin_ + g->xres_ * (x + i) + g->xres_ / 2.0),
+                              (float)(g->ymin_ + g->yres_ * (y + j) + g->yres_ / 2.0),
+                              (float)(g->zmin_ + g->zres_ * (z + k) + g->zres_ / 2.0)};
+          float pr[3];
+          project_to_vector(pt, c, &g->normal[3 * v], pr);
+          const float d[3] = {pt[0] - pr[0], pt[1] - pr[1], pt[2] - pr[2]};
+          const float dist = std::sqrt(sum3(d[0] * d[0], d[1] * d[1], d[2] * d[2]));
+          if ((double)dist < 0.001) {
+            const int cnt = ++g->count[v];
+            for (int a = 0; a < 3; ++a) g->centroid[3 * v + a] += (pr[a] - g->centroid[3 * v + a]) / (float)cnt;
+          }
+        }
+    if (g->valid_coords(x, y, z)) g->occupied[g->idx(x, y, z)] = 1;
+  }
+}
+
+// Dense state copy (normal, centroid: 3 floats; count; occupied | normal_found << 1).
+void orc_ogrid_state(const orc_ogrid* g, float* normal, float* centroid, int32_t* count, uint8_t* flags) {
+  const size_t n = g->count.size();
+  std::memcpy(normal, g->normal.data(), sizeof(float) * 3 * n);
+  std::memcpy(centroid, g->centroid.data(), sizeof(float) * 3 * n);
+  std::memcpy(count, g->count.data(), sizeof(int32_t) * n);
+  for (size_t i = 0; i < n; ++i) flags[i] = (uint8_t)(g->occupied[i] | (g->normal_found[i] << 1));
+}
+
+// :166-193 downloadCloud (mode 0) / :283-318 downloadHQCloud (mode 1): occupied voxels
+// in x-major order as (cx, cy, cz, nx, ny, nz).  Returns the count (writes <= cap).
+int64_t orc_ogrid_download(const orc_ogrid* g, int mode, float* out, int64_t cap) {
+  int64_t n = 0;
+  for (size_t v = 0; v < g->count.size(); ++v) {
+    if (!g->occupied[v]) continue;
+    if (mode == 1 && !(g->count[v] > 100)) continue;
+    if (n < cap)
+      for (int a = 0; a < 3; ++a) { out[6 * n + a] = g->centroid[3 * v + a]; out[6 * n + 3 + a] = g->normal[3 * v + a]; }
+    ++n;
+  }
+  return n;
+}
+
 // Clamped fixed-point log-odds (milli-logit units) from the exact counts.
 void orc_fuse_finalize(int64_t n, const int32_t* hits, const int32_t* misses, int l_hit, int l_miss,
                        int l_min, int l_max, int16_t* out) {

@@ -368,3 +368,66 @@ def fuse_finalize(hits, misses, l_hit=847, l_miss=-405, l_min=-2000, l_max=3511)
     lib().orc_fuse_finalize(hits.size, np.ascontiguousarray(hits, np.int32),
                             np.ascontiguousarray(misses, np.int32), l_hit, l_miss, l_min, l_max, out)
     return out
+
+
+class OccupancyGrid:
+    """OccupancyGrid.hpp:50-318 restated (sequential order), dense state."""
+
+    def __init__(self):
+        L = lib()
+        for name, res, args in (("orc_ogrid_new", _vp, []), ("orc_ogrid_free", None, [_vp]),
+                                ("orc_ogrid_setup", None, [_vp, _f64p, C.c_float, C.c_float, C.c_float, C.c_int]),
+                                ("orc_ogrid_dims", None, [_vp, _i32p]),
+                                ("orc_ogrid_update", None, [_vp, _f32p, C.c_int64, _f32p, C.c_int64]),
+                                ("orc_ogrid_state", None, [_vp, _f32p, _f32p, _i32p, _u8p]),
+                                ("orc_ogrid_download", C.c_int64, [_vp, C.c_int, _f32p, C.c_int64])):
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, args
+        self._L = L
+        self._h = L.orc_ogrid_new()
+        self._b = None
+        self._r = None
+        self._k = 0
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.orc_ogrid_free(self._h)
+            self._h = None
+
+    def setDimensions(self, xmin, xmax, ymin, ymax, zmin, zmax):
+        self._b = np.array([xmin, xmax, ymin, ymax, zmin, zmax], np.float64)
+
+    def setResolution(self, x, y, z):
+        self._r = (np.float32(x), np.float32(y), np.float32(z))
+
+    def setK(self, k):
+        self._k = int(k)
+
+    def construct(self):
+        self._L.orc_ogrid_setup(self._h, self._b, *self._r, self._k)
+        return True
+
+    @property
+    def dims(self):
+        d = np.zeros(3, np.int32)
+        self._L.orc_ogrid_dims(self._h, d)
+        return tuple(int(x) for x in d)
+
+    def updateStates(self, cloud, normals):
+        cloud = np.ascontiguousarray(cloud, np.float32).reshape(-1, 3)
+        normals = np.ascontiguousarray(normals, np.float32).reshape(-1, 6)
+        self._L.orc_ogrid_update(self._h, cloud, cloud.shape[0], normals, normals.shape[0])
+        return True
+
+    def state(self):
+        n = int(np.prod(self.dims))
+        nrm, cen = np.zeros(3 * n, np.float32), np.zeros(3 * n, np.float32)
+        cnt, fl = np.zeros(n, np.int32), np.zeros(n, np.uint8)
+        self._L.orc_ogrid_state(self._h, nrm, cen, cnt, fl)
+        return nrm.reshape(-1, 3), cen.reshape(-1, 3), cnt, fl
+
+    def download(self, mode=0):
+        n = self._L.orc_ogrid_download(self._h, mode, np.zeros(6, np.float32), 0)
+        out = np.zeros(6 * max(n, 1), np.float32)
+        self._L.orc_ogrid_download(self._h, mode, out, n)
+        return out[:6 * n].reshape(-1, 6)

@@ -1,6 +1,7 @@
 """CPU: the C-ABI library loads and exports every symbol include/dmf.h declares
 (no compute: there is no GPU here), and fails loudly without a device."""
 import ctypes as C
+import os
 
 import pytest
 
@@ -39,3 +40,40 @@ def test_null_arguments_rejected():
     assert L.dmf_volume_get_info(None, None) == _lib.DMF_ERR_INVALID
     assert L.dmf_device_count(None) == _lib.DMF_ERR_INVALID
     assert L.dmf_volume_destroy(None) == 0
+
+
+def test_compat_headers_compile(tmp_path):
+    """The C++ drop-in headers (compat/) compile without Eigen/PCL, including the
+    OccupancyGrid and Algorithms mirrors (g++ -fsyntax-only; no GPU needed)."""
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    compat = os.path.join(root, "depth-map-fusion-utils_amd", "compat")
+    src = tmp_path / "use.cpp"
+    src.write_text('''
+#include "Algorithms.hpp"
+#include "Camera.hpp"
+#include "OccupancyGrid.hpp"
+#include "RayTracingEngine.hpp"
+#include "Volume.hpp"
+int main() {
+  OccupancyGrid g;
+  g.setDimensions(-1, 1, -1, 1, -1, 1);
+  g.setResolution(0.05f, 0.05f, 0.05f);
+  g.setK(1);
+  g.construct();
+  auto c = std::make_shared<pcl::PointCloud<pcl::PointXYZRGB>>();
+  auto n = std::make_shared<pcl::PointCloud<pcl::PointNormal>>();
+  g.updateStates(c, n);
+  auto out = std::make_shared<pcl::PointCloud<pcl::PointXYZRGBNormal>>();
+  g.downloadHQCloud(out);
+  VoxelVolume v;
+  std::vector<std::vector<unsigned long long int>> sets;
+  auto sel = Algorithms::greedySetCover(v, sets);
+  return (int)(out->points.size() + sel.size());
+}
+''')
+    gxx = shutil.which("g++")
+    assert gxx, "g++ is part of the image"
+    subprocess.run([gxx, "-std=c++17", "-fsyntax-only", "-Wall", "-I", compat, "-I", os.path.join(root, "include"),
+                    str(src)], check=True, capture_output=True, text=True)
