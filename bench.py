@@ -338,7 +338,33 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16
     _lib.check(L.dmf_greedy_set_cover_masks_device(vol._h, good.data_ptr(), P, words, 5, sel.ctypes.data,
                                                    C.addressof(nsel)))
     cover_ms = (time.perf_counter() - t0) * 1e3
+    # Planner::run_tsp cost map (tests/CameraPathGen.cpp:310-331): willCollide over all
+    # ordered pairs of 1024 camera centres on a 0.45 m sphere inside the volume (the
+    # createCameraLocationsFromSphere layout), one launch
+    Vc = 1024
+    rng = np.random.default_rng(11)
+    dirs = rng.normal(size=(Vc, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    cp = np.tile(np.eye(3, 4, dtype=np.float32).reshape(1, 12), (Vc, 1))
+    cp[:, 3::4] = (0.45 * dirs).astype(np.float32)
+    d_cp = torch.from_numpy(cp).to(dev)
+    cmap = torch.empty((Vc, Vc), dtype=torch.int32, device=dev)
+
+    def costmap():
+        _lib.check(L.dmf_collision_cost_map_device(vol._h, d_cp.data_ptr(), Vc, cmap.data_ptr()))
+    costmap()
+    torch.cuda.synchronize(dev)
+    h0 = torch.cuda.Event(enable_timing=True)
+    h1 = torch.cuda.Event(enable_timing=True)
+    h0.record(stream)
+    costmap()
+    h1.record(stream)
+    torch.cuda.synchronize(dev)
+    cm_ms = h0.elapsed_time(h1)
+    collided = int((cmap == 0x7FFFFFFF).sum().item())
     return {"greedy_set_cover": {"candidates": P, "selected": int(nsel.value), "ms": cover_ms},
+            "collision_cost_map": {"centres": Vc, "pairs": Vc * Vc, "collided_pairs": collided, "ms": cm_ms,
+                                   "pairs_per_s": Vc * Vc / (cm_ms * 1e-3)},
             "forward_first_hits": forward,
             "reverse_ray_trace_fast": {
         "occupied_voxels": int(V), "poses": P, "ms_per_batch": ms,

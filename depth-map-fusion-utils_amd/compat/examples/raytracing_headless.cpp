@@ -19,6 +19,7 @@
 
 #include "Algorithms.hpp"
 #include "Camera.hpp"
+#include "PathPlanning.hpp"
 #include "RayTracingEngine.hpp"
 #include "Volume.hpp"
 
@@ -118,6 +119,19 @@ int main(int argc, char** argv) {
   for (auto s : cameras_selected) cout << " " << s;
   cout << "\nselected_from_sets";
   for (auto s : again) cout << " " << s;
+  cout << "\n";
+  // tests/CameraPathGen.cpp:310-331 run_tsp cost map over the camera centres
+  auto map = PathPlanning::collisionCostMap(volume, camera_locations);
+  cout << "costmap";
+  for (auto& row : map)
+    for (int m : row) cout << " " << m;
+  cout << "\ncollide_from_0";
+  for (auto& T : camera_locations) {
+    Eigen::Vector3f a, b;
+    a << camera_locations[0](0, 3), camera_locations[0](1, 3), camera_locations[0](2, 3);
+    b << T(0, 3), T(1, 3), T(2, 3);
+    cout << " " << PathPlanning::willCollide(volume, a, b);
+  }
   cout << "\n";
   return 0;
 }

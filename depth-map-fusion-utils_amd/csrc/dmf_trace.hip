@@ -914,6 +914,67 @@ __global__ void k_will_collide(Geom g, const uint32_t* __restrict__ occ, const f
   out[i] = collided ? 1 : 0;
 }
 
+// Planner::run_tsp cost map (tests/CameraPathGen.cpp:310-331): all V*V ordered pairs
+// of camera centres, map = INT_MAX if willCollide(a, b) else int(|a-b| * 1000).
+// willCollide's loop only ever sets `collided`, so its result is the OR over depths
+// 1..floor(distance*1000) of "sample valid and occupied": one wave per pair, lane l
+// tests depth base+l, a ballot ends the pair at the first occupied 64-depth group.
+// Every lane evaluates the same float expressions as the scalar loop, so the OR is
+// bit-identical to the sequential march and there is no per-lane length divergence.
+// Pairs whose segment the reference cannot march (non-finite, or more than INT_MAX
+// depths: the int counter overflows) get -1.
+constexpr int kCostWaves = 4;
+constexpr int32_t kMaxCostPoses = 46340;  // V*V int32 entries < 2^31
+__global__ __launch_bounds__(64 * kCostWaves) void k_cost_map(Geom g, const uint32_t* __restrict__ occ,
+                                                              const float* __restrict__ poses, int32_t V,
+                                                              int32_t* __restrict__ map) {
+  const int64_t pair = (int64_t)blockIdx.x * kCostWaves + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (pair >= (int64_t)V * V) return;
+  const int64_t i = pair / V, j = pair - i * V;
+  const float a[3] = {poses[12 * i + 3], poses[12 * i + 7], poses[12 * i + 11]};
+  const float b[3] = {poses[12 * j + 3], poses[12 * j + 7], poses[12 * j + 11]};
+  const float ab[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+  const double distance = (double)sqrtf(sum3(ab[0] * ab[0], ab[1] * ab[1], ab[2] * ab[2]));
+  const double lim = distance * 1000;
+  if (!(lim < 2147483647.0)) {  // NaN or an overflowing depth counter
+    if (lane == 0) map[pair] = -1;
+    return;
+  }
+  const float ba[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  float v[3];
+  normalized(ba, v);
+  bool collided = false;
+  for (int64_t base = 1; (double)base <= lim; base += 64) {
+    const int64_t depth = base + lane;
+    bool hit = false;
+    if ((double)depth <= lim) {
+      const float fd = (float)depth;
+      const float px = a[0] + ((v[0] * fd) / 1000.0f);
+      const float py = a[1] + ((v[1] * fd) / 1000.0f);
+      const float pz = a[2] + ((v[2] * fd) / 1000.0f);
+      if (valid_points(g, px, py, pz)) {
+        const int x = bin_axis(g, 0, px), y = bin_axis(g, 1, py), z = bin_axis(g, 2, pz);
+        hit = valid_coords(g, x, y, z) && occ_test(occ, lin_index(g, x, y, z));
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(hit)) {
+      collided = true;
+      break;
+    }
+  }
+  if (lane == 0) map[pair] = collided ? 0x7fffffff : to_int_x86(distance * 1000);
+}
+
+static int cost_map(dmf_volume* v, const float* d_poses, int32_t V, int32_t* d_map) {
+  const int64_t pairs = (int64_t)V * V;
+  if (pairs == 0) return DMF_OK;
+  hipLaunchKernelGGL(k_cost_map, dim3((unsigned)((pairs + kCostWaves - 1) / kCostWaves)), dim3(64 * kCostWaves), 0,
+                     v->stream, v->geom(), v->d_occ, d_poses, V, d_map);
+  DMF_LAUNCH_CHECK();
+  return DMF_OK;
+}
+
 }  // namespace dmf
 
 using namespace dmf;
@@ -1138,6 +1199,35 @@ int dmf_will_collide(dmf_volume* v, const float* a, const float* b, int64_t n, u
   DMF_HIP(hipMemcpyAsync(collided, dout, n, hipMemcpyDeviceToHost, v->stream));
   DMF_HIP(hipStreamSynchronize(v->stream));
   return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_collision_cost_map(dmf_volume* v, const float* poses, int32_t V, int32_t* map) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  if (V < 0 || V > kMaxCostPoses || (V > 0 && (!poses || !map))) return fail(DMF_ERR_INVALID, "bad arguments");
+  if (V == 0) return DMF_OK;
+  for (int64_t i = 0; i < V; ++i)
+    for (int k = 3; k < 12; k += 4)
+      if (!std::isfinite(poses[12 * i + k]))
+        return fail(DMF_ERR_INVALID, "non-finite camera centre (the reference never terminates)");
+  const int64_t pairs = (int64_t)V * V;
+  void *dp, *dm;
+  DMF_TRY(scratch(v, kScPoses, sizeof(float) * 12 * V, &dp));
+  DMF_TRY(scratch(v, kScOut0, sizeof(int32_t) * pairs, &dm));
+  DMF_HIP(hipMemcpyAsync(dp, poses, sizeof(float) * 12 * V, hipMemcpyHostToDevice, v->stream));
+  DMF_TRY(cost_map(v, (const float*)dp, V, (int32_t*)dm));
+  DMF_HIP(hipMemcpyAsync(map, dm, sizeof(int32_t) * pairs, hipMemcpyDeviceToHost, v->stream));
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_collision_cost_map_device(dmf_volume* v, const float* d_poses, int32_t V, int32_t* d_map) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  if (V < 0 || V > kMaxCostPoses || (V > 0 && (!d_poses || !d_map))) return fail(DMF_ERR_INVALID, "bad arguments");
+  return cost_map(v, d_poses, V, d_map);
   DMF_API_END
 }
 

@@ -428,6 +428,16 @@ def will_collide(volume, a, b):
     return out.astype(bool)
 
 
+def collision_cost_map(volume, poses):
+    """Planner::run_tsp cost map (tests/CameraPathGen.cpp:310-331): (V, V) int32 over the
+    camera centres of `poses` (V x 3x4), INT_MAX where willCollide, else int(dist * 1000)."""
+    poses = np.ascontiguousarray(poses, np.float32).reshape(-1, 12)
+    V = poses.shape[0]
+    out = np.zeros((V, V), np.int32)
+    check(volume._L.dmf_collision_cost_map(volume._h, ptr(poses), V, ptr(out)))
+    return out
+
+
 class OccupancyGrid:
     """OccupancyGrid.hpp:50-318 on the GPU (dmf_ogrid_*): same setup sequence
     (setDimensions, setResolution, setK, construct), updateStates(cloud, normals) and the

@@ -95,6 +95,8 @@ SIGNATURES = {
     "dmf_forward_first_hits": (C.c_int, [_vp, _p, _p, _i32, _i32, _i32, _i32, _p, _p]),
     "dmf_ray_trace_volume": (C.c_int, [_vp, _p, _p, _p]),
     "dmf_will_collide": (C.c_int, [_vp, _p, _p, _i64, _p]),
+    "dmf_collision_cost_map": (C.c_int, [_vp, _p, _i32, _p]),
+    "dmf_collision_cost_map_device": (C.c_int, [_vp, _p, _i32, _p]),
     "dmf_forward_first_hits_device": (C.c_int, [_vp, _p, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p]),
     "dmf_greedy_set_cover": (C.c_int, [_vp, _p, _p, _i32, _i32, _p, _p]),
     "dmf_greedy_set_cover_masks_device": (C.c_int, [_vp, _p, _i32, _i64, _i32, _p, _p]),

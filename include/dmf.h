@@ -200,6 +200,13 @@ int dmf_forward_first_hits_device(dmf_volume* v, const dmf_camera* cam, const fl
 int dmf_ray_trace_volume(dmf_volume* v, const dmf_camera* cam, const float* pose, int32_t* depth_out);
 /* willCollide  tests/CameraPathGen.cpp:128-156, for n segment pairs a[i] -> b[i]. */
 int dmf_will_collide(dmf_volume* v, const float* a, const float* b, int64_t n, uint8_t* collided);
+/* Planner::run_tsp cost map  tests/CameraPathGen.cpp:310-331 (also CameraMotionTSP.cpp:
+ * 291-306): for all V*V ordered pairs of camera centres (translation of poses[i], P*12
+ * floats) map[i*V+j] = INT_MAX if willCollide(c_i, c_j) else int(|c_i - c_j| * 1000).
+ * V <= 46340.  Device form: a pair the reference cannot march (non-finite centre, or a
+ * segment over INT_MAX mm) gets -1; the host form rejects non-finite centres. */
+int dmf_collision_cost_map(dmf_volume* v, const float* poses, int32_t V, int32_t* map);
+int dmf_collision_cost_map_device(dmf_volume* v, const float* d_poses, int32_t V, int32_t* d_map);
 
 /* ---- 3D-DDA log-odds fusion (new capability) ------------------ */
 /* Host form: depth P*H*W uint16 mm, poses P*12; hits/misses: xdim*ydim*zdim int32 in

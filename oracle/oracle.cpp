@@ -23,6 +23,7 @@
 // integratePointCloud binning (Volume.hpp:199-228) of the ray endpoint.
 // =============================================================================
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -696,6 +697,23 @@ int orc_will_collide(orc_volume* vol, const float* a, const float* b) {
     if (vol->voxels_[x][y][z] != nullptr) collided = true;
   }
   return collided ? 1 : 0;
+}
+
+// tests/CameraPathGen.cpp:310-331 Planner::run_tsp cost map over all V*V ordered pairs
+// of camera centres (pose translations); euclideanDistance is CameraPathGen.cpp:56-59.
+void orc_collision_cost_map(orc_volume* vol, const float* poses, int V, int32_t* map) {
+  for (int i = 0; i < V; i++)
+    for (int j = 0; j < V; j++) {
+      const float a[3] = {poses[12 * i + 3], poses[12 * i + 7], poses[12 * i + 11]};
+      const float b[3] = {poses[12 * j + 3], poses[12 * j + 7], poses[12 * j + 11]};
+      if (orc_will_collide(vol, a, b)) {
+        map[(int64_t)i * V + j] = INT_MAX;
+      } else {
+        const float ab[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+        const double d = std::sqrt(sum3(ab[0] * ab[0], ab[1] * ab[1], ab[2] * ab[2]));
+        map[(int64_t)i * V + j] = (int)(d * 1000);
+      }
+    }
 }
 
 // ============================================================================

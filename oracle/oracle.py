@@ -82,6 +82,7 @@ def lib():
                                           C.c_int, _i32p, _u64p]),
         "orc_ray_trace_volume": (None, [_vp, _f32p, C.c_int, C.c_int, _f32p, _i32p]),
         "orc_will_collide": (C.c_int, [_vp, _f32p, _f32p]),
+        "orc_collision_cost_map": (None, [_vp, _f32p, C.c_int, _i32p]),
         "orc_fuse_depth": (None, [_vp, _f32p, C.c_int, C.c_int, _u16p, _f32p, C.c_int, C.c_int, C.c_int,
                                   _i32p, _i32p, _i64p]),
         "orc_fuse_finalize": (None, [C.c_int64, _i32p, _i32p, C.c_int, C.c_int, C.c_int, C.c_int, _i16p]),
@@ -320,6 +321,15 @@ class Engine:
 def will_collide(vol, a, b):
     """tests/CameraPathGen.cpp:128-156."""
     return bool(lib().orc_will_collide(vol._h, _f32(a, 3), _f32(b, 3)))
+
+
+def collision_cost_map(vol, poses):
+    """tests/CameraPathGen.cpp:310-331 run_tsp cost map: (V, V) int32, INT_MAX = collided."""
+    poses = np.ascontiguousarray(poses, np.float32).reshape(-1, 12)
+    V = poses.shape[0]
+    out = np.zeros((V, V), np.int32)
+    lib().orc_collision_cost_map(vol._h, _f32(poses, 12 * V), V, out)
+    return out
 
 
 # --------------------------------------------------------------------------- fusion (own spec)

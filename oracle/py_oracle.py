@@ -226,3 +226,39 @@ def dda_cells(vol, O, E, end_inside):
     if end_inside:
         return missed, tuple(cur)
     return missed + [tuple(cur)], None
+
+
+def will_collide(vol, a, b):
+    """tests/CameraPathGen.cpp:128-156 (1 mm march a -> b; Eigen normalized())."""
+    a = [f32(v) for v in a]
+    b = [f32(v) for v in b]
+    ab = [f32(a[i] - b[i]) for i in range(3)]
+    distance = f64(f32(math.sqrt(s3(f32(ab[0] * ab[0]), f32(ab[1] * ab[1]), f32(ab[2] * ab[2])))))
+    ba = [f32(b[i] - a[i]) for i in range(3)]
+    sq = s3(f32(ba[0] * ba[0]), f32(ba[1] * ba[1]), f32(ba[2] * ba[2]))
+    v = [f32(x / f32(math.sqrt(sq))) for x in ba] if sq > 0 else ba
+    depth = 1
+    while True:
+        if depth > distance * 1000:
+            return False
+        pt = [f32(a[i] + f32(f32(v[i] * f32(depth)) / f32(1000))) for i in range(3)]
+        depth += 1
+        if not vol.valid_points(pt):
+            continue
+        c = vol.get_voxel(pt)
+        if vol.valid_coords(c) and c in vol.cells:
+            return True
+
+
+def collision_cost_map(vol, centres):
+    """tests/CameraPathGen.cpp:310-331 run_tsp: INT_MAX if willCollide else int(dist*1000)."""
+    V = len(centres)
+    out = np.zeros((V, V), np.int32)
+    for i in range(V):
+        for j in range(V):
+            if will_collide(vol, centres[i], centres[j]):
+                out[i, j] = 2 ** 31 - 1
+            else:
+                d = [f32(f32(centres[i][k]) - f32(centres[j][k])) for k in range(3)]
+                out[i, j] = int(f64(f32(math.sqrt(s3(f32(d[0] * d[0]), f32(d[1] * d[1]), f32(d[2] * d[2]))))) * 1000)
+    return out

@@ -35,7 +35,7 @@ def _run(tmp_path, pts, nrm, poses):
             res["goodlist"] = np.array([int(x) for x in f[1:]], np.uint64)
         elif f[0] == "Sizes:":
             res["sizes"].append(int(f[1]))
-        elif f[0] in ("selected", "selected_from_sets"):
+        elif f[0] in ("selected", "selected_from_sets", "costmap", "collide_from_0"):
             res[f[0]] = [int(x) for x in f[1:]]
     return res
 
@@ -68,3 +68,7 @@ def test_raytracing_driver_matches_oracle(tmp_path, oracle):
     # tests/SetCover.cpp:236-239 greedySetCover on the same good sets
     exp = [int(x) for x in oracle.greedy_set_cover(sets, 5)]
     assert got["selected"] == exp and got["selected_from_sets"] == exp and len(exp) > 0
+    # tests/CameraPathGen.cpp:310-331 run_tsp cost map (compat PathPlanning.hpp)
+    cm = oracle.collision_cost_map(ov, poses)
+    assert got["costmap"] == [int(x) for x in cm.ravel()]
+    assert got["collide_from_0"] == [int(x == 2**31 - 1) for x in cm[0]]

@@ -229,6 +229,54 @@ def test_will_collide(oracle, dmf):
     assert g.any() and not g.all()
 
 
+def test_collision_cost_map(oracle, dmf):
+    """Planner::run_tsp cost map (tests/CameraPathGen.cpp:310-331) over V*V pairs."""
+    ov = Hh.oracle_volume(oracle)
+    gv = Hh.gpu_volume()
+    poses = Hh.all_poses().reshape(-1, 12)
+    # add centres inside the box (every segment between them crosses the surface) and a
+    # duplicate centre (zero-length segment -> cost 0, no collision)
+    rng = np.random.default_rng(7)
+    inner = np.tile(poses[:1], (6, 1))
+    lo, hi = np.array(Hh.BOUNDS[0::2]), np.array(Hh.BOUNDS[1::2])
+    inner[:, 3::4] = (lo + (hi - lo) * rng.uniform(0.2, 0.8, (6, 3))).astype(np.float32)
+    poses = np.concatenate([poses, inner, poses[:1]])
+    got = dmf.collision_cost_map(gv, poses)
+    exp = oracle.collision_cost_map(ov, poses)
+    assert np.array_equal(got, exp)
+    coll = got == np.iinfo(np.int32).max
+    assert coll.any() and not coll.all()
+    assert np.all(np.diag(got) == 0) and got[0, -1] == 0
+    # the same pairs through the segment-batched willCollide
+    V = len(poses)
+    c = poses[:, 3::4]
+    wc = dmf.will_collide(gv, np.repeat(c, V, axis=0), np.tile(c, (V, 1))).reshape(V, V)
+    assert np.array_equal(wc, coll)
+    # edge sizes
+    assert dmf.collision_cost_map(gv, poses[:0]).shape == (0, 0)
+    assert np.array_equal(dmf.collision_cost_map(gv, poses[:1]), np.zeros((1, 1), np.int32))
+
+
+def test_collision_cost_map_device_invalid_centre(dmf):
+    import ctypes as C
+    import torch
+    gv = Hh.gpu_volume()
+    poses = Hh.all_poses().reshape(-1, 12)[:4].copy()
+    poses[2, 3] = np.nan
+    with pytest.raises(dmf.DmfError):
+        dmf.collision_cost_map(gv, poses)
+    dp = torch.from_numpy(poses).cuda()
+    dm = torch.zeros((4, 4), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    gv._L.dmf_volume_set_stream(gv._h, C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert gv._L.dmf_collision_cost_map_device(gv._h, C.c_void_p(dp.data_ptr()), 4, C.c_void_p(dm.data_ptr())) == 0
+    torch.cuda.synchronize()
+    m = dm.cpu().numpy()
+    assert (m[2, :] == -1).all() and (m[:, 2] == -1).all()
+    ok = np.delete(np.delete(m, 2, 0), 2, 1)
+    assert np.array_equal(ok, dmf.collision_cost_map(gv, np.delete(poses, 2, 0)))
+
+
 def test_fuse_parity(oracle, engine):
     poses, depth, _ = Hh.frames()
     ov = Hh.oracle_volume(oracle, clouds=[])

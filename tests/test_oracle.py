@@ -281,3 +281,32 @@ def test_golden_config1_regression(oracle):
     for k, v in out.items():
         assert np.array_equal(np.asarray(v), z[k]), k
     assert len(z["occ"]) > 1000 and len(z["rrtf_good"]) > 1000 and z["fuse_stats"][0] > 1e6
+
+
+def test_collision_cost_map_py_vs_cpp(oracle, gold):
+    """run_tsp cost map (tests/CameraPathGen.cpp:310-331): C++ restatement vs the pure-Python
+    one, on short segments (<= ~0.4 m, i.e. <= 400 march steps each) through a 24^3 grid."""
+    K, depth, poses = gold["K"], gold["depth"], gold["poses"]
+    xyz = oracle.backproject(K, depth[0], poses[0])
+    m = depth[0] > 0
+    pts = xyz[m][::13]
+    nrm = gold["normals16"][0][m][::13].astype(np.float32)
+    bounds = (-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    pv = PY.Vol(bounds, (24, 24, 24))
+    pv.integrate(pts, nrm)
+    ov = oracle.Volume()
+    ov.setDimensions(*bounds)
+    ov.setVolumeSize(24, 24, 24)
+    ov.constructVolume()
+    ov.integratePointCloud(pts, nrm)
+    rng = np.random.default_rng(3)
+    centres = rng.uniform(-0.2, 0.2, (9, 3)).astype(np.float32)
+    centres[8] = centres[0]
+    P = np.tile(np.eye(3, 4, dtype=np.float32).reshape(1, 12), (9, 1))
+    P[:, 3::4] = centres
+    got = oracle.collision_cost_map(ov, P)
+    exp = PY.collision_cost_map(pv, centres)
+    assert np.array_equal(got, exp)
+    coll = got == 2 ** 31 - 1
+    assert coll.any() and not coll.all()
+    assert got[0, 8] == 0 and np.all(np.diag(got) == 0)
