@@ -253,8 +253,8 @@ __device__ inline int small_div(int i, int b, float rb, int& rem) {
   return q;
 }
 
-// Production fusion kernel.  One 64-lane workgroup per 8x8 pixel packet; the wave
-// runs its own rounds (no cross-wave barriers).  Per round:
+// Tiled-box fusion kernel (production before k_fuse_l; DMF_FUSE_VARIANT=25).  One
+// 64-lane workgroup per 8x8 pixel packet; the wave runs its own rounds (no cross-wave barriers).  Per round:
 //  1. walk: each lane advances its DDA up to kS cell updates on the three int32
 //     crossing-time differences (dda_select: ties x < y < z), recording 2-bit axis
 //     codes; per-axis advance counts are popcounts;
@@ -679,6 +679,182 @@ __global__ __launch_bounds__(64) void k_fuse_r(Geom g, CamP cam, const uint16_t*
   }
 }
 
+// Production fusion kernel.  One 64-lane workgroup per 8x8 pixel
+// packet of one frame; the wave runs its own rounds (no cross-wave barriers).  Per
+// round of kS cell updates per ray:
+//  1. walk: kS unconditional exact-DDA steps (dda_select, ties x < y < z), recording
+//     2-bit axis codes.  A lane with fewer advances finishes in this round (or has
+//     finished): its walk state is never read again, codes past its advance count
+//     are masked off, and the crossing-time invariants keep |E| bounded past the
+//     ray's end, so no per-step predication is needed;
+//  2. box: exact extents of the round's miss cells (per-axis advance counts from
+//     popcounts of the codes), wave-reduced with packed DPP maxima; the LDS box is
+//     stored LINEARLY over those extents (x-major, z fastest, no padding);
+//  3. replay: each lane replays its miss cells into LDS adds, ROTATED to start at a
+//     lane-dependent cell P_o: moves o..nm-2, then code 3 = jump P_{nm-1} -> P_0, then
+//     moves 0..o-2.  Neighbouring rays of a packet sit in one cell at the same step;
+//     rotation puts them in different cells, cutting same-bank LDS atomics from ~9.6x
+//     to ~3.7x the conflict-free cycles (tools/sim_fusion_lds.py; SQ_LDS_BANK_CONFLICT
+//     1.89e9 -> 0.69e9 per launch);
+//  4. flush: an in-order scan compacts the non-zero cells (ballot + mbcnt) into a list
+//     kept in the box's own LDS; one device atomic per listed cell.  Box order puts
+//     ~4.4 cells of one 64-B tiled counter line into each wave instruction
+//     (tools/sim_fusion_flush_order.py; tile order: 4.85), which is one memory-side request.
+// A round whose box exceeds kBox cells adds its misses to HBM directly.  Hits (one per
+// ray) go straight to HBM.  Counts are exact integers: bit-identical to k_fuse_direct
+// and to the oracle.
+template <int kS, int kBox>
+__global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t* __restrict__ depth,
+                                               const PoseX* __restrict__ poses, int dmin, int dmax, int packets_x,
+                                               int32_t* __restrict__ hits, int32_t* __restrict__ misses,
+                                               unsigned long long* __restrict__ stats) {
+  static_assert(kS <= 15, "2-bit codes of up to 15 advances with a 32-bit field mask");
+  static_assert(kBox % 256 == 0 && kBox <= 65536, "box scanned 256 cells per iteration, 16-bit indices");
+  static_assert(kBox >= 64 * kS, "the non-zero list lives in the box");
+  stats = stat_slot(stats);
+  __shared__ __attribute__((aligned(16))) int box[kBox];
+  uint32_t* nzl = (uint32_t*)box;
+  const int l = threadIdx.x;
+  for (int i = l; i < kBox; i += 64) box[i] = 0;
+  const Tiles tl = tiles_of(g.n);
+  const int pr = (blockIdx.x / packets_x) * 8 + (l >> 3), pc = (blockIdx.x % packets_x) * 8 + (l & 7);
+  Ray R;
+  bool valid;
+  const unsigned long long upd = (unsigned long long)pixel_ray(g, cam, depth, poses, blockIdx.y, pr, pc, dmin, dmax,
+                                                               R, valid);
+  const unsigned long long nvalid = valid ? 1 : 0, nhit = (R.left > 0 && R.end_inside) ? 1 : 0;
+  int32_t E01 = R.E01, E02 = R.E02, E12 = R.E12;
+  const int32_t K0 = R.K[0], K1 = R.K[1], K2 = R.K[2];
+  const int st0 = R.st[0], st1 = R.st[1], st2 = R.st[2];
+  int c0 = R.c[0], c1 = R.c[1], c2 = R.c[2], left = R.left;
+  const bool end_inside = R.end_inside;
+  const int rot = ((l & 7) + 3 * (l >> 3)) % kS;  // replay start offset in a full round
+  unsigned long long nflush = 0, nround_lds = 0, nround_direct = 0;
+  while (__builtin_amdgcn_ballot_w64(left > 0)) {
+    const int rem = left < kS ? left : kS;
+    const bool fin = rem == left && rem > 0;
+    const int nadv = fin ? rem - 1 : rem;
+    uint32_t codes = 0;
+#pragma unroll
+    for (int k = 0; k < kS; ++k) {
+      bool s0, s1, s2;
+      dda_select(E01, E02, E12, K0, K1, K2, s0, s1, s2);
+      codes |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
+    }
+    const uint32_t fmask = (1u << (2 * nadv)) - 1u;
+    const int n2 = __builtin_popcount(codes & fmask & 0xAAAAAAAAu);
+    const int n1 = __builtin_popcount(codes & fmask & 0x55555555u);
+    const int n0 = nadv - n1 - n2;
+    const int e0 = c0 + st0 * n0, e1 = c1 + st1 * n1, e2 = c2 + st2 * n2;
+    const int nm = (fin && end_inside) ? rem - 1 : rem;  // miss cells of this round
+    int m0 = e0, m1 = e1, m2 = e2;                       // last miss cell
+    if (nm > 0 && nadv > 0 && (!fin || end_inside)) {
+      const uint32_t lc = (codes >> (2 * (nadv - 1))) & 3u;
+      m0 -= lc == 0u ? st0 : 0;
+      m1 -= lc == 1u ? st1 : 0;
+      m2 -= lc == 2u ? st2 : 0;
+    }
+    uint32_t px = 0, py = 0, pz = 0;
+    if (nm > 0) {
+      px = (uint32_t)max(c0, m0) | ((0xffffu - (uint32_t)min(c0, m0)) << 16);
+      py = (uint32_t)max(c1, m1) | ((0xffffu - (uint32_t)min(c1, m1)) << 16);
+      pz = (uint32_t)max(c2, m2) | ((0xffffu - (uint32_t)min(c2, m2)) << 16);
+    }
+    const uint32_t rx = wave_pkmax(px), ry = wave_pkmax(py), rz = wave_pkmax(pz);
+    if (rx != 0u) {
+      const int ax = 0xffff - (int)(rx >> 16), ay = 0xffff - (int)(ry >> 16), az = 0xffff - (int)(rz >> 16);
+      const int bx = (int)(rx & 0xffffu) - ax + 1, by = (int)(ry & 0xffffu) - ay + 1, bz = (int)(rz & 0xffffu) - az + 1;
+      const int byz = by * bz;
+      const int64_t ncell_box = (int64_t)bx * byz;
+      if (ncell_box <= kBox) {
+        ++nround_lds;
+        // byte offsets into the box; per-axis byte strides along this ray
+        const int dX = st0 * byz * 4, dY = st1 * bz * 4, dZ = st2 * 4;
+        const int cur0 = (((c0 - ax) * by + (c1 - ay)) * bz + (c2 - az)) * 4;
+        int cur = cur0, dJ = 0;
+        uint32_t rc = codes;
+        if (nm > 1) {
+          int o = rot;
+          if (o >= nm) small_div(o, nm, __builtin_amdgcn_rcpf((float)nm), o);
+          const uint32_t lo = (1u << (2 * o)) - 1u;
+          const int q2 = __builtin_popcount(codes & lo & 0xAAAAAAAAu);
+          const int q1 = __builtin_popcount(codes & lo & 0x55555555u);
+          cur += ((o - q1 - q2) * st0 * byz + q1 * st1 * bz + q2 * st2) * 4;
+          dJ = cur0 - (((m0 - ax) * by + (m1 - ay)) * bz + (m2 - az)) * 4;
+          const uint32_t a = (codes >> (2 * o)) & ((1u << (2 * (nm - 1 - o))) - 1u);
+          const uint32_t b = o > 1 ? (codes & ((1u << (2 * (o - 1))) - 1u)) << (2 * (nm - o)) : 0u;
+          rc = a | (3u << (2 * (nm - 1 - o))) | b;
+        }
+        const bool full = __builtin_amdgcn_ballot_w64(nm != kS) == 0;
+        char* const b8 = (char*)box;
+#pragma unroll
+        for (int k = 0; k < kS; ++k) {
+          if (full || k < nm) atomicAdd((int*)(b8 + cur), 1);
+          if (k + 1 < kS) {
+            const uint32_t cd = (rc >> (2 * k)) & 3u;
+            cur += cd == 3u ? dJ : (cd == 2u ? dZ : (cd == 1u ? dY : dX));
+          }
+        }
+        __syncthreads();  // single-wave workgroup: orders the LDS adds before the scan
+        const int nb = (int)ncell_box;
+        int nnz = 0;
+        for (int i0 = 0; i0 < nb; i0 += 256) {
+          int v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + l;
+            v[u] = i < nb ? box[i] : 0;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + l;
+            const uint64_t b = __builtin_amdgcn_ballot_w64(v[u] != 0);
+            if (i < nb) box[i] = 0;
+            if (v[u]) nzl[nnz + lane_prefix(b)] = (uint32_t)i | ((uint32_t)v[u] << 16);
+            nnz += __builtin_popcountll(b);
+          }
+        }
+        __syncthreads();
+        const float ryz = __builtin_amdgcn_rcpf((float)byz), rz1 = __builtin_amdgcn_rcpf((float)bz);
+        for (int e = l; e < nnz; e += 64) {
+          const uint32_t en = nzl[e];
+          int rr, qz;
+          const int qx = small_div((int)(en & 0xffffu), byz, ryz, rr);
+          const int qy = small_div(rr, bz, rz1, qz);
+          ++nflush;
+          atomic_add_dev(&misses[tiled_index(tl, ax + qx, ay + qy, az + qz)], (int)(en >> 16));
+        }
+        __syncthreads();
+        for (int e = l; e < nnz; e += 64) box[e] = 0;
+        __syncthreads();
+      } else {
+        ++nround_direct;
+        int x = c0, y = c1, z = c2;
+#pragma unroll
+        for (int k = 0; k < kS; ++k) {
+          if (k < nm) atomic_add_dev(&misses[tiled_index(tl, x, y, z)], 1);
+          const uint32_t cd = (codes >> (2 * k)) & 3u;
+          x += cd == 0u ? st0 : 0;
+          y += cd == 1u ? st1 : 0;
+          z += cd == 2u ? st2 : 0;
+        }
+      }
+    }
+    if (fin && end_inside) atomic_add_dev(&hits[tiled_index(tl, e0, e1, e2)], 1);
+    c0 = e0; c1 = e1; c2 = e2;
+    left -= rem;
+  }
+  if (stats) {
+    wave_stats(stats, upd, nvalid, nhit);
+    for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
+    if (l == 0) {
+      if (nflush) atomicAdd(&stats[6], nflush);
+      if (nround_lds) atomicAdd(&stats[4], nround_lds);
+      if (nround_direct) atomicAdd(&stats[5], nround_direct);
+    }
+  }
+}
+
 // Tiled counters -> clamped int16 log-odds in the reference's x-major voxel order.
 // One lane per 4 consecutive z cells: one 16-B read per counter, one 8-B write.
 __global__ __launch_bounds__(256) void k_finalize(Geom g, const int32_t* __restrict__ hits,
@@ -769,7 +945,11 @@ const char* dmf_fuse_kernel(void) {
     case 23: return "dmf::k_fuse_r<6, 2048, 3>";
     case 24: return "dmf::k_fuse_r<10, 1280, 1>";
     case 25: return "dmf::k_fuse_t<10, 1280, true>";
-    default: return "dmf::k_fuse_r<10, 1280, 1>";
+    case 30: return "dmf::k_fuse_l<10, 1280>";
+    case 31: return "dmf::k_fuse_l<12, 1280>";
+    case 32: return "dmf::k_fuse_l<14, 1536>";
+    case 33: return "dmf::k_fuse_l<12, 1536>";
+    default: return "dmf::k_fuse_l<12, 1280>";
   }
 }
 
@@ -838,7 +1018,11 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
     case 23: DMF_FUSE_LAUNCH_R((k_fuse_r<6, 2048, 3>), 3); break;
     case 24: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 1280, 1>), 1); break;
     case 25: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1280>)); break;
-    default: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 1280, 1>), 1); break;
+    case 30: DMF_FUSE_LAUNCH_R((k_fuse_l<10, 1280>), 1); break;
+    case 31: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1280>), 1); break;
+    case 32: DMF_FUSE_LAUNCH_R((k_fuse_l<14, 1536>), 1); break;
+    case 33: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1536>), 1); break;
+    default: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1280>), 1); break;
   }
 #undef DMF_FUSE_LAUNCH_T
 #undef DMF_FUSE_LAUNCH_R
