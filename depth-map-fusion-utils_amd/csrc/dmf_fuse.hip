@@ -7,16 +7,17 @@
 // endpoints, crossing times compared by cross-multiplication), so GPU and CPU
 // oracle visit the same cells and the int32 hit/miss counts are bit-identical.
 //
-// The kernel is bound by the memory-side atomic request rate (≈2e10 64-B requests/s
-// chip-wide, MI355X_MICROARCH.md §Global float atomics): one request per distinct
-// 64-B line per wave instruction.  Two measures raise the cell updates per request:
-// LDS aggregation of each 8x8 ray packet's updates (≈8.8 rays share a cell per
-// round) and a tiled counter layout (2x2x4-cell tiles = one 64-B line, ≈5.3 of a
-// round's distinct cells per line instead of ≈3.0 for x-major rows).
+// Device atomics execute at the memory side, one request per distinct 64-B line per
+// wave instruction (≈2e10 requests/s chip-wide, MI355X_MICROARCH.md §Global float
+// atomics), so one atomic per cell update costs ~320 ms per launch.  LDS aggregation
+// of each 8x8 ray packet's updates (≈8.2 rays share a cell per round) and a tiled
+// counter layout (2x2x4-cell tiles = one 64-B line) bring that to 2.3e8 requests;
+// what remains binding is instruction issue.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "dmf_host.hpp"
 
@@ -253,216 +254,12 @@ __device__ inline int small_div(int i, int b, float rb, int& rem) {
   return q;
 }
 
-// Tiled-box fusion kernel (production before k_fuse_l; DMF_FUSE_VARIANT=25).  One
-// 64-lane workgroup per 8x8 pixel packet; the wave runs its own rounds (no cross-wave barriers).  Per round:
-//  1. walk: each lane advances its DDA up to kS cell updates on the three int32
-//     crossing-time differences (dda_select: ties x < y < z), recording 2-bit axis
-//     codes; per-axis advance counts are popcounts;
-//  2. box: the exact extents of the round's miss cells, reduced over the wave with
-//     packed DPP maxima, widened to whole counter tiles (2x2x4), define a dense LDS
-//     box stored tile by tile, like the counters in HBM;
-//  3. replay: each lane replays its codes into LDS adds (odd lanes backwards from
-//     their last miss cell, so that neighbouring rays rarely hit one LDS address in
-//     the same instruction); the tiled LDS index moves by an in-tile delta or, when
-//     the step leaves the tile, by the tile stride;
-//  4. flush: an in-order scan of the box: 16 consecutive lanes = one tile = one 64-B
-//     line of the HBM counters, so each wave instruction issues at most 4 atomic
-//     requests, one per tile with a non-zero cell.
-// A round whose box exceeds kBox cells adds its misses to HBM directly.  Hits (one
-// per ray) go straight to HBM.  Counts are exact integers: bit-identical to
-// k_fuse_direct and to the oracle.
-template <int kS, int kBox, bool kShare = true>
-__global__ __launch_bounds__(64) void k_fuse_t(Geom g, CamP cam, const uint16_t* __restrict__ depth,
-                                               const PoseX* __restrict__ poses, int dmin, int dmax, int packets_x,
-                                               int32_t* __restrict__ hits, int32_t* __restrict__ misses,
-                                               unsigned long long* __restrict__ stats) {
-  static_assert(kS <= 15, "2-bit codes of up to 15 advances with a 32-bit field mask");
-  static_assert(kBox % 256 == 0 && kBox <= 65536, "box scanned 256 cells per iteration, 16-bit indices");
-  stats = stat_slot(stats);
-  __shared__ __attribute__((aligned(16))) int box[kBox];
-  // non-zero cells of a round (<= its updates).  kShare: the list lives in the box
-  // itself — entry j is written while scanning cell i >= j, after cells <= i were
-  // read and cleared, and is cleared again after the flush.
-  __shared__ uint32_t nzl_own[kShare ? 1 : 64 * kS];
-  uint32_t* nzl = kShare ? (uint32_t*)box : nzl_own;
-  const int l = threadIdx.x;
-  for (int i = l; i < kBox; i += 64) box[i] = 0;
-  const int r = (blockIdx.x / packets_x) * 8 + (l >> 3), c = (blockIdx.x % packets_x) * 8 + (l & 7);
-  Ray R;
-  bool valid;
-  const int upd = pixel_ray(g, cam, depth, poses, blockIdx.y, r, c, dmin, dmax, R, valid);
-  const bool hit = R.left > 0 && R.end_inside;
-  const Tiles tl = tiles_of(g.n);
-  int32_t E01 = R.E01, E02 = R.E02, E12 = R.E12;
-  const int32_t K0 = R.K[0], K1 = R.K[1], K2 = R.K[2];
-  const int st0 = R.st[0], st1 = R.st[1], st2 = R.st[2];
-  const bool end_inside = R.end_inside;
-  int c0 = R.c[0], c1 = R.c[1], c2 = R.c[2];
-  int left = R.left;
-  const bool odd = (l & 1) != 0;
-  unsigned long long nflush = 0, nround_lds = 0, nround_direct = 0;
-  while (__builtin_amdgcn_ballot_w64(left > 0)) {
-    const int rem = left < kS ? left : kS;
-    const bool fin = rem == left && rem > 0;
-    const int nadv = fin ? rem - 1 : rem;
-    uint32_t codes = 0;
-    if (__builtin_amdgcn_ballot_w64(nadv != kS) == 0) {  // every lane walks kS steps
-#pragma unroll
-      for (int k = 0; k < kS; ++k) {
-        bool s0, s1, s2;
-        dda_select(E01, E02, E12, K0, K1, K2, s0, s1, s2);
-        codes |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kS; ++k) {
-        if (k < nadv) {
-          bool s0, s1, s2;
-          dda_select(E01, E02, E12, K0, K1, K2, s0, s1, s2);
-          codes |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
-        }
-      }
-    }
-    const uint32_t fmask = (1u << (2 * nadv)) - 1u;
-    const int n2 = __builtin_popcount(codes & fmask & 0xAAAAAAAAu);
-    const int n1 = __builtin_popcount(codes & fmask & 0x55555555u);
-    const int n0 = nadv - n1 - n2;
-    const int e0 = c0 + st0 * n0, e1 = c1 + st1 * n1, e2 = c2 + st2 * n2;
-    const int nm = (fin && end_inside) ? rem - 1 : rem;  // miss updates this round
-    // cell of the last miss update: the end cell, or one advance before it
-    int m0 = e0, m1 = e1, m2 = e2;
-    if (nm > 0 && nadv > 0 && (!fin || end_inside)) {
-      const uint32_t lc = (codes >> (2 * (nadv - 1))) & 3u;
-      m0 -= lc == 0u ? st0 : 0;
-      m1 -= lc == 1u ? st1 : 0;
-      m2 -= lc == 2u ? st2 : 0;
-    }
-    const bool act = nm > 0;
-    const uint32_t px = act ? ((uint32_t)max(c0, m0) | ((0xffffu - (uint32_t)min(c0, m0)) << 16)) : 0u;
-    const uint32_t py = act ? ((uint32_t)max(c1, m1) | ((0xffffu - (uint32_t)min(c1, m1)) << 16)) : 0u;
-    const uint32_t pz = act ? ((uint32_t)max(c2, m2) | ((0xffffu - (uint32_t)min(c2, m2)) << 16)) : 0u;
-    const uint32_t rx = wave_pkmax(px), ry = wave_pkmax(py), rz = wave_pkmax(pz);
-    if (rx != 0u) {
-      // box = whole tiles covering the extents; origin (ax, ay, az) on a tile corner
-      const int ax = (0xffff - (int)(rx >> 16)) & ~1, ay = (0xffff - (int)(ry >> 16)) & ~1,
-                az = (0xffff - (int)(rz >> 16)) & ~3;
-      const int tbx = (((int)(rx & 0xffffu) - ax) >> 1) + 1, tby = (((int)(ry & 0xffffu) - ay) >> 1) + 1,
-                tbz = (((int)(rz & 0xffffu) - az) >> 2) + 1;
-      const int tyz = tby * tbz;
-      const int64_t ncell_box = (int64_t)tbx * tyz * 16;
-      // replay direction and first replayed cell
-      const int sgn = odd ? -1 : 1;
-      int x = odd ? m0 : c0, y = odd ? m1 : c1, z = odd ? m2 : c2;
-      const int gx = sgn * st0, gy = sgn * st1, gz = sgn * st2;
-      // Odd lanes replay backwards: bit-reverse the code word (field k -> 15 - k, and
-      // codes 1 <-> 2 swap their bits, so swap them back), then align the code of
-      // advance nm - 2 to field 0.  Field k then holds the k-th replayed advance.
-      uint32_t rc = codes;
-      if (odd) {
-        rc = __builtin_bitreverse32(codes);
-        rc = ((rc & 0x55555555u) << 1) | ((rc & 0xAAAAAAAAu) >> 1);
-        rc = nm >= 2 ? rc >> (2 * (17 - nm)) : 0u;
-      }
-      if (ncell_box <= kBox) {
-        ++nround_lds;
-        // Next-step delta per axis: in-tile (x: 8, y: 4, z: 1) or, when the step leaves
-        // the tile, the tile stride minus the in-tile span; x and y alternate between
-        // the two, z crosses every 4th step.  Signed by the replay direction.
-        const int ix = gx * 8, iy = gy * 4, iz = gz;
-        const int jx = gx * (tyz * 16 - 8), jy = gy * (tbz * 16 - 4), jz = gz * 13;
-        const int fz = gz > 0 ? 3 : 0;
-        int qz = z & 3;
-        int nx = ((x & 1) == (gx > 0 ? 1 : 0)) ? jx : ix;
-        int ny = ((y & 1) == (gy > 0 ? 1 : 0)) ? jy : iy;
-        int nzd = qz == fz ? jz : iz;
-        const int tx_ = ix ^ jx, ty_ = iy ^ jy;
-        int cur = ((((x - ax) >> 1) * tby + ((y - ay) >> 1)) * tbz + ((z - az) >> 2)) * 16 +
-                  (((x & 1) << 3) | ((y & 1) << 2) | qz);
-        const bool full = __builtin_amdgcn_ballot_w64(nm != kS) == 0;  // every lane has kS misses
-#pragma unroll
-        for (int k = 0; k < kS; ++k) {
-          if (full || k < nm) atomicAdd(&box[cur], 1);
-          if (k + 1 < kS) {
-            const uint32_t cd = (rc >> (2 * k)) & 3u;
-            const bool ax0 = cd == 0u, ax1 = cd == 1u, ax2 = cd == 2u;
-            cur += ax2 ? nzd : (ax1 ? ny : nx);
-            nx ^= ax0 ? tx_ : 0;
-            ny ^= ax1 ? ty_ : 0;
-            qz = ax2 ? ((qz + gz) & 3) : qz;
-            nzd = qz == fz ? jz : iz;
-          }
-        }
-        __syncthreads();  // single-wave workgroup: orders the LDS adds before the flush
-        // compact the non-zero cells (box order = tile order) into (index | count << 16)
-        const int nb = (int)ncell_box;
-        int nnz = 0;
-        for (int i0 = 0; i0 < nb; i0 += 256) {
-          int v[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int i = i0 + 64 * u + l;
-            v[u] = i < nb ? box[i] : 0;
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int i = i0 + 64 * u + l;
-            const uint64_t b = __builtin_amdgcn_ballot_w64(v[u] != 0);
-            if (i < nb) box[i] = 0;
-            if (v[u]) nzl[nnz + lane_prefix(b)] = (uint32_t)i | ((uint32_t)v[u] << 16);
-            nnz += __builtin_popcountll(b);
-          }
-        }
-        __syncthreads();
-        // approximate reciprocals suffice: small_div corrects the quotient by one
-        const float rtyz = __builtin_amdgcn_rcpf((float)tyz), rtz = __builtin_amdgcn_rcpf((float)tbz);
-        const int tax = ax >> 1, tay = ay >> 1, taz = az >> 2;
-        for (int e = l; e < nnz; e += 64) {
-          const uint32_t en = nzl[e];
-          const int i = (int)(en & 0xffffu);
-          int rr, tc;
-          const int t = i >> 4;
-          const int ta = small_div(t, tyz, rtyz, rr);
-          const int tb = small_div(rr, tbz, rtz, tc);
-          ++nflush;
-          atomic_add_dev(&misses[tile_base(tl, tax + ta, tay + tb, taz + tc) + (i & 15)], (int)(en >> 16));
-        }
-        if (kShare) {
-          __syncthreads();
-          for (int e = l; e < nnz; e += 64) box[e] = 0;
-        }
-        __syncthreads();
-      } else {
-        ++nround_direct;
-#pragma unroll
-        for (int k = 0; k < kS; ++k) {
-          if (k < nm) atomic_add_dev(&misses[tiled_index(tl, x, y, z)], 1);
-          const uint32_t cd = (rc >> (2 * k)) & 3u;
-          x += cd == 0u ? gx : 0;
-          y += cd == 1u ? gy : 0;
-          z += cd == 2u ? gz : 0;
-        }
-      }
-    }
-    if (fin && end_inside) atomic_add_dev(&hits[tiled_index(tl, e0, e1, e2)], 1);
-    c0 = e0; c1 = e1; c2 = e2;
-    left -= rem;
-  }
-  if (stats) {
-    wave_stats(stats, (unsigned long long)upd, valid ? 1ull : 0ull, hit ? 1ull : 0ull);
-    for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
-    if (l == 0) {
-      if (nflush) atomicAdd(&stats[6], nflush);
-      if (nround_lds) atomicAdd(&stats[4], nround_lds);
-      if (nround_direct) atomicAdd(&stats[5], nround_direct);
-    }
-  }
-}
-
-// k_fuse_t with kR rays per lane: the wave owns an 8 x (8 kR) pixel packet; every lane
-// walks and replays its kR rays interleaved (independent dependency chains for the
-// scheduler), and the rays share one LDS box per round (more rays per cell, fewer
-// flushed atomics, the round's reduction amortised over kR times the updates).
-// Odd (lane + ray) parities replay backwards.  Same exact counts as k_fuse_t.
+// Previous production kernel (DMF_FUSE_VARIANT=24, A/B reference).
+// Same rounds as k_fuse_l below but the LDS box is widened to whole 2x2x4 counter
+// tiles and stored tile by tile like HBM (the replay tracks in-tile / tile-crossing
+// index deltas, odd lanes replay backwards), and the flush list is in tile order.
+// kR rays per lane share one box (the wave owns an 8 x (8 kR) pixel packet); kR = 1
+// measured fastest (2 and 3 lose to register pressure).
 template <int kS, int kBox, int kR>
 __global__ __launch_bounds__(64) void k_fuse_r(Geom g, CamP cam, const uint16_t* __restrict__ depth,
                                                const PoseX* __restrict__ poses, int dmin, int dmax, int packets_x,
@@ -473,7 +270,7 @@ __global__ __launch_bounds__(64) void k_fuse_r(Geom g, CamP cam, const uint16_t*
   static_assert(kBox >= 64 * kS * kR, "the non-zero list lives in the box");
   stats = stat_slot(stats);
   __shared__ __attribute__((aligned(16))) int box[kBox];
-  uint32_t* nzl = (uint32_t*)box;  // non-zero list written behind the scan (see k_fuse_t)
+  uint32_t* nzl = (uint32_t*)box;  // non-zero list written behind the scan front
   const int l = threadIdx.x;
   for (int i = l; i < kBox; i += 64) box[i] = 0;
   const Tiles tl = tiles_of(g.n);
@@ -679,6 +476,9 @@ __global__ __launch_bounds__(64) void k_fuse_r(Geom g, CamP cam, const uint16_t*
   }
 }
 
+__device__ inline int popc(uint32_t v) { return __builtin_popcount(v); }
+__device__ inline int popc(uint64_t v) { return __builtin_popcountll(v); }
+
 // Production fusion kernel.  One 64-lane workgroup per 8x8 pixel
 // packet of one frame; the wave runs its own rounds (no cross-wave barriers).  Per
 // round of kS cell updates per ray:
@@ -708,7 +508,9 @@ __global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t*
                                                const PoseX* __restrict__ poses, int dmin, int dmax, int packets_x,
                                                int32_t* __restrict__ hits, int32_t* __restrict__ misses,
                                                unsigned long long* __restrict__ stats) {
-  static_assert(kS <= 15, "2-bit codes of up to 15 advances with a 32-bit field mask");
+  static_assert(kS <= 31, "2-bit codes of up to 31 advances with a 64-bit field mask");
+  using CodeT = typename std::conditional<(kS <= 15), uint32_t, uint64_t>::type;
+  constexpr CodeT kOne = 1, kOdd = (CodeT)0x5555555555555555ull, kEven = (CodeT)0xAAAAAAAAAAAAAAAAull;
   static_assert(kBox % 256 == 0 && kBox <= 65536, "box scanned 256 cells per iteration, 16-bit indices");
   static_assert(kBox >= 64 * kS, "the non-zero list lives in the box");
   stats = stat_slot(stats);
@@ -734,22 +536,22 @@ __global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t*
     const int rem = left < kS ? left : kS;
     const bool fin = rem == left && rem > 0;
     const int nadv = fin ? rem - 1 : rem;
-    uint32_t codes = 0;
+    CodeT codes = 0;
 #pragma unroll
     for (int k = 0; k < kS; ++k) {
       bool s0, s1, s2;
       dda_select(E01, E02, E12, K0, K1, K2, s0, s1, s2);
-      codes |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
+      codes |= (CodeT)(s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
     }
-    const uint32_t fmask = (1u << (2 * nadv)) - 1u;
-    const int n2 = __builtin_popcount(codes & fmask & 0xAAAAAAAAu);
-    const int n1 = __builtin_popcount(codes & fmask & 0x55555555u);
+    const CodeT fmask = (kOne << (2 * nadv)) - 1u;
+    const int n2 = popc(codes & fmask & kEven);
+    const int n1 = popc(codes & fmask & kOdd);
     const int n0 = nadv - n1 - n2;
     const int e0 = c0 + st0 * n0, e1 = c1 + st1 * n1, e2 = c2 + st2 * n2;
     const int nm = (fin && end_inside) ? rem - 1 : rem;  // miss cells of this round
     int m0 = e0, m1 = e1, m2 = e2;                       // last miss cell
     if (nm > 0 && nadv > 0 && (!fin || end_inside)) {
-      const uint32_t lc = (codes >> (2 * (nadv - 1))) & 3u;
+      const uint32_t lc = (uint32_t)(codes >> (2 * (nadv - 1))) & 3u;
       m0 -= lc == 0u ? st0 : 0;
       m1 -= lc == 1u ? st1 : 0;
       m2 -= lc == 2u ? st2 : 0;
@@ -772,18 +574,18 @@ __global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t*
         const int dX = st0 * byz * 4, dY = st1 * bz * 4, dZ = st2 * 4;
         const int cur0 = (((c0 - ax) * by + (c1 - ay)) * bz + (c2 - az)) * 4;
         int cur = cur0, dJ = 0;
-        uint32_t rc = codes;
+        CodeT rc = codes;
         if (nm > 1) {
           int o = rot;
           if (o >= nm) small_div(o, nm, __builtin_amdgcn_rcpf((float)nm), o);
-          const uint32_t lo = (1u << (2 * o)) - 1u;
-          const int q2 = __builtin_popcount(codes & lo & 0xAAAAAAAAu);
-          const int q1 = __builtin_popcount(codes & lo & 0x55555555u);
+          const CodeT lo = (kOne << (2 * o)) - 1u;
+          const int q2 = popc(codes & lo & kEven);
+          const int q1 = popc(codes & lo & kOdd);
           cur += ((o - q1 - q2) * st0 * byz + q1 * st1 * bz + q2 * st2) * 4;
           dJ = cur0 - (((m0 - ax) * by + (m1 - ay)) * bz + (m2 - az)) * 4;
-          const uint32_t a = (codes >> (2 * o)) & ((1u << (2 * (nm - 1 - o))) - 1u);
-          const uint32_t b = o > 1 ? (codes & ((1u << (2 * (o - 1))) - 1u)) << (2 * (nm - o)) : 0u;
-          rc = a | (3u << (2 * (nm - 1 - o))) | b;
+          const CodeT a = (codes >> (2 * o)) & ((kOne << (2 * (nm - 1 - o))) - 1u);
+          const CodeT b = o > 1 ? (codes & ((kOne << (2 * (o - 1))) - 1u)) << (2 * (nm - o)) : (CodeT)0;
+          rc = a | ((CodeT)3 << (2 * (nm - 1 - o))) | b;
         }
         const bool full = __builtin_amdgcn_ballot_w64(nm != kS) == 0;
         char* const b8 = (char*)box;
@@ -791,7 +593,7 @@ __global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t*
         for (int k = 0; k < kS; ++k) {
           if (full || k < nm) atomicAdd((int*)(b8 + cur), 1);
           if (k + 1 < kS) {
-            const uint32_t cd = (rc >> (2 * k)) & 3u;
+            const uint32_t cd = (uint32_t)(rc >> (2 * k)) & 3u;
             cur += cd == 3u ? dJ : (cd == 2u ? dZ : (cd == 1u ? dY : dX));
           }
         }
@@ -833,7 +635,7 @@ __global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t*
 #pragma unroll
         for (int k = 0; k < kS; ++k) {
           if (k < nm) atomic_add_dev(&misses[tiled_index(tl, x, y, z)], 1);
-          const uint32_t cd = (codes >> (2 * k)) & 3u;
+          const uint32_t cd = (uint32_t)(codes >> (2 * k)) & 3u;
           x += cd == 0u ? st0 : 0;
           y += cd == 1u ? st1 : 0;
           z += cd == 2u ? st2 : 0;
@@ -928,23 +730,7 @@ extern "C" {
 const char* dmf_fuse_kernel(void) {
   switch (fuse_variant()) {
     case 1: return "dmf::k_fuse_direct";
-    case 2: return "dmf::k_fuse_t<10, 1536, true>";
-    case 3: return "dmf::k_fuse_t<12, 2048, true>";
-    case 4: return "dmf::k_fuse_t<15, 2560, true>";
-    case 5: return "dmf::k_fuse_t<14, 1536, true>";
-    case 6: return "dmf::k_fuse_t<15, 3072, true>";
-    case 7: return "dmf::k_fuse_t<8, 1024, true>";
-    case 8: return "dmf::k_fuse_t<10, 1280, true>";
-    case 9: return "dmf::k_fuse_t<6, 768, true>";
-    case 10: return "dmf::k_fuse_t<10, 1536, false>";
-    case 11: return "dmf::k_fuse_t<12, 1536, true>";
-    case 12: return "dmf::k_fuse_t<14, 2048, true>";
-    case 20: return "dmf::k_fuse_r<10, 2560, 2>";
-    case 21: return "dmf::k_fuse_r<8, 2048, 2>";
-    case 22: return "dmf::k_fuse_r<10, 2048, 2>";
-    case 23: return "dmf::k_fuse_r<6, 2048, 3>";
     case 24: return "dmf::k_fuse_r<10, 1280, 1>";
-    case 25: return "dmf::k_fuse_t<10, 1280, true>";
     case 30: return "dmf::k_fuse_l<10, 1280>";
     case 31: return "dmf::k_fuse_l<12, 1280>";
     case 32: return "dmf::k_fuse_l<14, 1536>";
@@ -986,14 +772,10 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
   const Geom g = v->geom();
   unsigned long long* st = nullptr;
   if (d_stats) DMF_TRY(stats_begin(v, &st));
-  const int pkx = (cp.W + 7) / 8, pky = (cp.H + 7) / 8;
-  const dim3 gridw((unsigned)(pkx * pky), (unsigned)P);
+  const int pkx = (cp.W + 7) / 8;
 #define DMF_FUSE_LAUNCH_R(K, NR)                                                                               \
   hipLaunchKernelGGL(K, dim3((unsigned)(pkx * ((cp.H + 8 * (NR) - 1) / (8 * (NR)))), (unsigned)P), dim3(64), 0,        \
                      v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, d_misses, st)
-#define DMF_FUSE_LAUNCH_T(K)                                                                                    \
-  hipLaunchKernelGGL(K, gridw, dim3(64), 0, v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, \
-                     d_misses, st)
   switch (fuse_variant()) {
     case 1: {
       const int tx = (cp.W + 15) / 16, ty = (cp.H + 15) / 16;
@@ -1001,30 +783,13 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
                          d_depth, tab, prm->dmin_mm, prm->dmax_mm, tx, d_hits, d_misses, st);
       break;
     }
-    case 2: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1536>)); break;
-    case 3: DMF_FUSE_LAUNCH_T((k_fuse_t<12, 2048>)); break;
-    case 4: DMF_FUSE_LAUNCH_T((k_fuse_t<15, 2560>)); break;
-    case 5: DMF_FUSE_LAUNCH_T((k_fuse_t<14, 1536>)); break;
-    case 6: DMF_FUSE_LAUNCH_T((k_fuse_t<15, 3072>)); break;
-    case 7: DMF_FUSE_LAUNCH_T((k_fuse_t<8, 1024>)); break;
-    case 8: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1280>)); break;
-    case 9: DMF_FUSE_LAUNCH_T((k_fuse_t<6, 768>)); break;
-    case 10: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1536, false>)); break;
-    case 11: DMF_FUSE_LAUNCH_T((k_fuse_t<12, 1536>)); break;
-    case 12: DMF_FUSE_LAUNCH_T((k_fuse_t<14, 2048>)); break;
-    case 20: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 2560, 2>), 2); break;
-    case 21: DMF_FUSE_LAUNCH_R((k_fuse_r<8, 2048, 2>), 2); break;
-    case 22: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 2048, 2>), 2); break;
-    case 23: DMF_FUSE_LAUNCH_R((k_fuse_r<6, 2048, 3>), 3); break;
     case 24: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 1280, 1>), 1); break;
-    case 25: DMF_FUSE_LAUNCH_T((k_fuse_t<10, 1280>)); break;
     case 30: DMF_FUSE_LAUNCH_R((k_fuse_l<10, 1280>), 1); break;
     case 31: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1280>), 1); break;
     case 32: DMF_FUSE_LAUNCH_R((k_fuse_l<14, 1536>), 1); break;
     case 33: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1536>), 1); break;
     default: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1280>), 1); break;
   }
-#undef DMF_FUSE_LAUNCH_T
 #undef DMF_FUSE_LAUNCH_R
   DMF_LAUNCH_CHECK();
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
