@@ -1,0 +1,222 @@
+// dmf_brick.hpp — exact brick decomposition of the fusion DDA.
+//
+// The fusion walk (oracle.cpp dda_ray) visits the cells of a ray in
+// the order of its crossing EVENTS: axis a's k-th crossing happens at time
+// T_a(k) = (h_a + 2Qk) * prod_{b != a, |dq_b| > 0} |dq_b|, and events are taken in
+// lexicographic (T, axis) order (ties x < y < z).  Everything here follows from that
+// one ordering, in exact integer arithmetic:
+//
+//  * comparing two events (a, k_a), (b, k_b) divides out the common factor:
+//      (h_a + 2Q k_a) |dq_b|  vs  (h_b + 2Q k_b) |dq_a|        (< 2^40, 64-bit)
+//  * the number of b-events at or before event (a*, H*) [H* = h_a* + 2Q k*] is
+//      #{k >= 0 : k Y < X}  (b > a*)   or   #{k >= 0 : k Y <= X}  (b < a*)
+//      with X = H* |dq_b| - h_b |dq_a*|, Y = 2Q |dq_a*|  (an integer division);
+//  * the fine walk's int32 state after c_a crossings per axis is
+//      E_ab = E_ab(0) + c_a K_b - c_b K_a  (K = 2Q|dq|; exact mod 2^32, |E| < 2^29);
+//  * brick boundaries are a subset of the crossings, so the sequence of 32^3 bricks
+//    the walk passes through is a coarse walk over those events with the same order.
+//
+// Pass A/B (k_bk_count / k_bk_scatter) run the coarse walk per ray to build per-brick
+// ray lists; phase 2 (k_bk_fuse) restarts the fine walk at each (ray, brick) pair's
+// entry event and stops at its exit event, so every cell update of the fine walk is
+// made exactly once, inside the workgroup that owns the brick (LDS counters, no
+// device atomics per update).  All functions are __host__ __device__: the CPU
+// self-test (tools/brick_selftest.cpp) checks them against the plain fine walk.
+#pragma once
+#include <cstdint>
+
+#ifndef __HIPCC__
+#define __host__
+#define __device__
+#endif
+
+namespace dmf {
+namespace brick {
+
+constexpr int kLog = 5;                 // bricks of 32^3 cells
+constexpr int kB = 1 << kLog;
+constexpr int kCells = kB * kB * kB;    // 32768 LDS counters (128 KiB)
+constexpr int kMaxBricks = 32768;       // per-WG LDS histograms of pass A/B (grids <= 1024^3)
+constexpr int64_t kQ = 256;             // sub-cell fixed point (oracle.cpp kQ)
+constexpr int32_t kNever = 1 << 30;     // fine-walk E of a pair with a non-moving axis
+constexpr int64_t kNever64 = (int64_t)1 << 62;  // coarse-walk equivalent
+
+// Ray after clipping/quantisation: start/end fixed-point positions (1/256 cell).
+struct QRay {
+  int32_t cs[3], ce[3];  // start / end cell
+  int32_t st[3];         // step per axis (-1, 0, +1)
+  int32_t n[3];          // crossings per axis |ce - cs|
+  int32_t adq[3];        // |qe - qs|
+  int32_t h0[3];         // first-crossing numerator (half fixed-point units)
+  int32_t nsteps;        // n[0] + n[1] + n[2]
+  bool end_inside;
+};
+
+// 16-byte ray record: 19 bits per fixed-point coordinate (grids <= 2048 cells/axis).
+//   A = qs0 | qs1 << 19 | qs2 << 38 | end_inside << 63
+//   B = qe0 | qe1 << 19 | qe2 << 38 | valid << 63
+__host__ __device__ inline void pack_ray(const int64_t qs[3], const int64_t qe[3], bool end_inside, uint64_t& A,
+                                         uint64_t& B) {
+  A = (uint64_t)qs[0] | ((uint64_t)qs[1] << 19) | ((uint64_t)qs[2] << 38) | ((uint64_t)(end_inside ? 1 : 0) << 63);
+  B = (uint64_t)qe[0] | ((uint64_t)qe[1] << 19) | ((uint64_t)qe[2] << 38) | ((uint64_t)1 << 63);
+}
+
+__host__ __device__ inline void decode_ray(uint64_t A, uint64_t B, QRay& r) {
+  constexpr uint64_t m = (1u << 19) - 1;
+  const int32_t qs[3] = {(int32_t)(A & m), (int32_t)((A >> 19) & m), (int32_t)((A >> 38) & m)};
+  const int32_t qe[3] = {(int32_t)(B & m), (int32_t)((B >> 19) & m), (int32_t)((B >> 38) & m)};
+  r.end_inside = (A >> 63) != 0;
+  r.nsteps = 0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    r.cs[a] = qs[a] >> 8;
+    r.ce[a] = qe[a] >> 8;
+    const int32_t dq = qe[a] - qs[a];
+    r.adq[a] = dq < 0 ? -dq : dq;
+    r.st[a] = r.ce[a] > r.cs[a] ? 1 : (r.ce[a] < r.cs[a] ? -1 : 0);
+    r.n[a] = r.ce[a] > r.cs[a] ? r.ce[a] - r.cs[a] : r.cs[a] - r.ce[a];
+    // oracle.cpp dda_ray: moving up 2((cs+1)Q - qs), moving down 2(qs - cs Q) + 1
+    r.h0[a] = r.st[a] > 0 ? 2 * ((r.cs[a] + 1) * (int32_t)kQ - qs[a]) : 2 * (qs[a] - r.cs[a] * (int32_t)kQ) + 1;
+    r.nsteps += r.n[a];
+  }
+}
+
+// Fine-walk E of the pair (a, b) at the ray start (dmf_fuse.hip dda_setup).
+__host__ __device__ inline int32_t e0_pair(const QRay& r, int a, int b) {
+  if (r.st[a] && r.st[b]) return (int32_t)((int64_t)r.h0[a] * r.adq[b] - (int64_t)r.h0[b] * r.adq[a]);
+  return r.st[a] ? -kNever : (r.st[b] ? kNever : 0);
+}
+
+// Event (a, H_a) strictly before event (b, H_b) in (T, axis) order; both axes moving.
+__host__ __device__ inline bool ev_before(const QRay& r, int a, int64_t Ha, int b, int64_t Hb) {
+  const int64_t L = Ha * (int64_t)r.adq[b], R = Hb * (int64_t)r.adq[a];
+  return L < R || (L == R && a < b);
+}
+
+// floor(X / Y) for 0 <= X < 2^41, 0 < Y < 2^29 with a small quotient (< 2^20):
+// float estimate (relative error < 2^-21) and one exact correction step.
+__host__ __device__ inline int64_t small_quot(int64_t X, int64_t Y) {
+  const float xf = (float)(int32_t)(X >> 20) * 1048576.0f + (float)(int32_t)(X & 0xfffff);
+  const float yf = (float)(int32_t)Y;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // v_rcp_f32 (1 ulp): the estimate stays within 1 of floor(X/Y); the steps below fix it
+  int64_t q = (int64_t)(xf * __builtin_amdgcn_rcpf(yf));
+#else
+  int64_t q = (int64_t)(xf / yf);
+#endif
+  int64_t rm = X - q * Y;
+  if (rm < 0) { --q; rm += Y; }
+  if (rm < 0) { --q; rm += Y; }
+  if (rm >= Y) { ++q; rm -= Y; }
+  if (rm >= Y) { ++q; }
+  return q;
+}
+
+// Number of b-crossings taken at or before the event (a, Ha) (a's own crossings are
+// the caller's: k + 1).  b != a.
+__host__ __device__ inline int32_t count_at(const QRay& r, int b, int a, int64_t Ha) {
+  if (r.st[b] == 0) return 0;
+  const int64_t X = Ha * (int64_t)r.adq[b] - (int64_t)r.h0[b] * r.adq[a];
+  const int64_t Y = 2 * kQ * (int64_t)r.adq[a];
+  int64_t c;
+  if (b < a) c = X < 0 ? 0 : small_quot(X, Y) + 1;
+  else c = X <= 0 ? 0 : small_quot(X - 1, Y) + 1;
+  return c < r.n[b] ? (int32_t)c : r.n[b];
+}
+
+// Crossing counts per axis at (and including) event (a, k); a < 0 = the ray start.
+__host__ __device__ inline void counts_at(const QRay& r, int a, int32_t k, int32_t c[3]) {
+  if (a < 0) { c[0] = c[1] = c[2] = 0; return; }
+  const int64_t Ha = (int64_t)r.h0[a] + 2 * kQ * (int64_t)k;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) c[b] = (b == a) ? k + 1 : count_at(r, b, a, Ha);
+}
+
+// One (ray, brick) pair: where the fine walk enters brick (bx, by, bz), how many
+// cells it visits there, and whether the last of them is the ray's end cell.
+struct Pair {
+  int32_t cin[3];  // crossings taken before the first cell in the brick
+  int32_t cells;   // cells visited in the brick (>= 1 for a visited brick)
+  bool ends;       // the ray's end cell is the last of them
+};
+
+__host__ __device__ inline void pair_in_brick(const QRay& r, const int32_t bb[3], const int32_t ng[3], Pair& p) {
+  int ai = -1, ao = -1;
+  int32_t ki = 0, ko = 0;
+  int64_t Hi = 0, Ho = 0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int32_t lo = bb[a] << kLog;
+    const int32_t hi = (lo + kB - 1 < ng[a] - 1) ? lo + kB - 1 : ng[a] - 1;
+    // entry along a: the crossing that brings c_a into [lo, hi]
+    int32_t k = -1;
+    if (r.st[a] > 0 && r.cs[a] < lo) k = lo - r.cs[a] - 1;
+    if (r.st[a] < 0 && r.cs[a] > hi) k = r.cs[a] - hi - 1;
+    if (k >= 0) {
+      const int64_t H = (int64_t)r.h0[a] + 2 * kQ * (int64_t)k;
+      if (ai < 0 || ev_before(r, ai, Hi, a, H)) { ai = a; ki = k; Hi = H; }  // latest entry
+    }
+    // exit along a: the crossing that takes c_a out of [lo, hi]
+    k = -1;
+    if (r.st[a] > 0 && r.ce[a] > hi) k = hi - r.cs[a];
+    if (r.st[a] < 0 && r.ce[a] < lo) k = r.cs[a] - lo;
+    if (k >= 0) {
+      const int64_t H = (int64_t)r.h0[a] + 2 * kQ * (int64_t)k;
+      if (ao < 0 || ev_before(r, a, H, ao, Ho)) { ao = a; ko = k; Ho = H; }  // earliest exit
+    }
+  }
+  counts_at(r, ai, ki, p.cin);
+  const int32_t idx_in = p.cin[0] + p.cin[1] + p.cin[2];
+  if (ao >= 0) {
+    int32_t co[3];
+    counts_at(r, ao, ko, co);
+    p.cells = co[0] + co[1] + co[2] - idx_in;
+    p.ends = false;
+  } else {
+    p.cells = r.nsteps - idx_in + 1;
+    p.ends = true;
+  }
+}
+
+// Coarse walk over brick-boundary crossings: the bricks the fine walk passes
+// through, in order.  init() then `total` calls of next().
+struct Coarse {
+  int64_t E01, E02, E12, K0, K1, K2;  // E at the next boundary crossings; K = 32 * 2Q|dq|
+  int32_t total;                      // boundary crossings of the whole ray
+};
+
+__host__ __device__ inline void coarse_init(const QRay& r, Coarse& w) {
+  int64_t H[3];
+  w.total = 0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int32_t off = r.cs[a] & (kB - 1);
+    const int32_t k0 = r.st[a] > 0 ? kB - 1 - off : off;  // first boundary crossing
+    H[a] = (int64_t)r.h0[a] + 2 * kQ * (int64_t)k0;
+    if (r.st[a] != 0 && r.n[a] > k0) w.total += (r.n[a] - 1 - k0) / kB + 1;
+  }
+  auto pr = [&](int a, int b) -> int64_t {
+    if (r.st[a] && r.st[b]) return H[a] * (int64_t)r.adq[b] - H[b] * (int64_t)r.adq[a];
+    return r.st[a] ? -kNever64 : (r.st[b] ? kNever64 : 0);
+  };
+  w.E01 = pr(0, 1);
+  w.E02 = pr(0, 2);
+  w.E12 = pr(1, 2);
+  w.K0 = (int64_t)kB * 2 * kQ * r.adq[0];
+  w.K1 = (int64_t)kB * 2 * kQ * r.adq[1];
+  w.K2 = (int64_t)kB * 2 * kQ * r.adq[2];
+}
+
+// Next boundary crossing: returns its axis (ties x < y < z, as the fine walk).
+__host__ __device__ inline int coarse_next(Coarse& w) {
+  const bool b10 = w.E01 > 0;
+  const bool s2 = (b10 ? w.E12 : w.E02) > 0;
+  const bool s1 = !s2 && b10, s0 = !s2 && !b10;
+  w.E01 += s0 ? w.K1 : (s1 ? -w.K0 : 0);
+  w.E02 += s0 ? w.K2 : (s2 ? -w.K0 : 0);
+  w.E12 += s1 ? w.K2 : (s2 ? -w.K1 : 0);
+  return s2 ? 2 : (s1 ? 1 : 0);
+}
+
+}  // namespace brick
+}  // namespace dmf

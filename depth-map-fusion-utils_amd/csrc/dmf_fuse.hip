@@ -14,11 +14,13 @@
 // counter layout (2x2x4-cell tiles = one 64-B line) bring that to 2.3e8 requests;
 // what remains binding is instruction issue.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <string>
 #include <type_traits>
 
+#include "dmf_brick.hpp"
 #include "dmf_host.hpp"
 
 namespace dmf {
@@ -81,9 +83,11 @@ __device__ inline void dda_select(int32_t& E01, int32_t& E02, int32_t& E12, int3
   E12 += s1 ? K2 : (s2 ? -K1 : 0);
 }
 
-// Clip O->E to the grid and set up the walk.  Mirrors oracle.cpp dda_ray()
-// operation for operation.  Returns false when the ray misses the grid.
-__device__ inline bool dda_setup(const Geom& g, const float O[3], const float E[3], bool end_inside, Ray& R) {
+// Clip O->E to the grid and quantise the clipped endpoints to 1/256 cell (clamped
+// into their cells).  Mirrors oracle.cpp dda_ray() lines 752-780 operation for
+// operation.  Returns false when the ray misses the grid.
+__device__ inline bool dda_quantize(const Geom& g, const float O[3], const float E[3], bool end_inside, int64_t qs[3],
+                                    int64_t qe[3]) {
   double go[3], ge[3], D[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
@@ -106,15 +110,27 @@ __device__ inline bool dda_setup(const Geom& g, const float O[3], const float E[
   }
   if (end_inside) { t1 = 1.0; if (t0 > 1.0) t0 = 1.0; }
   if (t0 > t1) return false;
-  int64_t cs[3], ce[3], qs[3], qe[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const double gs = go[a] + t0 * D[a];
     const double gx = end_inside ? ge[a] : go[a] + t1 * D[a];
-    cs[a] = clampi((int64_t)floor(gs), 0, g.n[a] - 1);
-    ce[a] = end_inside ? (int64_t)floor(ge[a]) : clampi((int64_t)floor(gx), 0, g.n[a] - 1);
-    qs[a] = clampi((int64_t)floor(gs * (double)kQ), cs[a] * kQ, cs[a] * kQ + kQ - 1);
-    qe[a] = clampi((int64_t)floor(gx * (double)kQ), ce[a] * kQ, ce[a] * kQ + kQ - 1);
+    const int64_t cs = clampi((int64_t)floor(gs), 0, g.n[a] - 1);
+    const int64_t ce = end_inside ? (int64_t)floor(ge[a]) : clampi((int64_t)floor(gx), 0, g.n[a] - 1);
+    qs[a] = clampi((int64_t)floor(gs * (double)kQ), cs * kQ, cs * kQ + kQ - 1);
+    qe[a] = clampi((int64_t)floor(gx * (double)kQ), ce * kQ, ce * kQ + kQ - 1);
+  }
+  return true;
+}
+
+// Clip/quantise, then set up the walk state (oracle.cpp dda_ray lines 781-806).
+__device__ inline bool dda_setup(const Geom& g, const float O[3], const float E[3], bool end_inside, Ray& R) {
+  int64_t qs[3], qe[3];
+  if (!dda_quantize(g, O, E, end_inside, qs, qe)) return false;
+  int64_t cs[3], ce[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    cs[a] = qs[a] / kQ;  // qs, qe >= 0 and clamped into their cells
+    ce[a] = qe[a] / kQ;
   }
   int64_t adq[3], h[3];
 #pragma unroll
@@ -172,6 +188,26 @@ __device__ inline int pixel_ray(const Geom& g, const CamP& cam, const uint16_t* 
   const float O[3] = {T.f[3], T.f[7], T.f[11]};
   if (!dda_setup(g, O, E, inside, R)) { R.left = 0; return 0; }
   return R.left;
+}
+
+// pixel_ray up to the quantised endpoints (the brick path's ray record).
+__device__ inline bool pixel_quant(const Geom& g, const CamP& cam, const uint16_t* __restrict__ depth,
+                                   const PoseX* __restrict__ poses, int p, int r, int c, int dmin, int dmax,
+                                   int64_t qs[3], int64_t qe[3], bool& inside, bool& valid) {
+  valid = false;
+  inside = false;
+  if (r >= cam.H || c >= cam.W) return false;
+  const int d = depth[((int64_t)p * cam.H + r) * cam.W + c];
+  if (!(d >= dmin && d < dmax)) return false;
+  valid = true;
+  const PoseX& T = poses[p];
+  float pc[3], E[3];
+  project(cam, r, c, d, pc);
+  xform(T.f, pc[0], pc[1], pc[2], E);
+  inside = valid_points(g, E[0], E[1], E[2]);
+  if (inside) inside = valid_coords(g, bin_axis(g, 0, E[0]), bin_axis(g, 1, E[1]), bin_axis(g, 2, E[2]));
+  const float O[3] = {T.f[3], T.f[7], T.f[11]};
+  return dda_quantize(g, O, E, inside, qs, qe);
 }
 
 __device__ inline void wave_stats(unsigned long long* stats, unsigned long long upd, unsigned long long ray,
@@ -657,6 +693,391 @@ __global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t*
   }
 }
 
+// ------------------------------------------------------------ brick-owned fusion
+// (exact decomposition in dmf_brick.hpp, checked on the CPU by
+// tools/brick_selftest.cpp).  The grid is cut into 32^3-cell bricks.  One fusion
+// batch runs four kernels:
+//  A  k_bk_rays   — per pixel: back-projection, clip, quantised ray record (16 B);
+//                   the coarse walk over brick boundaries counts (ray, brick) pairs per
+//                   brick (LDS histogram, one device atomic per brick per workgroup);
+//  S  k_bk_scan   — brick offsets and the part table (parts of <= 65535 pairs);
+//  B  k_bk_pairs  — the coarse walk again: per pair a self-contained 24-B record (the
+//                   fine walk's int32 state at the brick entry, entry cell, cells in
+//                   the brick), written into the brick's list (ranges reserved per
+//                   workgroup);
+//  F  k_bk_fuse   — persistent, one 1024-lane workgroup per CU, 128 KiB of LDS
+//                   counters (16-bit misses | 16-bit hits per cell) for the brick of
+//                   its part: each lane restarts the exact int32 walk at its pair's
+//                   entry event and adds one LDS count per cell; the part's counters
+//                   are then added to HBM once (plain adds when the brick has a single
+//                   part, device atomics otherwise).  No device atomic per update.
+namespace bk = dmf::brick;
+
+struct BkGeom {
+  int nb[3];    // bricks per axis
+  int nbricks;
+};
+
+constexpr int kBkThreads = 1024;
+constexpr uint32_t kBkPartMax = 65535;  // pairs per part: 16-bit miss / hit fields never carry
+constexpr int kBkFuseLds = bk::kCells * 4 + 16;
+
+__device__ inline int bk_index(const BkGeom& bg, int x, int y, int z) { return (x * bg.nb[1] + y) * bg.nb[2] + z; }
+
+// Coarse walk of one ray: calls f(brick index) for every brick it passes, in order.
+template <class F>
+__device__ inline void bk_coarse(const BkGeom& bg, const bk::QRay& R, F&& f) {
+  int b0 = R.cs[0] >> bk::kLog, b1 = R.cs[1] >> bk::kLog, b2 = R.cs[2] >> bk::kLog;
+  f(bk_index(bg, b0, b1, b2), -1);
+  bk::Coarse cw;
+  bk::coarse_init(R, cw);
+  for (int t = 0; t < cw.total; ++t) {
+    const int a = bk::coarse_next(cw);
+    b0 += a == 0 ? R.st[0] : 0;
+    b1 += a == 1 ? R.st[1] : 0;
+    b2 += a == 2 ? R.st[2] : 0;
+    f(bk_index(bg, b0, b1, b2), a);
+  }
+}
+
+// Pass A.  Workgroup = 16 waves over a span of 8x8 packets; ray index = packet * 64 + lane.
+__global__ __launch_bounds__(kBkThreads) void k_bk_rays(Geom g, CamP cam, const uint16_t* __restrict__ depth,
+                                                        const PoseX* __restrict__ poses, int dmin, int dmax,
+                                                        int packets_x, int packets_pose, int64_t npackets, int span,
+                                                        BkGeom bg, ulonglong2* __restrict__ rays,
+                                                        uint32_t* __restrict__ brick_count,
+                                                        unsigned long long* __restrict__ stats) {
+  extern __shared__ uint32_t hist[];
+  stats = stat_slot(stats);
+  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int64_t pk0 = (int64_t)blockIdx.x * span, pk1 = min(npackets, pk0 + span);
+  unsigned long long upd = 0, nvalid = 0, nhit = 0;
+  for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
+    const int p = (int)(pk / packets_pose);
+    const int q = (int)(pk - (int64_t)p * packets_pose);
+    const int r = (q / packets_x) * 8 + (l >> 3), c = (q % packets_x) * 8 + (l & 7);
+    int64_t qs[3], qe[3];
+    bool inside, valid;
+    ulonglong2 rec;
+    rec.x = 0;
+    rec.y = 0;
+    if (pixel_quant(g, cam, depth, poses, p, r, c, dmin, dmax, qs, qe, inside, valid)) {
+      uint64_t A, B;
+      bk::pack_ray(qs, qe, inside, A, B);
+      rec.x = A;
+      rec.y = B;
+      bk::QRay R;
+      bk::decode_ray(A, B, R);
+      upd += (unsigned long long)(R.nsteps + 1);
+      nhit += inside ? 1 : 0;
+      bk_coarse(bg, R, [&](int b, int) { atomicAdd(&hist[b], 1u); });
+    }
+    nvalid += valid ? 1 : 0;
+    rays[pk * 64 + l] = rec;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) {
+    const uint32_t n = hist[i];
+    if (n) atomicAdd(&brick_count[i], n);
+  }
+  if (stats) wave_stats(stats, upd, nvalid, nhit);
+}
+
+// Scan of the brick counts (one workgroup): list offsets, write cursors, and the part
+// table part_pref[b] = parts of bricks < b (a brick of n pairs has ceil(n / 65535)
+// parts).  ctl[0] = pairs, ctl[1] = parts.
+__global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* __restrict__ cnt,
+                                                  uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
+                                                  uint32_t* __restrict__ part_pref,
+                                                  unsigned long long* __restrict__ ctl) {
+  __shared__ unsigned long long s_pairs[1024];
+  __shared__ uint32_t s_parts[1024];
+  const int t = threadIdx.x;
+  const int per = (nbricks + 1023) / 1024;
+  const int i0 = min(nbricks, t * per), i1 = min(nbricks, i0 + per);
+  unsigned long long sp = 0;
+  uint32_t spt = 0;
+  for (int i = i0; i < i1; ++i) {
+    sp += cnt[i];
+    spt += (cnt[i] + kBkPartMax - 1) / kBkPartMax;
+  }
+  s_pairs[t] = sp;
+  s_parts[t] = spt;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const unsigned long long a = t >= o ? s_pairs[t - o] : 0ull;
+    const uint32_t b = t >= o ? s_parts[t - o] : 0u;
+    __syncthreads();
+    s_pairs[t] += a;
+    s_parts[t] += b;
+    __syncthreads();
+  }
+  unsigned long long base = t ? s_pairs[t - 1] : 0ull;
+  uint32_t pbase = t ? s_parts[t - 1] : 0u;
+  for (int i = i0; i < i1; ++i) {
+    off[i] = (uint32_t)base;
+    cursor[i] = (uint32_t)base;
+    part_pref[i] = pbase;
+    base += cnt[i];
+    pbase += (cnt[i] + kBkPartMax - 1) / kBkPartMax;
+  }
+  if (t == 1023) {
+    part_pref[nbricks] = s_parts[1023];
+    ctl[0] = s_pairs[1023];
+    ctl[1] = s_parts[1023];
+  }
+}
+
+// Pass B.  Same spans as pass A; the workgroup counts its pairs per brick, reserves one
+// contiguous range per brick, then writes one self-contained 24-B record per pair (the
+// fine walk's state at the brick entry, so phase F makes ONE coalesced load per pair
+// and never touches the ray records):
+//   pa = {E01, E02, E12 at entry, cell | cells << 15 | ends << 22 | neg_x << 23 | ...}
+//   pb = {adq0 | adq2[0:14) << 18, adq1 | adq2[14:18) << 18}
+// Entry crossing counts at a brick boundary event (axis a, fine crossing k) come from
+// bk::counts_at; E = E(0) + c_a K_b - c_b K_a (exact mod 2^32, |E| < 2^29); the cell
+// count of a pair is the next entry index minus its own (the ray's last brick: up to and
+// including the end cell).
+__global__ __launch_bounds__(kBkThreads) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
+                                                         const ulonglong2* __restrict__ rays,
+                                                         uint32_t* __restrict__ cursor, uint4* __restrict__ pa,
+                                                         uint2* __restrict__ pb) {
+  extern __shared__ uint32_t hist[];
+  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int64_t pk0 = (int64_t)blockIdx.x * span, pk1 = min(npackets, pk0 + span);
+  for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
+    const ulonglong2 rec = rays[pk * 64 + l];
+    if (!(rec.y >> 63)) continue;
+    bk::QRay R;
+    bk::decode_ray(rec.x, rec.y, R);
+    bk_coarse(bg, R, [&](int b, int) { atomicAdd(&hist[b], 1u); });
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) {
+    const uint32_t n = hist[i];
+    if (n) hist[i] = atomicAdd(&cursor[i], n);
+  }
+  __syncthreads();
+  constexpr uint32_t m5 = bk::kB - 1;
+  for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
+    const ulonglong2 rec = rays[pk * 64 + l];
+    if (!(rec.y >> 63)) continue;
+    bk::QRay R;
+    bk::decode_ray(rec.x, rec.y, R);
+    const uint32_t K0 = (uint32_t)(2 * bk::kQ) * (uint32_t)R.adq[0], K1 = (uint32_t)(2 * bk::kQ) * (uint32_t)R.adq[1],
+                   K2 = (uint32_t)(2 * bk::kQ) * (uint32_t)R.adq[2];
+    const uint32_t e01 = (uint32_t)bk::e0_pair(R, 0, 1), e02 = (uint32_t)bk::e0_pair(R, 0, 2),
+                   e12 = (uint32_t)bk::e0_pair(R, 1, 2);
+    const uint32_t signs = (R.st[0] < 0 ? 1u << 23 : 0u) | (R.st[1] < 0 ? 1u << 24 : 0u) | (R.st[2] < 0 ? 1u << 25 : 0u);
+    const uint2 wb = make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
+                                (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18));
+    // entry state of the pair being built
+    auto entry = [&](const int32_t c[3]) {
+      uint4 e;
+      e.x = e01 + (uint32_t)c[0] * K1 - (uint32_t)c[1] * K0;
+      e.y = e02 + (uint32_t)c[0] * K2 - (uint32_t)c[2] * K0;
+      e.z = e12 + (uint32_t)c[1] * K2 - (uint32_t)c[2] * K1;
+      const uint32_t x = (uint32_t)(R.cs[0] + R.st[0] * c[0]) & m5, y = (uint32_t)(R.cs[1] + R.st[1] * c[1]) & m5,
+                     z = (uint32_t)(R.cs[2] + R.st[2] * c[2]) & m5;
+      e.w = (x << (2 * bk::kLog)) | (y << bk::kLog) | z | signs;
+      return e;
+    };
+    auto first_k = [&](int a) {
+      const int32_t o = R.cs[a] & (bk::kB - 1);
+      return R.st[a] > 0 ? bk::kB - 1 - o : o;
+    };
+    int32_t kb0 = first_k(0), kb1 = first_k(1), kb2 = first_k(2);
+    const int32_t c00[3] = {0, 0, 0};
+    uint4 cur = entry(c00);
+    uint32_t slot = 0;
+    int32_t idx_prev = 0;
+    bk_coarse(bg, R, [&](int b, int a) {
+      if (a >= 0) {
+        int32_t c[3];
+        // constant axis in each call: no dynamically indexed (scratch) arrays
+        if (a == 0) { bk::counts_at(R, 0, kb0, c); kb0 += bk::kB; }
+        else if (a == 1) { bk::counts_at(R, 1, kb1, c); kb1 += bk::kB; }
+        else { bk::counts_at(R, 2, kb2, c); kb2 += bk::kB; }
+        const int32_t idx = c[0] + c[1] + c[2];
+        cur.w |= (uint32_t)(idx - idx_prev) << 15;
+        pa[slot] = cur;
+        pb[slot] = wb;
+        cur = entry(c);
+        idx_prev = idx;
+      }
+      slot = atomicAdd(&hist[b], 1u);
+    });
+    cur.w |= ((uint32_t)(R.nsteps + 1 - idx_prev) << 15) | (R.end_inside ? 1u << 22 : 0u);
+    pa[slot] = cur;
+    pb[slot] = wb;
+  }
+}
+
+// Pair order inside a part: lane-adjacent picks come from S_ORDER far-apart regions of
+// the brick's list (neighbouring rays sit in the same cells at the same step, so taking
+// them together serialises the LDS adds), while each region is still read in order
+// (coalesced record loads).  A bijection on [0, n).
+template <int S_ORDER>
+__device__ inline uint32_t bk_order(uint32_t k, uint32_t n) {
+  if (S_ORDER <= 1) return k;
+  const uint32_t per = n / S_ORDER, n1 = per * S_ORDER;
+  return k < n1 ? (k % S_ORDER) * per + k / S_ORDER : k;
+}
+
+// Phase F (persistent; a work queue of parts, every workgroup exits when it is empty).
+// Each lane walks one pair at a time; a wave refills its idle lanes when >= REFILL are
+// idle, from per-lane records prefetched one refill ahead (their load latency is hidden
+// behind the walk of the current pairs).
+template <int REFILL, int S_ORDER>
+__global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const uint4* __restrict__ pa,
+                                                        const uint2* __restrict__ pb,
+                                                        const uint32_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ cnt,
+                                                        const uint32_t* __restrict__ part_pref,
+                                                        unsigned long long* __restrict__ ctl,
+                                                        int32_t* __restrict__ hits, int32_t* __restrict__ misses,
+                                                        unsigned long long* __restrict__ stats) {
+  extern __shared__ uint32_t box[];  // bk::kCells counters, then 4 control words
+  uint32_t* sh = box + bk::kCells;
+  stats = stat_slot(stats);
+  const int tid = threadIdx.x, l = tid & 63;
+  for (int i = tid; i < bk::kCells; i += blockDim.x) box[i] = 0;
+  const uint32_t nparts = (uint32_t)ctl[1];
+  const Tiles tl = tiles_of(g.n);
+  unsigned long long npairs = 0, nparts_done = 0, nflush = 0;
+  for (;;) {
+    if (tid == 0) {
+      sh[0] = (uint32_t)atomicAdd(&ctl[2], 1ull);
+      sh[1] = 0;
+    }
+    __syncthreads();
+    const uint32_t t = sh[0];
+    if (t >= nparts) break;
+    int lo = 0, hi = bg.nbricks - 1;  // last brick b with part_pref[b] <= t
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (part_pref[mid] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const int b = lo;
+    const uint32_t np = part_pref[b + 1] - part_pref[b], j = t - part_pref[b], nb_pairs = cnt[b];
+    const uint32_t p0 = off[b] + (uint32_t)(((uint64_t)nb_pairs * j) / np);
+    const uint32_t n = (uint32_t)(((uint64_t)nb_pairs * (j + 1)) / np) - (uint32_t)(((uint64_t)nb_pairs * j) / np);
+    const int bz = b % bg.nb[2], by = (b / bg.nb[2]) % bg.nb[1], bx = b / (bg.nb[2] * bg.nb[1]);
+    const int lo0 = bx << bk::kLog, lo1 = by << bk::kLog, lo2 = bz << bk::kLog;
+    if (tid == 0) {
+      npairs += n;
+      ++nparts_done;
+    }
+    // prefetched record of this lane's next pair
+    uint4 fa = make_uint4(0, 0, 0, 0);
+    uint2 fb = make_uint2(0, 0);
+    bool fok = false;
+    bool more = true;  // wave-uniform: unallocated pairs of the part remain
+    auto prefetch = [&](uint64_t need) {  // lanes in `need` allocate and load their next record
+      const int nn = __builtin_popcountll(need);
+      uint32_t base0 = 0;
+      if (l == 0) base0 = atomicAdd(&sh[1], (uint32_t)nn);
+      const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
+      if (base + (uint32_t)nn >= n) more = false;
+      if ((need >> l) & 1ull) {
+        const uint32_t k = base + (uint32_t)lane_prefix(need);
+        fok = k < n;
+        if (fok) {
+          const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
+          fa = pa[i];
+          fb = pb[i];
+        }
+      }
+    };
+    prefetch(~0ull);
+    // walk state
+    uint32_t left = 0, inc_last = 1;
+    int32_t E01 = 0, E02 = 0, E12 = 0, K0 = 0, K1 = 0, K2 = 0;
+    int cur = 0, dX = 0, dY = 0, dZ = 0;
+    for (;;) {
+      uint64_t act = __builtin_amdgcn_ballot_w64(left > 0);
+      if (__builtin_popcountll(act) <= 64 - REFILL) {
+        const uint64_t take = __builtin_amdgcn_ballot_w64(left == 0 && fok);
+        if (take) {
+          if (left == 0 && fok) {
+            E01 = (int32_t)fa.x;
+            E02 = (int32_t)fa.y;
+            E12 = (int32_t)fa.z;
+            const uint32_t w = fa.w;
+            const uint32_t a0 = fb.x & 0x3ffffu, a1 = fb.y & 0x3ffffu, a2 = (fb.x >> 18) | ((fb.y >> 18) << 14);
+            K0 = (int32_t)(a0 << 9);
+            K1 = (int32_t)(a1 << 9);
+            K2 = (int32_t)(a2 << 9);
+            cur = (int)(w & 0x7fffu) << 2;
+            left = (w >> 15) & 127u;
+            inc_last = (w >> 22) & 1u ? 0x10000u : 1u;
+            dX = (w >> 23) & 1u ? -(4 << (2 * bk::kLog)) : (4 << (2 * bk::kLog));
+            dY = (w >> 24) & 1u ? -(4 << bk::kLog) : (4 << bk::kLog);
+            dZ = (w >> 25) & 1u ? -4 : 4;
+            fok = false;
+          }
+          if (more) prefetch(take);
+          act = __builtin_amdgcn_ballot_w64(left > 0);
+        }
+      }
+      if (!act) {
+        if (!__builtin_amdgcn_ballot_w64(fok)) break;
+        continue;
+      }
+      if (left > 0) {
+        atomicAdd((uint32_t*)((char*)box + cur), left == 1 ? inc_last : 1u);
+        const bool b10 = E01 > 0;
+        const bool s2 = (b10 ? E12 : E02) > 0;
+        const bool s1 = !s2 && b10, s0 = !s2 && !b10;
+        E01 += s0 ? K1 : (s1 ? -K0 : 0);
+        E02 += s0 ? K2 : (s2 ? -K0 : 0);
+        E12 += s1 ? K2 : (s2 ? -K1 : 0);
+        cur += s2 ? dZ : (s1 ? dY : dX);
+        --left;
+      }
+    }
+    __syncthreads();
+    // flush: e -> 2x2x4 tile (e >> 4) of the brick, cell (e & 15) as in the tiled layout,
+    // so 16 lanes cover one 64-B counter line
+    const bool single = np == 1;
+    for (int e = tid; e < bk::kCells; e += blockDim.x) {
+      const int tile = e >> 4, w16 = e & 15;
+      const int tx = tile >> (2 * bk::kLog - 3), ty = (tile >> (bk::kLog - 2)) & ((bk::kB >> 1) - 1),
+                tz = tile & ((bk::kB >> 2) - 1);
+      const int lx = tx * 2 + (w16 >> 3), ly = ty * 2 + ((w16 >> 2) & 1), lz = tz * 4 + (w16 & 3);
+      const int li = (lx << (2 * bk::kLog)) + (ly << bk::kLog) + lz;
+      const uint32_t v = box[li];
+      if (v) {
+        box[li] = 0;
+        const uint32_t ti = tiled_index(tl, lo0 + lx, lo1 + ly, lo2 + lz);
+        const int32_t mi = (int32_t)(v & 0xffffu), hv = (int32_t)(v >> 16);
+        if (single) {
+          if (mi) misses[ti] += mi;
+          if (hv) hits[ti] += hv;
+        } else {
+          if (mi) atomic_add_dev(&misses[ti], mi);
+          if (hv) atomic_add_dev(&hits[ti], hv);
+        }
+        ++nflush;
+      }
+    }
+    __syncthreads();
+  }
+  if (stats) {
+    for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
+    if (l == 0 && nflush) atomicAdd(&stats[6], nflush);
+    if (tid == 0) {
+      if (npairs) atomicAdd(&stats[4], npairs);
+      if (nparts_done) atomicAdd(&stats[5], nparts_done);
+    }
+  }
+}
+
 // Tiled counters -> clamped int16 log-odds in the reference's x-major voxel order.
 // One lane per 4 consecutive z cells: one 16-B read per counter, one 8-B write.
 __global__ __launch_bounds__(256) void k_finalize(Geom g, const int32_t* __restrict__ hits,
@@ -700,13 +1121,119 @@ __global__ __launch_bounds__(256) void k_counter_layout(Geom g, const int32_t* _
   else dst[ti] = src[i];
 }
 
-// Kernel variant: DMF_FUSE_VARIANT=<n> selects an instantiation for A/B measurements.
+// Kernel variant: DMF_FUSE_VARIANT=<n> (or dmf_fuse_set_variant) selects an
+// implementation for A/B measurements; 0 = the default.
+static std::atomic<int> g_fuse_variant{-1};
 static int fuse_variant() {
-  static const int v = [] {
+  int v = g_fuse_variant.load(std::memory_order_relaxed);
+  if (v < 0) {
     const char* e = getenv("DMF_FUSE_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
+    v = e ? atoi(e) : 0;
+    g_fuse_variant.store(v, std::memory_order_relaxed);
+  }
   return v;
+}
+constexpr int kVariantBrick = 40;
+static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantBrick + 3; }
+static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
+
+static BkGeom brick_geom(const Geom& g) {
+  BkGeom bg;
+  for (int a = 0; a < 3; ++a) bg.nb[a] = (g.n[a] + bk::kB - 1) >> bk::kLog;
+  bg.nbricks = bg.nb[0] * bg.nb[1] * bg.nb[2];
+  return bg;
+}
+
+// The brick path covers grids up to 1024 cells per axis (18-bit |dq| fields in the
+// pair record) and <= 32768 bricks (LDS histogram of passes A/B).
+static bool brick_path_ok(const Geom& g) {
+  const BkGeom bg = brick_geom(g);
+  return g.n[0] <= 1024 && g.n[1] <= 1024 && g.n[2] <= 1024 && bg.nbricks <= 32768;
+}
+
+static int cu_count(int device) {
+  static std::atomic<int> cached{0};
+  int n = cached.load();
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) n = 256;
+    cached.store(n);
+  }
+  return n;
+}
+
+// Brick-owned fusion of P frames (kernels above), in pose batches whose ray indices fit
+// the pair record and whose pair offsets fit 32 bits.
+static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint16_t* d_depth, const PoseX* tab, int P,
+                       const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses, unsigned long long* st) {
+  const BkGeom bg = brick_geom(g);
+  const int pkx = (cp.W + 7) / 8, pky = (cp.H + 7) / 8;
+  const int64_t ppose = (int64_t)pkx * pky;
+  const int64_t max_pairs_ray = 1 + (bg.nb[0] - 1) + (bg.nb[1] - 1) + (bg.nb[2] - 1);
+  const int64_t ray_cap = (int64_t)UINT32_MAX / max_pairs_ray;
+  const int64_t PB = std::min<int64_t>(P, ray_cap / (ppose * 64));
+  if (PB < 1) return fail(DMF_ERR_RANGE, "image too large for one brick fusion batch");
+  const int span = std::max(128, (bg.nbricks + 31) / 32);  // packets per workgroup of passes A/B
+  const size_t hist_bytes = sizeof(uint32_t) * (size_t)bg.nbricks;
+  static std::atomic<bool> attr_set{false};
+  if (!attr_set.load()) {
+    for (const void* f : {(const void*)k_bk_fuse<16, 8>, (const void*)k_bk_fuse<16, 1>, (const void*)k_bk_fuse<32, 8>,
+                          (const void*)k_bk_fuse<8, 8>})
+      DMF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kBkFuseLds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(uint32_t) * 32768)));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(uint32_t) * 32768)));
+    attr_set.store(true);
+  }
+  void *rays, *bricks, *ctl;
+  DMF_TRY(scratch(v, kScBkRays, sizeof(ulonglong2) * (size_t)(PB * ppose * 64), &rays));
+  DMF_TRY(scratch(v, kScBkBricks, sizeof(uint32_t) * (4 * (size_t)bg.nbricks + 4), &bricks));
+  DMF_TRY(scratch(v, kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
+  uint32_t* cnt = (uint32_t*)bricks;
+  uint32_t* off = cnt + bg.nbricks;
+  uint32_t* cursor = off + bg.nbricks;
+  uint32_t* part_pref = cursor + bg.nbricks;  // nbricks + 1
+  unsigned long long* ctlp = (unsigned long long*)ctl;
+  const int ncu = cu_count(v->device);
+  for (int64_t p0 = 0; p0 < P; p0 += PB) {
+    const int64_t pb = std::min<int64_t>(PB, P - p0);
+    const int64_t npk = pb * ppose;
+    const unsigned nwg = (unsigned)((npk + span - 1) / span);
+    DMF_HIP(hipMemsetAsync(cnt, 0, hist_bytes, v->stream));
+    DMF_HIP(hipMemsetAsync(ctlp, 0, sizeof(unsigned long long) * 4, v->stream));
+    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(kBkThreads), hist_bytes, v->stream, g, cp,
+                       d_depth + (size_t)p0 * cp.H * cp.W, tab + p0, prm->dmin_mm, prm->dmax_mm, pkx, (int)ppose, npk,
+                       span, bg, (ulonglong2*)rays, cnt, st);
+    DMF_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, v->stream, bg.nbricks, (const uint32_t*)cnt, off, cursor,
+                       part_pref, ctlp);
+    DMF_LAUNCH_CHECK();
+    unsigned long long hc[2];
+    DMF_HIP(hipMemcpyAsync(hc, ctlp, sizeof(hc), hipMemcpyDeviceToHost, v->stream));
+    DMF_HIP(hipStreamSynchronize(v->stream));
+    if (hc[0] > (unsigned long long)UINT32_MAX) return fail(DMF_ERR_RANGE, "brick fusion batch exceeds 2^32 pairs");
+    if (hc[0] == 0) continue;
+    void *pra, *prb;
+    DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * (size_t)hc[0], &pra));
+    DMF_TRY(scratch(v, kScBkPairsB, sizeof(uint2) * (size_t)hc[0], &prb));
+    hipLaunchKernelGGL(k_bk_pairs, dim3(nwg), dim3(kBkThreads), hist_bytes, v->stream, npk, span, bg,
+                       (const ulonglong2*)rays, cursor, (uint4*)pra, (uint2*)prb);
+    DMF_LAUNCH_CHECK();
+    const unsigned nf = (unsigned)std::min<unsigned long long>((unsigned long long)ncu, hc[1]);
+#define DMF_BK_FUSE(R, S)                                                                                        \
+  hipLaunchKernelGGL((k_bk_fuse<R, S>), dim3(nf), dim3(kBkThreads), kBkFuseLds, v->stream, g, bg, (const uint4*)pra, \
+                     (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt, (const uint32_t*)part_pref, ctlp,  \
+                     d_hits, d_misses, st)
+    switch (fuse_variant()) {
+      case 41: DMF_BK_FUSE(16, 1); break;
+      case 42: DMF_BK_FUSE(32, 8); break;
+      case 43: DMF_BK_FUSE(8, 8); break;
+      default: DMF_BK_FUSE(16, 8); break;
+    }
+#undef DMF_BK_FUSE
+    DMF_LAUNCH_CHECK();
+  }
+  return DMF_OK;
 }
 
 static int check_fuse(const dmf_volume* v, const dmf_camera* cam, int P, const dmf_fuse_params* prm) {
@@ -735,8 +1262,18 @@ const char* dmf_fuse_kernel(void) {
     case 31: return "dmf::k_fuse_l<12, 1280>";
     case 32: return "dmf::k_fuse_l<14, 1536>";
     case 33: return "dmf::k_fuse_l<12, 1536>";
+    case 40: return "dmf::k_bk_fuse<16, 8>";
+    case 41: return "dmf::k_bk_fuse<16, 1>";
+    case 42: return "dmf::k_bk_fuse<32, 8>";
+    case 43: return "dmf::k_bk_fuse<8, 8>";
     default: return "dmf::k_fuse_l<12, 1280>";
   }
+}
+
+int dmf_fuse_set_variant(int32_t variant) {
+  if (!is_known_variant(variant)) return fail(DMF_ERR_INVALID, "unknown fusion variant %d", variant);
+  g_fuse_variant.store(variant, std::memory_order_relaxed);
+  return DMF_OK;
 }
 
 int dmf_fuse_counter_cells(const dmf_volume* v, int64_t* n) {
@@ -773,6 +1310,12 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
   unsigned long long* st = nullptr;
   if (d_stats) DMF_TRY(stats_begin(v, &st));
   const int pkx = (cp.W + 7) / 8;
+  if (is_brick_variant(fuse_variant()) && brick_path_ok(g)) {
+    DMF_TRY(fuse_bricks(v, cp, g, d_depth, tab, P, prm, d_hits, d_misses, st));
+    if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
+    DMF_LAUNCH_CHECK();
+    return DMF_OK;
+  }
 #define DMF_FUSE_LAUNCH_R(K, NR)                                                                               \
   hipLaunchKernelGGL(K, dim3((unsigned)(pkx * ((cp.H + 8 * (NR) - 1) / (8 * (NR)))), (unsigned)P), dim3(64), 0,        \
                      v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, d_misses, st)

@@ -49,7 +49,8 @@ int require_constructed(const dmf_volume* v);
 int scratch(dmf_volume* v, int k, size_t bytes, void** out);
 enum ScratchSlot {
   kScPoses = 0, kScHost0, kScHost1, kScHost2, kScOut0, kScOut1, kScOut2, kScOut3, kScTmp, kScSort0,
-  kScSort1, kScSort2, kScSort3, kScCount, kScStats
+  kScSort1, kScSort2, kScSort3, kScCount, kScStats,
+  kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkChunks, kScBkCtl  // brick-owned fusion (dmf_fuse.hip)
 };
 
 // Striped statistics: kernels add into slot (block % kStatSlots) of a zeroed buffer

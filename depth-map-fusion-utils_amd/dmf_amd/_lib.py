@@ -64,6 +64,7 @@ SIGNATURES = {
     "dmf_fuse_params_default": (None, [_p]),
     "dmf_angle_threshold": (C.c_int, [_p]),
     "dmf_fuse_kernel": (C.c_char_p, []),
+    "dmf_fuse_set_variant": (C.c_int, [_i32]),
     "dmf_volume_create": (C.c_int, [_p, _i32]),
     "dmf_volume_destroy": (C.c_int, [_vp]),
     "dmf_volume_set_stream": (C.c_int, [_vp, _vp]),

@@ -93,6 +93,11 @@ void dmf_fuse_params_default(dmf_fuse_params* p);
 int dmf_angle_threshold(float* dstar);
 /* Diagnostic: name of the fusion kernel dmf_fuse_depth* launches (DMF_FUSE_VARIANT). */
 const char* dmf_fuse_kernel(void);
+/* Diagnostic / A-B: select the fusion implementation for this process (0 = default,
+ * 1 = one device atomic per update, 24/30-33 = LDS-box kernels, 40 = brick-owned
+ * fusion; grids over 1024 cells per axis always use the LDS-box kernel).  Results are
+ * identical for every variant. */
+int dmf_fuse_set_variant(int32_t variant);
 
 /* ---- VoxelVolume  (Volume.hpp:50-255) ------------------------------------ */
 /* VoxelVolume::VoxelVolume()  Volume.hpp:63 — device = HIP device ordinal. */

@@ -578,3 +578,42 @@ def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
     finally:
         for p_ in (dp, dk, ds):
             L.dmf_device_free(h, p_)
+
+
+@pytest.fixture(params=[40, 41, 42, 43])
+def brick_variant(dmf, request):
+    """Select a brick-owned fusion variant (DMF_FUSE_VARIANT 40-43: refill threshold
+    and pair order) for one test."""
+    from dmf_amd import _lib
+    L = _lib.load()
+    _lib.check(L.dmf_fuse_set_variant(request.param))
+    assert L.dmf_fuse_kernel().decode().startswith("dmf::k_bk_fuse<")
+    yield
+    _lib.check(L.dmf_fuse_set_variant(0))
+
+
+@pytest.mark.parametrize("dims,nframes", [((128, 128, 128), 6),   # 4^3 bricks
+                                          ((100, 100, 100), 3),   # partial edge bricks
+                                          ((61, 50, 47), 3),      # odd dims, padded tiles
+                                          ((32, 32, 32), 6)])     # one brick, ~30 parts: atomic flush
+def test_fuse_brick_path(oracle, engine, dmf, brick_variant, dims, nframes):
+    """Brick-owned fusion (k_bk_rays / k_bk_pairs / k_bk_fuse, dmf_brick.hpp): the
+    per-brick restart of the exact walk must give the oracle's counters bit for bit,
+    for single-part bricks (plain adds) and multi-part bricks (device atomics)."""
+    poses, depth, _ = Hh.frames()
+    poses = np.concatenate([poses, Hh.ref_style_poses()[:2]])[:nframes + 2]
+    depth = np.concatenate([depth, depth[:2]])[:nframes + 2]
+    ov = oracle.Volume()
+    ov.setDimensions(*Hh.BOUNDS)
+    ov.setVolumeSize(*dims)
+    ov.constructVolume()
+    ho, mo, so = oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
+    gv = dmf.VoxelVolume()
+    gv.setDimensions(*Hh.BOUNDS)
+    gv.setVolumeSize(*dims)
+    gv.constructVolume()
+    prm = dmf.FuseParams(dmin_mm=200, dmax_mm=1000)
+    for _ in range(2):  # repeatable (LDS counters, work queue)
+        hg, mg, sg = engine.fuse_depth(gv, depth, poses, prm)
+        assert np.array_equal(so, sg)
+        assert np.array_equal(ho, hg) and np.array_equal(mo, mg)

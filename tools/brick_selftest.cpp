@@ -1,0 +1,182 @@
+// CPU self-test of the exact brick decomposition (csrc/dmf_brick.hpp) against the
+// plain fine walk of oracle.cpp dda_ray (64-bit crossing times, ties x < y < z).
+// For random and adversarial fixed-point rays on grids that are and are not
+// multiples of 32 cells it checks that
+//   1. the coarse walk lists exactly the bricks the fine walk passes through, in order;
+//   2. for every such brick, pair_in_brick's entry counts, cell count and end flag
+//      restart the int32 fine walk (E = E0 + c_a K_b - c_b K_a) on exactly the cells
+//      the fine walk visits there.
+// Build: make -C depth-map-fusion-utils_amd build/brick_selftest ; run: <exe> [rays] [seed]
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "dmf_brick.hpp"
+
+using namespace dmf::brick;
+
+struct Cell {
+  int x, y, z;
+  bool operator==(const Cell& o) const { return x == o.x && y == o.y && z == o.z; }
+};
+
+// oracle.cpp dda_ray lines 781-818, from quantised endpoints
+static void fine_walk(const int64_t qs[3], const int64_t qe[3], std::vector<Cell>& out) {
+  int64_t cs[3], ce[3], adq[3], step[3];
+  for (int a = 0; a < 3; ++a) {
+    cs[a] = qs[a] / kQ;
+    ce[a] = qe[a] / kQ;
+    const int64_t dq = qe[a] - qs[a];
+    adq[a] = dq < 0 ? -dq : dq;
+    step[a] = ce[a] > cs[a] ? 1 : (ce[a] < cs[a] ? -1 : 0);
+  }
+  uint64_t Tm[3], In[3];
+  for (int a = 0; a < 3; ++a) {
+    if (step[a] == 0) { Tm[a] = UINT64_MAX; In[a] = 0; continue; }
+    uint64_t M = 1;
+    for (int b = 0; b < 3; ++b)
+      if (b != a && adq[b] > 0) M *= (uint64_t)adq[b];
+    const int64_t h = step[a] > 0 ? 2 * ((cs[a] + 1) * kQ - qs[a]) : 2 * (qs[a] - cs[a] * kQ) + 1;
+    Tm[a] = (uint64_t)h * M;
+    In[a] = (uint64_t)(2 * kQ) * M;
+  }
+  int64_t nsteps = 0;
+  for (int a = 0; a < 3; ++a) nsteps += ce[a] > cs[a] ? ce[a] - cs[a] : cs[a] - ce[a];
+  int64_t cur[3] = {cs[0], cs[1], cs[2]};
+  out.clear();
+  for (int64_t s = 0; s < nsteps; ++s) {
+    out.push_back({(int)cur[0], (int)cur[1], (int)cur[2]});
+    int a = 0;
+    if (Tm[1] < Tm[a]) a = 1;
+    if (Tm[2] < Tm[a]) a = 2;
+    cur[a] += step[a];
+    Tm[a] += In[a];
+  }
+  out.push_back({(int)cur[0], (int)cur[1], (int)cur[2]});
+}
+
+// The kernels' int32 walk (dmf_fuse.hip dda_select) restarted from crossing counts c.
+static void restart_walk(const QRay& r, const int32_t c[3], int cells, std::vector<Cell>& out) {
+  const uint32_t K[3] = {(uint32_t)(2 * kQ * r.adq[0]), (uint32_t)(2 * kQ * r.adq[1]), (uint32_t)(2 * kQ * r.adq[2])};
+  int32_t E01 = (int32_t)((uint32_t)e0_pair(r, 0, 1) + (uint32_t)c[0] * K[1] - (uint32_t)c[1] * K[0]);
+  int32_t E02 = (int32_t)((uint32_t)e0_pair(r, 0, 2) + (uint32_t)c[0] * K[2] - (uint32_t)c[2] * K[0]);
+  int32_t E12 = (int32_t)((uint32_t)e0_pair(r, 1, 2) + (uint32_t)c[1] * K[2] - (uint32_t)c[2] * K[1]);
+  int x = r.cs[0] + r.st[0] * c[0], y = r.cs[1] + r.st[1] * c[1], z = r.cs[2] + r.st[2] * c[2];
+  out.clear();
+  for (int k = 0; k < cells; ++k) {
+    out.push_back({x, y, z});
+    const bool b10 = E01 > 0;
+    const bool s2 = (b10 ? E12 : E02) > 0;
+    const bool s1 = !s2 && b10, s0 = !s2 && !b10;
+    E01 = (int32_t)((uint32_t)E01 + (s0 ? K[1] : (s1 ? (uint32_t)-K[0] : 0u)));
+    E02 = (int32_t)((uint32_t)E02 + (s0 ? K[2] : (s2 ? (uint32_t)-K[0] : 0u)));
+    E12 = (int32_t)((uint32_t)E12 + (s1 ? K[2] : (s2 ? (uint32_t)-K[1] : 0u)));
+    x += s0 ? r.st[0] : 0;
+    y += s1 ? r.st[1] : 0;
+    z += s2 ? r.st[2] : 0;
+  }
+}
+
+int main(int argc, char** argv) {
+  const long nrays = argc > 1 ? atol(argv[1]) : 200000;
+  const unsigned seed = argc > 2 ? (unsigned)atol(argv[2]) : 1234u;
+  std::mt19937_64 rng(seed);
+  auto U = [&](int64_t lo, int64_t hi) { return lo + (int64_t)(rng() % (uint64_t)(hi - lo + 1)); };
+  const int grids[][3] = {{64, 64, 64}, {96, 40, 33}, {128, 128, 128}, {200, 31, 77}, {512, 512, 512},
+                          {37, 300, 65}, {1024, 1024, 1024}, {1, 90, 5}};
+  std::vector<Cell> fine, seg;
+  long checked = 0, pairs = 0, bad = 0;
+  for (long i = 0; i < nrays && bad < 10; ++i) {
+    const int* ng = grids[i % 8];
+    int64_t qs[3], qe[3];
+    const int mode = (int)(i % 7);
+    for (int a = 0; a < 3; ++a) {
+      const int64_t span = (int64_t)ng[a] * kQ - 1;
+      qs[a] = U(0, span);
+      qe[a] = U(0, span);
+    }
+    if (mode == 1) {  // shared fractions: exact ties between axes
+      const int64_t f = U(0, kQ - 1);
+      for (int a = 0; a < 3; ++a) { qs[a] = qs[a] / kQ * kQ + f; qe[a] = qe[a] / kQ * kQ + f; }
+    } else if (mode == 2) {  // equal |dq| on two or three axes (exact diagonals)
+      const int64_t d = U(1, 40 * kQ);
+      for (int a = 0; a < 3; ++a) {
+        const int64_t span = (int64_t)ng[a] * kQ - 1;
+        qs[a] = U(0, span);
+        qe[a] = qs[a] + ((a + i) % 2 ? d : -d);
+        if (qe[a] < 0 || qe[a] > span) qe[a] = qs[a];
+      }
+    } else if (mode == 3) {  // axis-aligned / planar rays
+      const int a = (int)(i / 7 % 3);
+      for (int b = 0; b < 3; ++b)
+        if (b != a && (i / 21) % 2) qe[b] = qs[b];
+      qe[(a + 1) % 3] = qs[(a + 1) % 3];
+    } else if (mode == 4) {  // endpoints on brick boundaries and cell corners
+      for (int a = 0; a < 3; ++a) {
+        const int64_t nb = (ng[a] + kB - 1) / kB;
+        qs[a] = std::min<int64_t>(U(0, nb) * kB * kQ, (int64_t)ng[a] * kQ - 1);
+        qe[a] = std::min<int64_t>(U(0, nb) * kB * kQ + U(-1, 0) * kQ, (int64_t)ng[a] * kQ - 1);
+        if (qe[a] < 0) qe[a] = 0;
+      }
+    } else if (mode == 5) {  // short rays inside one or two bricks
+      for (int a = 0; a < 3; ++a) {
+        const int64_t span = (int64_t)ng[a] * kQ - 1;
+        qe[a] = std::max<int64_t>(0, std::min<int64_t>(span, qs[a] + U(-40 * kQ, 40 * kQ)));
+      }
+    }
+    const bool end_inside = (rng() & 1) != 0;
+    uint64_t A, B;
+    pack_ray(qs, qe, end_inside, A, B);
+    QRay r;
+    decode_ray(A, B, r);
+    fine_walk(qs, qe, fine);
+    if ((int)fine.size() != r.nsteps + 1) { printf("nsteps mismatch\n"); ++bad; continue; }
+    // 1. brick sequence
+    std::vector<int> fb;  // brick ids of fine cells, consecutive duplicates removed
+    const int nbx = (ng[0] + kB - 1) / kB, nby = (ng[1] + kB - 1) / kB, nbz = (ng[2] + kB - 1) / kB;
+    auto bid = [&](const Cell& c) { return ((c.x >> kLog) * nby + (c.y >> kLog)) * nbz + (c.z >> kLog); };
+    for (const Cell& c : fine)
+      if (fb.empty() || fb.back() != bid(c)) fb.push_back(bid(c));
+    Coarse w;
+    coarse_init(r, w);
+    std::vector<int> cb;
+    int bx = r.cs[0] >> kLog, by = r.cs[1] >> kLog, bz = r.cs[2] >> kLog;
+    cb.push_back((bx * nby + by) * nbz + bz);
+    for (int s = 0; s < w.total; ++s) {
+      const int a = coarse_next(w);
+      if (a == 0) bx += r.st[0];
+      if (a == 1) by += r.st[1];
+      if (a == 2) bz += r.st[2];
+      cb.push_back((bx * nby + by) * nbz + bz);
+    }
+    if (cb != fb) {
+      printf("ray %ld: coarse bricks differ (%zu vs %zu)\n", i, cb.size(), fb.size());
+      ++bad;
+      continue;
+    }
+    // 2. per-brick restart
+    size_t pos = 0;
+    for (int b : cb) {
+      const int32_t bb[3] = {b / (nby * nbz), (b / nbz) % nby, b % nbz};
+      Pair p;
+      pair_in_brick(r, bb, ng, p);
+      restart_walk(r, p.cin, p.cells, seg);
+      size_t len = 0;
+      while (pos + len < fine.size() && bid(fine[pos + len]) == b) ++len;
+      bool ok = p.cells == (int)len && p.ends == (pos + len == fine.size());
+      for (size_t k = 0; ok && k < len; ++k) ok = seg[k] == fine[pos + k];
+      if (!ok) {
+        printf("ray %ld (mode %d) brick %d: cells %d vs %zu, ends %d\n", i, mode, b, p.cells, len, (int)p.ends);
+        ++bad;
+        break;
+      }
+      pos += len;
+      ++pairs;
+    }
+    ++checked;
+  }
+  printf("brick selftest: %ld rays, %ld (ray, brick) pairs, %ld failures\n", checked, pairs, bad);
+  return bad ? 1 : 0;
+}
