@@ -719,8 +719,14 @@ struct BkGeom {
 };
 
 constexpr int kBkThreads = 1024;
+constexpr int kBkPassThreads = 256;  // passes A/B: 4 waves per workgroup, several workgroups per CU
 constexpr uint32_t kBkPartMax = 65535;  // pairs per part: 16-bit miss / hit fields never carry
-constexpr int kBkFuseLds = bk::kCells * 4 + 16;
+// LDS box of phase F: cell (x, y, z) of the brick at word x*kSx + y*kSy + z.  The skew
+// (kSy = 33, kSx = 32*33 + 1) puts the cell in bank (x + y + z) mod 32 instead of z alone,
+// so lanes on different rows/columns of one z-plane do not collide.
+constexpr int kBkSy = bk::kB + 1, kBkSx = bk::kB * kBkSy + 1;
+constexpr int kBkBoxWords = bk::kB * kBkSx;               // 33824 words
+constexpr int kBkFuseLds = kBkBoxWords * 4 + 16;         // 135,312 B of the CU's 160 KiB
 
 __device__ inline int bk_index(const BkGeom& bg, int x, int y, int z) { return (x * bg.nb[1] + y) * bg.nb[2] + z; }
 
@@ -740,8 +746,43 @@ __device__ inline void bk_coarse(const BkGeom& bg, const bk::QRay& R, F&& f) {
   }
 }
 
-// Pass A.  Workgroup = 16 waves over a span of 8x8 packets; ray index = packet * 64 + lane.
-__global__ __launch_bounds__(kBkThreads) void k_bk_rays(Geom g, CamP cam, const uint16_t* __restrict__ depth,
+// Wave-aggregated LDS histogram add: the lanes of a packet walk near-parallel rays and
+// name the same brick at the same coarse step, so one atomic per distinct brick among
+// the active lanes replaces a same-address atomic per lane (which the LDS serialises).
+// Callable from divergent code: the loop runs over the currently active lanes.
+__device__ inline void hist_add_agg(uint32_t* hist, int b) {
+  uint64_t rem = __builtin_amdgcn_ballot_w64(true);
+  const int l = (int)(threadIdx.x & 63);
+  while (rem) {
+    const int leader = __builtin_ctzll(rem);
+    const int bl = __builtin_amdgcn_readlane(b, leader);
+    const uint64_t same = __builtin_amdgcn_ballot_w64(b == bl) & rem;
+    if (l == leader) atomicAdd(&hist[bl], (uint32_t)__builtin_popcountll(same));
+    rem &= ~same;
+  }
+}
+
+// As hist_add_agg, returning this lane's slot (the old count plus its rank among the
+// lanes naming the same brick).
+__device__ inline uint32_t hist_take_agg(uint32_t* hist, int b) {
+  uint64_t rem = __builtin_amdgcn_ballot_w64(true);
+  const int l = (int)(threadIdx.x & 63);
+  uint32_t slot = 0;
+  while (rem) {
+    const int leader = __builtin_ctzll(rem);
+    const int bl = __builtin_amdgcn_readlane(b, leader);
+    const uint64_t same = __builtin_amdgcn_ballot_w64(b == bl) & rem;
+    uint32_t old = 0;
+    if (l == leader) old = atomicAdd(&hist[bl], (uint32_t)__builtin_popcountll(same));
+    old = (uint32_t)__builtin_amdgcn_readlane((int)old, leader);
+    if ((same >> l) & 1ull) slot = old + (uint32_t)lane_prefix(same);
+    rem &= ~same;
+  }
+  return slot;
+}
+
+// Pass A.  Workgroup = 4 waves over a span of 8x8 packets; ray index = packet * 64 + lane.
+__global__ __launch_bounds__(kBkPassThreads) void k_bk_rays(Geom g, CamP cam, const uint16_t* __restrict__ depth,
                                                         const PoseX* __restrict__ poses, int dmin, int dmax,
                                                         int packets_x, int packets_pose, int64_t npackets, int span,
                                                         BkGeom bg, ulonglong2* __restrict__ rays,
@@ -772,7 +813,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_rays(Geom g, CamP cam, const 
       bk::decode_ray(A, B, R);
       upd += (unsigned long long)(R.nsteps + 1);
       nhit += inside ? 1 : 0;
-      bk_coarse(bg, R, [&](int b, int) { atomicAdd(&hist[b], 1u); });
+      bk_coarse(bg, R, [&](int b, int) { hist_add_agg(hist, b); });
     }
     nvalid += valid ? 1 : 0;
     rays[pk * 64 + l] = rec;
@@ -840,7 +881,7 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
 // bk::counts_at; E = E(0) + c_a K_b - c_b K_a (exact mod 2^32, |E| < 2^29); the cell
 // count of a pair is the next entry index minus its own (the ray's last brick: up to and
 // including the end cell).
-__global__ __launch_bounds__(kBkThreads) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
+__global__ __launch_bounds__(kBkPassThreads) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
                                                          uint32_t* __restrict__ cursor, uint4* __restrict__ pa,
                                                          uint2* __restrict__ pb) {
@@ -854,7 +895,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_pairs(int64_t npackets, int s
     if (!(rec.y >> 63)) continue;
     bk::QRay R;
     bk::decode_ray(rec.x, rec.y, R);
-    bk_coarse(bg, R, [&](int b, int) { atomicAdd(&hist[b], 1u); });
+    bk_coarse(bg, R, [&](int b, int) { hist_add_agg(hist, b); });
   }
   __syncthreads();
   for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) {
@@ -873,8 +914,8 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_pairs(int64_t npackets, int s
     const uint32_t e01 = (uint32_t)bk::e0_pair(R, 0, 1), e02 = (uint32_t)bk::e0_pair(R, 0, 2),
                    e12 = (uint32_t)bk::e0_pair(R, 1, 2);
     const uint32_t signs = (R.st[0] < 0 ? 1u << 23 : 0u) | (R.st[1] < 0 ? 1u << 24 : 0u) | (R.st[2] < 0 ? 1u << 25 : 0u);
-    const uint2 wb = make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
-                                (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18));
+    const uint2 wb0 = make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
+                                 (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18));
     // entry state of the pair being built
     auto entry = [&](const int32_t c[3]) {
       uint4 e;
@@ -886,6 +927,9 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_pairs(int64_t npackets, int s
       e.w = (x << (2 * bk::kLog)) | (y << bk::kLog) | z | signs;
       return e;
     };
+    // the end cell (brick-local) rides in the spare bits: low 6 in pa.w[26:32), high 9 in pb.y[22:31)
+    const uint32_t endc = (((uint32_t)R.ce[0] & m5) << (2 * bk::kLog)) | (((uint32_t)R.ce[1] & m5) << bk::kLog) |
+                          ((uint32_t)R.ce[2] & m5);
     auto first_k = [&](int a) {
       const int32_t o = R.cs[a] & (bk::kB - 1);
       return R.st[a] > 0 ? bk::kB - 1 - o : o;
@@ -905,15 +949,15 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_pairs(int64_t npackets, int s
         const int32_t idx = c[0] + c[1] + c[2];
         cur.w |= (uint32_t)(idx - idx_prev) << 15;
         pa[slot] = cur;
-        pb[slot] = wb;
+        pb[slot] = wb0;
         cur = entry(c);
         idx_prev = idx;
       }
-      slot = atomicAdd(&hist[b], 1u);
+      slot = hist_take_agg(hist, b);
     });
-    cur.w |= ((uint32_t)(R.nsteps + 1 - idx_prev) << 15) | (R.end_inside ? 1u << 22 : 0u);
+    cur.w |= ((uint32_t)(R.nsteps + 1 - idx_prev) << 15) | (R.end_inside ? 1u << 22 : 0u) | ((endc & 63u) << 26);
     pa[slot] = cur;
-    pb[slot] = wb;
+    pb[slot] = make_uint2(wb0.x, wb0.y | ((endc >> 6) << 22));
   }
 }
 
@@ -932,7 +976,7 @@ __device__ inline uint32_t bk_order(uint32_t k, uint32_t n) {
 // Each lane walks one pair at a time; a wave refills its idle lanes when >= REFILL are
 // idle, from per-lane records prefetched one refill ahead (their load latency is hidden
 // behind the walk of the current pairs).
-template <int REFILL, int S_ORDER>
+template <int REFILL, int S_ORDER, bool BATCH>
 __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const uint4* __restrict__ pa,
                                                         const uint2* __restrict__ pb,
                                                         const uint32_t* __restrict__ off,
@@ -941,11 +985,11 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
                                                         unsigned long long* __restrict__ ctl,
                                                         int32_t* __restrict__ hits, int32_t* __restrict__ misses,
                                                         unsigned long long* __restrict__ stats) {
-  extern __shared__ uint32_t box[];  // bk::kCells counters, then 4 control words
-  uint32_t* sh = box + bk::kCells;
+  extern __shared__ uint32_t box[];  // kBkBoxWords counters (skewed), then 4 control words
+  uint32_t* sh = box + kBkBoxWords;
   stats = stat_slot(stats);
   const int tid = threadIdx.x, l = tid & 63;
-  for (int i = tid; i < bk::kCells; i += blockDim.x) box[i] = 0;
+  for (int i = tid; i < kBkBoxWords; i += blockDim.x) box[i] = 0;
   const uint32_t nparts = (uint32_t)ctl[1];
   const Tiles tl = tiles_of(g.n);
   unsigned long long npairs = 0, nparts_done = 0, nflush = 0;
@@ -973,11 +1017,50 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       npairs += n;
       ++nparts_done;
     }
-    // prefetched record of this lane's next pair
-    uint4 fa = make_uint4(0, 0, 0, 0);
-    uint2 fb = make_uint2(0, 0);
-    bool fok = false;
-    bool more = true;  // wave-uniform: unallocated pairs of the part remain
+    // walk state (K negated once per pair: the step is adds and selects only)
+    uint32_t left = 0;
+    int32_t E01 = 0, E02 = 0, E12 = 0, K1 = 0, K2 = 0, nK0 = 0, nK1 = 0;
+    int cur = 0, dX = 0, dY = 0, dZ = 0;
+    auto decode = [&](const uint4& ra, const uint2& rb) {
+      E01 = (int32_t)ra.x;
+      E02 = (int32_t)ra.y;
+      E12 = (int32_t)ra.z;
+      const uint32_t w = ra.w;
+      const uint32_t a0 = rb.x & 0x3ffffu, a1 = rb.y & 0x3ffffu, a2 = (rb.x >> 18) | (((rb.y >> 18) & 15u) << 14);
+      nK0 = -(int32_t)(a0 << 9);
+      K1 = (int32_t)(a1 << 9);
+      K2 = (int32_t)(a2 << 9);
+      nK1 = -K1;
+      cur = (int)(((w >> 10) & 31u) * kBkSx + ((w >> 5) & 31u) * kBkSy + (w & 31u)) << 2;
+      left = (w >> 15) & 127u;
+      dX = (w >> 23) & 1u ? -(4 * kBkSx) : 4 * kBkSx;
+      dY = (w >> 24) & 1u ? -(4 * kBkSy) : 4 * kBkSy;
+      dZ = (w >> 25) & 1u ? -4 : 4;
+      if ((w >> 22) & 1u) {  // the ray ends inside this brick: its end cell takes the hit
+        const uint32_t e = (w >> 26) | ((rb.y >> 22) << 6);
+        atomicAdd(&box[((e >> 10) & 31u) * kBkSx + ((e >> 5) & 31u) * kBkSy + (e & 31u)], 0x10000u);
+        --left;  // ... and the walk covers the cells before it
+      }
+    };
+    // BATCH: two 64-record batches per wave; `c` is handed out to idle lanes (ds_bpermute
+    // from the lane holding the record) while `x` is in flight.  Otherwise: one record
+    // per lane (in c), prefetched one refill ahead.
+    uint4 ca = make_uint4(0, 0, 0, 0), xa = ca;
+    uint2 cb = make_uint2(0, 0), xb = cb;
+    int c_n = 0, c_pos = 0, x_n = 0;
+    bool fok = false, more = true;
+    auto load_batch = [&](uint4& ra, uint2& rb) -> int {
+      uint32_t base0 = 0;
+      if (l == 0) base0 = atomicAdd(&sh[1], 64u);
+      const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
+      const int cntb = base >= n ? 0 : (int)min(64u, n - base);
+      if (l < cntb) {
+        const uint32_t i = p0 + bk_order<S_ORDER>(base + (uint32_t)l, n);
+        ra = pa[i];
+        rb = pb[i];
+      }
+      return cntb;
+    };
     auto prefetch = [&](uint64_t need) {  // lanes in `need` allocate and load their next record
       const int nn = __builtin_popcountll(need);
       uint32_t base0 = 0;
@@ -989,56 +1072,89 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
         fok = k < n;
         if (fok) {
           const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
-          fa = pa[i];
-          fb = pb[i];
+          ca = pa[i];
+          cb = pb[i];
         }
       }
     };
-    prefetch(~0ull);
-    // walk state
-    uint32_t left = 0, inc_last = 1;
-    int32_t E01 = 0, E02 = 0, E12 = 0, K0 = 0, K1 = 0, K2 = 0;
-    int cur = 0, dX = 0, dY = 0, dZ = 0;
+    auto adopt = [&](uint64_t take, int src) {  // BATCH: lanes in `take` adopt lane `src` of c
+      const int ad = src << 2;
+      uint4 ra;
+      uint2 rb;
+      ra.x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)ca.x);
+      ra.y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)ca.y);
+      ra.z = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)ca.z);
+      ra.w = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)ca.w);
+      rb.x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)cb.x);
+      rb.y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)cb.y);
+      if ((take >> l) & 1ull) decode(ra, rb);
+    };
+    if constexpr (BATCH) {
+      c_n = load_batch(ca, cb);
+      x_n = c_n == 64 ? load_batch(xa, xb) : 0;
+    } else {
+      prefetch(~0ull);
+    }
     for (;;) {
       uint64_t act = __builtin_amdgcn_ballot_w64(left > 0);
-      if (__builtin_popcountll(act) <= 64 - REFILL) {
-        const uint64_t take = __builtin_amdgcn_ballot_w64(left == 0 && fok);
-        if (take) {
-          if (left == 0 && fok) {
-            E01 = (int32_t)fa.x;
-            E02 = (int32_t)fa.y;
-            E12 = (int32_t)fa.z;
-            const uint32_t w = fa.w;
-            const uint32_t a0 = fb.x & 0x3ffffu, a1 = fb.y & 0x3ffffu, a2 = (fb.x >> 18) | ((fb.y >> 18) << 14);
-            K0 = (int32_t)(a0 << 9);
-            K1 = (int32_t)(a1 << 9);
-            K2 = (int32_t)(a2 << 9);
-            cur = (int)(w & 0x7fffu) << 2;
-            left = (w >> 15) & 127u;
-            inc_last = (w >> 22) & 1u ? 0x10000u : 1u;
-            dX = (w >> 23) & 1u ? -(4 << (2 * bk::kLog)) : (4 << (2 * bk::kLog));
-            dY = (w >> 24) & 1u ? -(4 << bk::kLog) : (4 << bk::kLog);
-            dZ = (w >> 25) & 1u ? -4 : 4;
-            fok = false;
+      if constexpr (BATCH) {
+        if (__builtin_popcountll(act) <= 64 - REFILL && c_pos < c_n) {
+          const uint64_t idle = ~act;
+          const int need = 64 - __builtin_popcountll(act);
+          const int k = lane_prefix(idle);  // rank of this lane among the idle ones
+          const int avail = c_n - c_pos;
+          adopt(idle & __builtin_amdgcn_ballot_w64(k < avail), min(c_pos + k, 63));
+          if (need < avail) {
+            c_pos += need;
+          } else {  // batch c exhausted: x becomes c, the next batch is loaded into x
+            ca = xa;
+            cb = xb;
+            c_n = x_n;
+            c_pos = 0;
+            x_n = c_n == 64 ? load_batch(xa, xb) : 0;
+            const int rest = need - avail;
+            if (rest > 0 && c_n > 0) {
+              const int k2 = k - avail;
+              adopt(idle & __builtin_amdgcn_ballot_w64(k2 >= 0 && k2 < c_n), min(max(k2, 0), 63));
+              c_pos = min(rest, c_n);
+            }
           }
-          if (more) prefetch(take);
           act = __builtin_amdgcn_ballot_w64(left > 0);
         }
+        if (!act) {
+          if (c_pos >= c_n) break;
+          continue;
+        }
+      } else {
+        if (__builtin_popcountll(act) <= 64 - REFILL) {
+          const uint64_t take = __builtin_amdgcn_ballot_w64(left == 0 && fok);
+          if (take) {
+            if (left == 0 && fok) {
+              decode(ca, cb);
+              fok = false;
+            }
+            if (more) prefetch(take);
+            act = __builtin_amdgcn_ballot_w64(left > 0);
+          }
+        }
+        if (!act) {
+          if (!__builtin_amdgcn_ballot_w64(fok)) break;
+          continue;
+        }
       }
-      if (!act) {
-        if (!__builtin_amdgcn_ballot_w64(fok)) break;
-        continue;
-      }
-      if (left > 0) {
-        atomicAdd((uint32_t*)((char*)box + cur), left == 1 ? inc_last : 1u);
-        const bool b10 = E01 > 0;
-        const bool s2 = (b10 ? E12 : E02) > 0;
-        const bool s1 = !s2 && b10, s0 = !s2 && !b10;
-        E01 += s0 ? K1 : (s1 ? -K0 : 0);
-        E02 += s0 ? K2 : (s2 ? -K0 : 0);
-        E12 += s1 ? K2 : (s2 ? -K1 : 0);
-        cur += s2 ? dZ : (s1 ? dY : dX);
-        --left;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (left > 0) {
+          atomicAdd((uint32_t*)((char*)box + cur), 1u);
+          const bool b10 = E01 > 0;
+          const bool s2 = (b10 ? E12 : E02) > 0;
+          const bool s1 = !s2 && b10, s0 = !s2 && !b10;
+          E01 += s0 ? K1 : (s1 ? nK0 : 0);
+          E02 += s0 ? K2 : (s2 ? nK0 : 0);
+          E12 += s1 ? K2 : (s2 ? nK1 : 0);
+          cur += s2 ? dZ : (s1 ? dY : dX);
+          --left;
+        }
       }
     }
     __syncthreads();
@@ -1050,7 +1166,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       const int tx = tile >> (2 * bk::kLog - 3), ty = (tile >> (bk::kLog - 2)) & ((bk::kB >> 1) - 1),
                 tz = tile & ((bk::kB >> 2) - 1);
       const int lx = tx * 2 + (w16 >> 3), ly = ty * 2 + ((w16 >> 2) & 1), lz = tz * 4 + (w16 & 3);
-      const int li = (lx << (2 * bk::kLog)) + (ly << bk::kLog) + lz;
+      const int li = lx * kBkSx + ly * kBkSy + lz;
       const uint32_t v = box[li];
       if (v) {
         box[li] = 0;
@@ -1172,12 +1288,12 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   const int64_t ray_cap = (int64_t)UINT32_MAX / max_pairs_ray;
   const int64_t PB = std::min<int64_t>(P, ray_cap / (ppose * 64));
   if (PB < 1) return fail(DMF_ERR_RANGE, "image too large for one brick fusion batch");
-  const int span = std::max(128, (bg.nbricks + 31) / 32);  // packets per workgroup of passes A/B
+  const int span = std::max(64, (bg.nbricks + 63) / 64);  // packets per workgroup of passes A/B
   const size_t hist_bytes = sizeof(uint32_t) * (size_t)bg.nbricks;
   static std::atomic<bool> attr_set{false};
   if (!attr_set.load()) {
-    for (const void* f : {(const void*)k_bk_fuse<16, 8>, (const void*)k_bk_fuse<16, 1>, (const void*)k_bk_fuse<32, 8>,
-                          (const void*)k_bk_fuse<8, 8>})
+    for (const void* f : {(const void*)k_bk_fuse<16, 8, false>, (const void*)k_bk_fuse<16, 8, true>,
+                          (const void*)k_bk_fuse<32, 8, false>, (const void*)k_bk_fuse<8, 8, false>})
       DMF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kBkFuseLds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(sizeof(uint32_t) * 32768)));
@@ -1201,7 +1317,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     const unsigned nwg = (unsigned)((npk + span - 1) / span);
     DMF_HIP(hipMemsetAsync(cnt, 0, hist_bytes, v->stream));
     DMF_HIP(hipMemsetAsync(ctlp, 0, sizeof(unsigned long long) * 4, v->stream));
-    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(kBkThreads), hist_bytes, v->stream, g, cp,
+    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(kBkPassThreads), hist_bytes, v->stream, g, cp,
                        d_depth + (size_t)p0 * cp.H * cp.W, tab + p0, prm->dmin_mm, prm->dmax_mm, pkx, (int)ppose, npk,
                        span, bg, (ulonglong2*)rays, cnt, st);
     DMF_LAUNCH_CHECK();
@@ -1216,19 +1332,19 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     void *pra, *prb;
     DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * (size_t)hc[0], &pra));
     DMF_TRY(scratch(v, kScBkPairsB, sizeof(uint2) * (size_t)hc[0], &prb));
-    hipLaunchKernelGGL(k_bk_pairs, dim3(nwg), dim3(kBkThreads), hist_bytes, v->stream, npk, span, bg,
+    hipLaunchKernelGGL(k_bk_pairs, dim3(nwg), dim3(kBkPassThreads), hist_bytes, v->stream, npk, span, bg,
                        (const ulonglong2*)rays, cursor, (uint4*)pra, (uint2*)prb);
     DMF_LAUNCH_CHECK();
     const unsigned nf = (unsigned)std::min<unsigned long long>((unsigned long long)ncu, hc[1]);
-#define DMF_BK_FUSE(R, S)                                                                                        \
-  hipLaunchKernelGGL((k_bk_fuse<R, S>), dim3(nf), dim3(kBkThreads), kBkFuseLds, v->stream, g, bg, (const uint4*)pra, \
+#define DMF_BK_FUSE(R, S, B)                                                                                     \
+  hipLaunchKernelGGL((k_bk_fuse<R, S, B>), dim3(nf), dim3(kBkThreads), kBkFuseLds, v->stream, g, bg, (const uint4*)pra, \
                      (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt, (const uint32_t*)part_pref, ctlp,  \
                      d_hits, d_misses, st)
     switch (fuse_variant()) {
-      case 41: DMF_BK_FUSE(16, 1); break;
-      case 42: DMF_BK_FUSE(32, 8); break;
-      case 43: DMF_BK_FUSE(8, 8); break;
-      default: DMF_BK_FUSE(16, 8); break;
+      case 41: DMF_BK_FUSE(16, 8, true); break;
+      case 42: DMF_BK_FUSE(32, 8, false); break;
+      case 43: DMF_BK_FUSE(8, 8, false); break;
+      default: DMF_BK_FUSE(16, 8, false); break;
     }
 #undef DMF_BK_FUSE
     DMF_LAUNCH_CHECK();
@@ -1262,10 +1378,10 @@ const char* dmf_fuse_kernel(void) {
     case 31: return "dmf::k_fuse_l<12, 1280>";
     case 32: return "dmf::k_fuse_l<14, 1536>";
     case 33: return "dmf::k_fuse_l<12, 1536>";
-    case 40: return "dmf::k_bk_fuse<16, 8>";
-    case 41: return "dmf::k_bk_fuse<16, 1>";
-    case 42: return "dmf::k_bk_fuse<32, 8>";
-    case 43: return "dmf::k_bk_fuse<8, 8>";
+    case 40: return "dmf::k_bk_fuse<16, 8, false>";
+    case 41: return "dmf::k_bk_fuse<16, 8, true>";
+    case 42: return "dmf::k_bk_fuse<32, 8, false>";
+    case 43: return "dmf::k_bk_fuse<8, 8, false>";
     default: return "dmf::k_fuse_l<12, 1280>";
   }
 }
