@@ -719,14 +719,20 @@ struct BkGeom {
 };
 
 constexpr int kBkThreads = 1024;
-constexpr int kBkPassThreads = 256;  // passes A/B: 4 waves per workgroup, several workgroups per CU
+constexpr int kBkPassThreads = 256;
+constexpr int kBkUnroll = 4;  // phase F steps between refill checks  // passes A/B: 4 waves per workgroup, several workgroups per CU
 constexpr uint32_t kBkPartMax = 65535;  // pairs per part: 16-bit miss / hit fields never carry
 // LDS box of phase F: cell (x, y, z) of the brick at word x*kSx + y*kSy + z.  The skew
 // (kSy = 33, kSx = 32*33 + 1) puts the cell in bank (x + y + z) mod 32 instead of z alone,
 // so lanes on different rows/columns of one z-plane do not collide.
 constexpr int kBkSy = bk::kB + 1, kBkSx = bk::kB * kBkSy + 1;
 constexpr int kBkBoxWords = bk::kB * kBkSx;               // 33824 words
-constexpr int kBkFuseLds = kBkBoxWords * 4 + 16;         // 135,312 B of the CU's 160 KiB
+// (k_bk_fuse declares the box statically: 135,312 B of the CU's 160 KiB)
+
+// LDS byte offset of brick-local cell (x, y, z) in phase F's skewed box (< 2^18)
+__host__ __device__ constexpr uint32_t bk_lds_off(uint32_t x, uint32_t y, uint32_t z) {
+  return (x * kBkSx + y * kBkSy + z) * 4u;
+}
 
 __device__ inline int bk_index(const BkGeom& bg, int x, int y, int z) { return (x * bg.nb[1] + y) * bg.nb[2] + z; }
 
@@ -787,6 +793,7 @@ __global__ __launch_bounds__(kBkPassThreads) void k_bk_rays(Geom g, CamP cam, co
                                                         int packets_x, int packets_pose, int64_t npackets, int span,
                                                         BkGeom bg, ulonglong2* __restrict__ rays,
                                                         uint32_t* __restrict__ brick_count,
+                                                        uint32_t* __restrict__ wg_base,
                                                         unsigned long long* __restrict__ stats) {
   extern __shared__ uint32_t hist[];
   stats = stat_slot(stats);
@@ -821,7 +828,7 @@ __global__ __launch_bounds__(kBkPassThreads) void k_bk_rays(Geom g, CamP cam, co
   __syncthreads();
   for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) {
     const uint32_t n = hist[i];
-    if (n) atomicAdd(&brick_count[i], n);
+    if (n) wg_base[(size_t)blockIdx.x * bg.nbricks + i] = atomicAdd(&brick_count[i], n);
   }
   if (stats) wave_stats(stats, upd, nvalid, nhit);
 }
@@ -830,7 +837,7 @@ __global__ __launch_bounds__(kBkPassThreads) void k_bk_rays(Geom g, CamP cam, co
 // table part_pref[b] = parts of bricks < b (a brick of n pairs has ceil(n / 65535)
 // parts).  ctl[0] = pairs, ctl[1] = parts.
 __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* __restrict__ cnt,
-                                                  uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
+                                                  uint32_t* __restrict__ off,
                                                   uint32_t* __restrict__ part_pref,
                                                   unsigned long long* __restrict__ ctl) {
   __shared__ unsigned long long s_pairs[1024];
@@ -859,7 +866,6 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
   uint32_t pbase = t ? s_parts[t - 1] : 0u;
   for (int i = i0; i < i1; ++i) {
     off[i] = (uint32_t)base;
-    cursor[i] = (uint32_t)base;
     part_pref[i] = pbase;
     base += cnt[i];
     pbase += (cnt[i] + kBkPartMax - 1) / kBkPartMax;
@@ -883,26 +889,17 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
 // including the end cell).
 __global__ __launch_bounds__(kBkPassThreads) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
-                                                         uint32_t* __restrict__ cursor, uint4* __restrict__ pa,
+                                                         const uint32_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ wg_base, uint4* __restrict__ pa,
                                                          uint2* __restrict__ pb) {
   extern __shared__ uint32_t hist[];
-  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = 0;
+  // this workgroup's range in brick i starts at off[i] + wg_base[wg][i] (pass A); entries
+  // of bricks pass A did not count for this workgroup are never used
+  const uint32_t* wb = wg_base + (size_t)blockIdx.x * bg.nbricks;
+  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = off[i] + wb[i];
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int64_t pk0 = (int64_t)blockIdx.x * span, pk1 = min(npackets, pk0 + span);
-  for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
-    const ulonglong2 rec = rays[pk * 64 + l];
-    if (!(rec.y >> 63)) continue;
-    bk::QRay R;
-    bk::decode_ray(rec.x, rec.y, R);
-    bk_coarse(bg, R, [&](int b, int) { hist_add_agg(hist, b); });
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) {
-    const uint32_t n = hist[i];
-    if (n) hist[i] = atomicAdd(&cursor[i], n);
-  }
-  __syncthreads();
   constexpr uint32_t m5 = bk::kB - 1;
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
     const ulonglong2 rec = rays[pk * 64 + l];
@@ -913,9 +910,9 @@ __global__ __launch_bounds__(kBkPassThreads) void k_bk_pairs(int64_t npackets, i
                    K2 = (uint32_t)(2 * bk::kQ) * (uint32_t)R.adq[2];
     const uint32_t e01 = (uint32_t)bk::e0_pair(R, 0, 1), e02 = (uint32_t)bk::e0_pair(R, 0, 2),
                    e12 = (uint32_t)bk::e0_pair(R, 1, 2);
-    const uint32_t signs = (R.st[0] < 0 ? 1u << 23 : 0u) | (R.st[1] < 0 ? 1u << 24 : 0u) | (R.st[2] < 0 ? 1u << 25 : 0u);
+    const uint32_t signs = (R.st[0] < 0 ? 1u << 22 : 0u) | (R.st[1] < 0 ? 1u << 23 : 0u) | (R.st[2] < 0 ? 1u << 24 : 0u);
     const uint2 wb0 = make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
-                                 (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18));
+                                 (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18) | signs);
     // entry state of the pair being built
     auto entry = [&](const int32_t c[3]) {
       uint4 e;
@@ -924,12 +921,18 @@ __global__ __launch_bounds__(kBkPassThreads) void k_bk_pairs(int64_t npackets, i
       e.z = e12 + (uint32_t)c[1] * K2 - (uint32_t)c[2] * K1;
       const uint32_t x = (uint32_t)(R.cs[0] + R.st[0] * c[0]) & m5, y = (uint32_t)(R.cs[1] + R.st[1] * c[1]) & m5,
                      z = (uint32_t)(R.cs[2] + R.st[2] * c[2]) & m5;
-      e.w = (x << (2 * bk::kLog)) | (y << bk::kLog) | z | signs;
+      e.w = bk_lds_off(x, y, z);
       return e;
     };
-    // the end cell (brick-local) rides in the spare bits: low 6 in pa.w[26:32), high 9 in pb.y[22:31)
-    const uint32_t endc = (((uint32_t)R.ce[0] & m5) << (2 * bk::kLog)) | (((uint32_t)R.ce[1] & m5) << bk::kLog) |
-                          ((uint32_t)R.ce[2] & m5);
+    // brick-local index of the cell before the crossing (axis a) that produced counts c
+    auto last_before = [&](const int32_t c[3], int a) {
+      const uint32_t x = (uint32_t)(R.cs[0] + R.st[0] * (c[0] - (a == 0))) & m5,
+                     y = (uint32_t)(R.cs[1] + R.st[1] * (c[1] - (a == 1))) & m5,
+                     z = (uint32_t)(R.cs[2] + R.st[2] * (c[2] - (a == 2))) & m5;
+      return bk_lds_off(x, y, z);
+    };
+    // the end cell (brick-local): the last cell of the ray's last pair
+    const uint32_t endc = bk_lds_off((uint32_t)R.ce[0] & m5, (uint32_t)R.ce[1] & m5, (uint32_t)R.ce[2] & m5);
     auto first_k = [&](int a) {
       const int32_t o = R.cs[a] & (bk::kB - 1);
       return R.st[a] > 0 ? bk::kB - 1 - o : o;
@@ -938,7 +941,6 @@ __global__ __launch_bounds__(kBkPassThreads) void k_bk_pairs(int64_t npackets, i
     const int32_t c00[3] = {0, 0, 0};
     uint4 cur = entry(c00);
     uint32_t slot = 0;
-    int32_t idx_prev = 0;
     bk_coarse(bg, R, [&](int b, int a) {
       if (a >= 0) {
         int32_t c[3];
@@ -946,18 +948,17 @@ __global__ __launch_bounds__(kBkPassThreads) void k_bk_pairs(int64_t npackets, i
         if (a == 0) { bk::counts_at(R, 0, kb0, c); kb0 += bk::kB; }
         else if (a == 1) { bk::counts_at(R, 1, kb1, c); kb1 += bk::kB; }
         else { bk::counts_at(R, 2, kb2, c); kb2 += bk::kB; }
-        const int32_t idx = c[0] + c[1] + c[2];
-        cur.w |= (uint32_t)(idx - idx_prev) << 15;
+        const uint32_t lc = last_before(c, a);
+        cur.w |= lc << 18;
         pa[slot] = cur;
-        pb[slot] = wb0;
+        pb[slot] = make_uint2(wb0.x, wb0.y | ((lc >> 14) << 25));
         cur = entry(c);
-        idx_prev = idx;
       }
       slot = hist_take_agg(hist, b);
     });
-    cur.w |= ((uint32_t)(R.nsteps + 1 - idx_prev) << 15) | (R.end_inside ? 1u << 22 : 0u) | ((endc & 63u) << 26);
+    cur.w |= endc << 18;
     pa[slot] = cur;
-    pb[slot] = make_uint2(wb0.x, wb0.y | ((endc >> 6) << 22));
+    pb[slot] = make_uint2(wb0.x, wb0.y | ((endc >> 14) << 25) | (R.end_inside ? 1u << 29 : 0u));
   }
 }
 
@@ -985,7 +986,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
                                                         unsigned long long* __restrict__ ctl,
                                                         int32_t* __restrict__ hits, int32_t* __restrict__ misses,
                                                         unsigned long long* __restrict__ stats) {
-  extern __shared__ uint32_t box[];  // kBkBoxWords counters (skewed), then 4 control words
+  __shared__ uint32_t box[kBkBoxWords + 4];  // counters (skewed), then 4 control words
   uint32_t* sh = box + kBkBoxWords;
   stats = stat_slot(stats);
   const int tid = threadIdx.x, l = tid & 63;
@@ -1018,9 +1019,8 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       ++nparts_done;
     }
     // walk state (K negated once per pair: the step is adds and selects only)
-    uint32_t left = 0;
     int32_t E01 = 0, E02 = 0, E12 = 0, K1 = 0, K2 = 0, nK0 = 0, nK1 = 0;
-    int cur = 0, dX = 0, dY = 0, dZ = 0;
+    int cur = 0, cend = 0, dX = 0, dY = 0, dZ = 0;  // LDS byte offsets; idle lane: cur == cend
     auto decode = [&](const uint4& ra, const uint2& rb) {
       E01 = (int32_t)ra.x;
       E02 = (int32_t)ra.y;
@@ -1031,16 +1031,13 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       K1 = (int32_t)(a1 << 9);
       K2 = (int32_t)(a2 << 9);
       nK1 = -K1;
-      cur = (int)(((w >> 10) & 31u) * kBkSx + ((w >> 5) & 31u) * kBkSy + (w & 31u)) << 2;
-      left = (w >> 15) & 127u;
-      dX = (w >> 23) & 1u ? -(4 * kBkSx) : 4 * kBkSx;
-      dY = (w >> 24) & 1u ? -(4 * kBkSy) : 4 * kBkSy;
-      dZ = (w >> 25) & 1u ? -4 : 4;
-      if ((w >> 22) & 1u) {  // the ray ends inside this brick: its end cell takes the hit
-        const uint32_t e = (w >> 26) | ((rb.y >> 22) << 6);
-        atomicAdd(&box[((e >> 10) & 31u) * kBkSx + ((e >> 5) & 31u) * kBkSy + (e & 31u)], 0x10000u);
-        --left;  // ... and the walk covers the cells before it
-      }
+      cur = (int)(w & 0x3ffffu);
+      cend = (int)((w >> 18) | (((rb.y >> 25) & 15u) << 14));
+      dX = (rb.y >> 22) & 1u ? -(4 * kBkSx) : 4 * kBkSx;
+      dY = (rb.y >> 23) & 1u ? -(4 * kBkSy) : 4 * kBkSy;
+      dZ = (rb.y >> 24) & 1u ? -4 : 4;
+      // the pair's last cell: a hit when the ray ends there inside the grid, else a miss
+      atomicAdd((uint32_t*)((char*)box + cend), (rb.y >> 29) & 1u ? 0x10000u : 1u);
     };
     // BATCH: two 64-record batches per wave; `c` is handed out to idle lanes (ds_bpermute
     // from the lane holding the record) while `x` is in flight.  Otherwise: one record
@@ -1096,7 +1093,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       prefetch(~0ull);
     }
     for (;;) {
-      uint64_t act = __builtin_amdgcn_ballot_w64(left > 0);
+      uint64_t act = __builtin_amdgcn_ballot_w64(cur != cend);
       if constexpr (BATCH) {
         if (__builtin_popcountll(act) <= 64 - REFILL && c_pos < c_n) {
           const uint64_t idle = ~act;
@@ -1119,7 +1116,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
               c_pos = min(rest, c_n);
             }
           }
-          act = __builtin_amdgcn_ballot_w64(left > 0);
+          act = __builtin_amdgcn_ballot_w64(cur != cend);
         }
         if (!act) {
           if (c_pos >= c_n) break;
@@ -1127,14 +1124,14 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
         }
       } else {
         if (__builtin_popcountll(act) <= 64 - REFILL) {
-          const uint64_t take = __builtin_amdgcn_ballot_w64(left == 0 && fok);
+          const uint64_t take = __builtin_amdgcn_ballot_w64(cur == cend && fok);
           if (take) {
-            if (left == 0 && fok) {
+            if (cur == cend && fok) {
               decode(ca, cb);
               fok = false;
             }
             if (more) prefetch(take);
-            act = __builtin_amdgcn_ballot_w64(left > 0);
+            act = __builtin_amdgcn_ballot_w64(cur != cend);
           }
         }
         if (!act) {
@@ -1143,8 +1140,8 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
         }
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (left > 0) {
+      for (int u = 0; u < kBkUnroll; ++u) {
+        if (cur != cend) {
           atomicAdd((uint32_t*)((char*)box + cur), 1u);
           const bool b10 = E01 > 0;
           const bool s2 = (b10 ? E12 : E02) > 0;
@@ -1153,7 +1150,6 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
           E02 += s0 ? K2 : (s2 ? nK0 : 0);
           E12 += s1 ? K2 : (s2 ? nK1 : 0);
           cur += s2 ? dZ : (s1 ? dY : dX);
-          --left;
         }
       }
     }
@@ -1292,23 +1288,22 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   const size_t hist_bytes = sizeof(uint32_t) * (size_t)bg.nbricks;
   static std::atomic<bool> attr_set{false};
   if (!attr_set.load()) {
-    for (const void* f : {(const void*)k_bk_fuse<16, 8, false>, (const void*)k_bk_fuse<16, 8, true>,
-                          (const void*)k_bk_fuse<32, 8, false>, (const void*)k_bk_fuse<8, 8, false>})
-      DMF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kBkFuseLds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(sizeof(uint32_t) * 32768)));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(sizeof(uint32_t) * 32768)));
     attr_set.store(true);
   }
-  void *rays, *bricks, *ctl;
+  void *rays, *bricks, *ctl, *wgb;
   DMF_TRY(scratch(v, kScBkRays, sizeof(ulonglong2) * (size_t)(PB * ppose * 64), &rays));
-  DMF_TRY(scratch(v, kScBkBricks, sizeof(uint32_t) * (4 * (size_t)bg.nbricks + 4), &bricks));
+  DMF_TRY(scratch(v, kScBkBricks, sizeof(uint32_t) * (3 * (size_t)bg.nbricks + 4), &bricks));
   DMF_TRY(scratch(v, kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
+  // per-workgroup base inside each brick (pass A -> pass B)
+  const size_t nwg_max = (size_t)((PB * ppose + span - 1) / span);
+  DMF_TRY(scratch(v, kScBkWgBase, sizeof(uint32_t) * nwg_max * (size_t)bg.nbricks, &wgb));
   uint32_t* cnt = (uint32_t*)bricks;
   uint32_t* off = cnt + bg.nbricks;
-  uint32_t* cursor = off + bg.nbricks;
-  uint32_t* part_pref = cursor + bg.nbricks;  // nbricks + 1
+  uint32_t* part_pref = off + bg.nbricks;  // nbricks + 1
   unsigned long long* ctlp = (unsigned long long*)ctl;
   const int ncu = cu_count(v->device);
   for (int64_t p0 = 0; p0 < P; p0 += PB) {
@@ -1319,10 +1314,10 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     DMF_HIP(hipMemsetAsync(ctlp, 0, sizeof(unsigned long long) * 4, v->stream));
     hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(kBkPassThreads), hist_bytes, v->stream, g, cp,
                        d_depth + (size_t)p0 * cp.H * cp.W, tab + p0, prm->dmin_mm, prm->dmax_mm, pkx, (int)ppose, npk,
-                       span, bg, (ulonglong2*)rays, cnt, st);
+                       span, bg, (ulonglong2*)rays, cnt, (uint32_t*)wgb, st);
     DMF_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, v->stream, bg.nbricks, (const uint32_t*)cnt, off, cursor,
-                       part_pref, ctlp);
+    hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, v->stream, bg.nbricks, (const uint32_t*)cnt, off, part_pref,
+                       ctlp);
     DMF_LAUNCH_CHECK();
     unsigned long long hc[2];
     DMF_HIP(hipMemcpyAsync(hc, ctlp, sizeof(hc), hipMemcpyDeviceToHost, v->stream));
@@ -1333,11 +1328,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * (size_t)hc[0], &pra));
     DMF_TRY(scratch(v, kScBkPairsB, sizeof(uint2) * (size_t)hc[0], &prb));
     hipLaunchKernelGGL(k_bk_pairs, dim3(nwg), dim3(kBkPassThreads), hist_bytes, v->stream, npk, span, bg,
-                       (const ulonglong2*)rays, cursor, (uint4*)pra, (uint2*)prb);
+                       (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra, (uint2*)prb);
     DMF_LAUNCH_CHECK();
     const unsigned nf = (unsigned)std::min<unsigned long long>((unsigned long long)ncu, hc[1]);
 #define DMF_BK_FUSE(R, S, B)                                                                                     \
-  hipLaunchKernelGGL((k_bk_fuse<R, S, B>), dim3(nf), dim3(kBkThreads), kBkFuseLds, v->stream, g, bg, (const uint4*)pra, \
+  hipLaunchKernelGGL((k_bk_fuse<R, S, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg, (const uint4*)pra, \
                      (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt, (const uint32_t*)part_pref, ctlp,  \
                      d_hits, d_misses, st)
     switch (fuse_variant()) {

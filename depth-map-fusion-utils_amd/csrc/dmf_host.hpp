@@ -50,7 +50,7 @@ int scratch(dmf_volume* v, int k, size_t bytes, void** out);
 enum ScratchSlot {
   kScPoses = 0, kScHost0, kScHost1, kScHost2, kScOut0, kScOut1, kScOut2, kScOut3, kScTmp, kScSort0,
   kScSort1, kScSort2, kScSort3, kScCount, kScStats,
-  kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkChunks, kScBkCtl  // brick-owned fusion (dmf_fuse.hip)
+  kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkWgBase, kScBkCtl  // brick-owned fusion (dmf_fuse.hip)
 };
 
 // Striped statistics: kernels add into slot (block % kStatSlots) of a zeroed buffer
