@@ -5,7 +5,7 @@
 into a replicated 512^3 grid, N=8 -> 1024 poses).
 
 One step = clear the int32 hit/miss counters, fuse the rank's 128 depth frames
-(back-projection + exact integer 3D-DDA + atomics, libdmf.so k_fuse), RCCL
+(back-projection + exact integer 3D-DDA, libdmf.so brick pipeline k_bk_*), RCCL
 all-reduce(SUM) of the counters across ranks (N>1), finalize to the clamped int16
 log-odds grid (k_finalize).  Inputs are resident in HBM before timing starts.
 
@@ -191,7 +191,7 @@ def main():
     elapsed = D.max_over_ranks(elapsed, device=dev)
     updates, rays, hits = D.sum_over_ranks(st[:3], device=dev)
 
-    # per-launch algorithmic bytes of the dominant kernel (k_fuse), this rank
+    # per-launch algorithmic bytes of the fusion launch (all its kernels), this rank
     upd_launch = float(st[0]) / args.steps
     bytes_launch = BYTES_PER_UPDATE * upd_launch + BYTES_PER_DEPTH * P * HEIGHT * WIDTH
     achieved = bytes_launch / (fuse_ms * 1e-3) / 1e9
@@ -225,6 +225,19 @@ def main():
                       "sample": f"oracle fuse (OpenMP rows, atomic counters) of {nf} of the {P} frames, "
                                 f"{dt_mt:.1f}s on {nt} threads; Mrays/s {rps_mt / 1e6:.3f}"}
         ms = elapsed / args.steps * 1e3
+        kname = L.dmf_fuse_kernel().decode()
+        if kname.startswith("dmf::k_bk_fuse"):
+            # brick-owned pipeline: kernel_ms spans all four launches
+            pipeline = ["dmf::k_bk_rays", "dmf::k_bk_scan", "dmf::k_bk_pairs", kname]
+            diagnostics = {"pairs": int(st[4]) // args.steps, "parts": int(st[5]) // args.steps,
+                           "flushed_cells": int(st[6]) // args.steps,
+                           "updates_per_pair": float(st[0]) / max(float(st[4]), 1.0),
+                           "updates_per_flushed_cell": float(st[0]) / max(float(st[6]), 1.0)}
+        else:
+            pipeline = [kname]
+            diagnostics = {"lds_rounds": int(st[4]), "fallback_rounds": int(st[5]),
+                           "flushed_cell_atomics": int(st[6]),
+                           "updates_per_flushed_atomic": float(st[0]) / max(float(st[6]), 1.0)}
         result = {
             "metric": "ray-voxel updates/sec (3D-DDA log-odds fusion, 512^3 grid, 640x480 depth)",
             "value": updates / elapsed,
@@ -243,13 +256,11 @@ def main():
                        "grid": grid, "image": f"{WIDTH}x{HEIGHT}", "poses_per_gpu": P, "global_poses": P * world,
                        "parallelism": f"pose-sharded dp{world} + RCCL all-reduce(sum) of counters"},
             "mrays_per_s": rays / elapsed / 1e6,
-            "fuse_diagnostics": {"lds_rounds": int(st[4]), "fallback_rounds": int(st[5]),
-                                 "flushed_cell_atomics": int(st[6]),
-                                 "updates_per_flushed_atomic": float(st[0]) / max(float(st[6]), 1.0)},
+            "fuse_diagnostics": diagnostics,
             "updates_per_ray": updates / max(rays, 1.0),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": L.dmf_fuse_kernel().decode(), "kernel_ms": fuse_ms,
+                         "kernel": kname, "kernel_ms": fuse_ms, "pipeline": pipeline,
                          "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,

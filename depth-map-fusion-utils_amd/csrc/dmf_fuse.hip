@@ -1377,7 +1377,7 @@ const char* dmf_fuse_kernel(void) {
     case 41: return "dmf::k_bk_fuse<16, 8, true>";
     case 42: return "dmf::k_bk_fuse<32, 8, false>";
     case 43: return "dmf::k_bk_fuse<8, 8, false>";
-    default: return "dmf::k_fuse_l<12, 1280>";
+    default: return "dmf::k_bk_fuse<16, 8, false>";  // grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
 }
 
@@ -1421,7 +1421,9 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
   unsigned long long* st = nullptr;
   if (d_stats) DMF_TRY(stats_begin(v, &st));
   const int pkx = (cp.W + 7) / 8;
-  if (is_brick_variant(fuse_variant()) && brick_path_ok(g)) {
+  // default (variant 0): the brick-owned pipeline where it applies (<= 1024 cells per
+  // axis), the LDS-box kernel k_fuse_l<12, 1280> otherwise
+  if ((fuse_variant() == 0 || is_brick_variant(fuse_variant())) && brick_path_ok(g)) {
     DMF_TRY(fuse_bricks(v, cp, g, d_depth, tab, P, prm, d_hits, d_misses, st));
     if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
     DMF_LAUNCH_CHECK();

@@ -617,3 +617,23 @@ def test_fuse_brick_path(oracle, engine, dmf, brick_variant, dims, nframes):
         hg, mg, sg = engine.fuse_depth(gv, depth, poses, prm)
         assert np.array_equal(so, sg)
         assert np.array_equal(ho, hg) and np.array_equal(mo, mg)
+
+
+def test_fuse_lds_box_kernel(oracle, engine, dmf):
+    """k_fuse_l<12, 1280> (variant 31; the path for grids over 1024 cells per axis) stays
+    bit-exact now that the brick pipeline is the default."""
+    from dmf_amd import _lib
+    L = _lib.load()
+    _, depth, _ = Hh.frames()
+    poses = np.concatenate([Hh.ref_style_poses()[:2], Hh.frames()[0][:2]])
+    frames = np.concatenate([depth[:2], depth[2:4]])
+    ov = Hh.oracle_volume(oracle, n=96, clouds=[])
+    ho, mo, so = oracle.fuse_depth(ov, K, frames, poses)
+    gv = Hh.gpu_volume(n=96, clouds=[])
+    _lib.check(L.dmf_fuse_set_variant(31))
+    try:
+        assert L.dmf_fuse_kernel().decode() == "dmf::k_fuse_l<12, 1280>"
+        hg, mg, sg = engine.fuse_depth(gv, frames, poses)
+    finally:
+        _lib.check(L.dmf_fuse_set_variant(0))
+    assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)

@@ -32,18 +32,26 @@ with open(os.path.join(dst, "pmc_per_kernel.csv"), "w") as f:
     for (k, c), v in sorted(tot.items()):
         n = len(ndisp[(k, c)])
         f.write(f"{k},{c},{v:.0f},{n},{v / n:.1f}\n")
-fuse = [k for (k, c) in tot if k.startswith("dmf::k_fuse")]
 bench = json.load(open(os.path.join(src, "bench_kt.json")))
-if fuse:
-    k = fuse[0]
-    per = lambda c: tot.get((k, c), 0.0) / max(len(ndisp.get((k, c), ())), 1)
-    fetch, write = per("FETCH_SIZE") * 1024, per("WRITE_SIZE") * 1024
-    summ = {"kernel": k, "grid": bench["config"]["grid"], "poses": bench["config"]["poses_per_gpu"],
-            "hbm_bytes_per_launch": 2 * fetch + write, "fetch_bytes_raw": fetch, "write_bytes": write,
-            "tcc_ea0_atomic_requests_per_launch": per("TCC_EA0_ATOMIC_sum"),
+# the fusion launch = every kernel of the fusion pipeline (brick path: k_bk_rays, k_bk_scan,
+# k_bk_pairs, k_bk_fuse; LDS-box path: k_fuse_l alone), priced per bench step
+PIPE = ("dmf::k_bk_", "dmf::k_fuse")
+kernels = sorted({k for (k, c) in tot if k.startswith(PIPE)})
+if kernels:
+    def per(k, c):
+        return tot.get((k, c), 0.0) / max(len(ndisp.get((k, c), ())), 1)
+    per_kernel = {k: {"fetch_bytes_raw": per(k, "FETCH_SIZE") * 1024, "write_bytes": per(k, "WRITE_SIZE") * 1024,
+                      "hbm_bytes": (2 * per(k, "FETCH_SIZE") + per(k, "WRITE_SIZE")) * 1024} for k in kernels}
+    # k_bk_scan runs once per batch like the others: one launch of each per fusion call
+    hbm = sum(v["hbm_bytes"] for v in per_kernel.values())
+    summ = {"kernel": bench["roofline"]["kernel"], "pipeline": kernels, "grid": bench["config"]["grid"],
+            "poses": bench["config"]["poses_per_gpu"], "hbm_bytes_per_launch": hbm,
+            "per_kernel": per_kernel,
+            "tcc_ea0_atomic_requests_per_launch": sum(per(k, "TCC_EA0_ATOMIC_sum") for k in kernels),
             "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
             "kernel_ms_bench": bench["roofline"]["kernel_ms"],
-            "note": "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch; FETCH doubled per MI355X_MICROARCH.md"}
+            "note": "traffic = sum over the pipeline's kernels of (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch; "
+                    "FETCH doubled per MI355X_MICROARCH.md"}
     json.dump(summ, open(os.path.join(dst, "pmc_fuse_summary.json"), "w"), indent=1)
     json.dump(summ, open(os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_fuse_summary.json"), "w"), indent=1)
     print(json.dumps(summ, indent=1))
