@@ -86,6 +86,11 @@ def host_threads():
 
 
 def main():
+    # stdout carries exactly ONE JSON line (rank 0): anything else written to fd 1 by the
+    # native libraries (e.g. RCCL's init banner) is sent to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -102,7 +107,8 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local_rank)
-    if world > 1:
+    force_pipe = os.environ.get("DMF_BENCH_PIPELINE") == "1" and "RANK" in os.environ
+    if world > 1 or force_pipe:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     grid = args.grid
@@ -134,50 +140,108 @@ def main():
     logodds = torch.empty(ncell, dtype=torch.int16, device=dev)
     stats = torch.zeros(8, dtype=torch.int64, device=dev)
     pcam, pprm = C.addressof(cam), C.addressof(prm)
-    hits_p = counters.data_ptr()
-    miss_p = counters.data_ptr() + 4 * nct
 
+    # N > 1: the merge of step i (RCCL all-reduce on its own stream) overlaps the fusion of
+    # step i+1 on the compute stream; counters are double-buffered and step i is finalized
+    # behind fuse(i+1).  N = 1 has no collective and runs the plain sequence.
+    # (DMF_BENCH_PIPELINE=1 forces the pipelined schedule, e.g. under a world-1 RCCL group.)
+    pipelined = world > 1 or force_pipe
+    comm = torch.cuda.Stream(dev) if pipelined else None
+    bufs = [counters, torch.zeros_like(counters)] if pipelined else [counters]
+    pending = []  # (buffer, all-reduce-done event) of the step awaiting its finalize
     ev = []
 
-    def step(record=False):
-        # events on the engine's stream (torch's current stream): clear | fuse | all-reduce | finalize
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
-        if record:
-            e[0].record(stream)
-        counters.zero_()
-        if record:
-            e[1].record(stream)
-        _lib.check(L.dmf_fuse_depth_device(vol._h, pcam, d_depth.data_ptr(), d_poses.data_ptr(), P, pprm, hits_p,
-                                           miss_p, stats.data_ptr()))
-        if record:
-            e[2].record(stream)
-        D.merge_counters(counters)  # RCCL all-reduce(sum) of [hits | misses] when world > 1
-        if record:
-            e[3].record(stream)
-        _lib.check(L.dmf_fuse_finalize_device(vol._h, hits_p, miss_p, pprm, logodds.data_ptr()))
-        if record:
-            e[4].record(stream)
-            ev.append(e)
+    class Marks(dict):
+        """Timing events of one step; only recorded ones are read back."""
+        def mark(self, key, strm):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(strm)
+            self[key] = e
 
-    for _ in range(args.warmup):
-        step()
+    def fuse_into(c):
+        _lib.check(L.dmf_fuse_depth_device(vol._h, pcam, d_depth.data_ptr(), d_poses.data_ptr(), P, pprm,
+                                           c.data_ptr(), c.data_ptr() + 4 * nct, stats.data_ptr()))
+
+    def finalize(c):
+        _lib.check(L.dmf_fuse_finalize_device(vol._h, c.data_ptr(), c.data_ptr() + 4 * nct, pprm,
+                                              logodds.data_ptr()))
+
+    def finish_pending(rec=None):
+        if pending:
+            c, reduced = pending.pop()
+            stream.wait_event(reduced)
+            if rec is not None:
+                rec.mark("f0", stream)
+            finalize(c)
+            if rec is not None:
+                rec.mark("f1", stream)
+
+    def step(i, record=False):
+        # events: clear | fuse on the compute stream, all-reduce on its stream, finalize
+        r = Marks() if record else None
+        c = bufs[i % len(bufs)]
+        if record:
+            r.mark("c0", stream)
+        c.zero_()
+        if record:
+            r.mark("c1", stream)
+        fuse_into(c)
+        if record:
+            r.mark("c2", stream)
+        if not pipelined:
+            if record:
+                r.mark("a0", stream)
+            D.merge_counters(c)  # no collective at world 1
+            if record:
+                r.mark("a1", stream)
+                r.mark("f0", stream)
+            finalize(c)
+            if record:
+                r.mark("f1", stream)
+                ev.append(r)
+            return
+        fused = torch.cuda.Event()
+        fused.record(stream)
+        comm.wait_event(fused)
+        with torch.cuda.stream(comm):
+            if record:
+                r.mark("a0", comm)
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)  # RCCL all-reduce(sum) of [hits | misses]
+            if record:
+                r.mark("a1", comm)
+            reduced = torch.cuda.Event()
+            reduced.record(comm)
+        finish_pending(r)  # finalize step i-1 behind fuse(i)
+        pending.append((c, reduced))
+        if record:
+            ev.append(r)
+
+    for i in range(args.warmup):
+        step(i)
+    finish_pending()
     torch.cuda.synchronize(dev)
     stats.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(record=True)
+    for i in range(args.steps):
+        step(i, record=True)
+    finish_pending()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = stats.cpu().numpy()
-    seg = np.array([[e[i].elapsed_time(e[i + 1]) for i in range(4)] for e in ev])  # ms per segment
-    clear_ms, fuse_ms, allreduce_ms, finalize_ms = (float(x) for x in seg.mean(0))
+
+    def seg(a, b):
+        v = [r[a].elapsed_time(r[b]) for r in ev if a in r and b in r]
+        return float(np.mean(v)) if v else 0.0
+    clear_ms, fuse_ms, allreduce_ms = seg("c0", "c1"), seg("c1", "c2"), seg("a0", "a1")
+    finalize_ms = seg("f0", "f1")
     breakdown = {"clear": clear_ms, "fuse": fuse_ms, "allreduce": allreduce_ms, "finalize": finalize_ms,
-                 "compute_only": clear_ms + fuse_ms + finalize_ms}
+                 "compute_only": clear_ms + fuse_ms + finalize_ms,
+                 "schedule": "all-reduce of step i overlapped with fuse of step i+1" if pipelined else "sequential"}
     # grid-wide streaming passes, priced separately (SURVEY.md §8d): clear writes the
     # 2 tiled int32 counter arrays; finalize reads them and writes int16 log-odds
     clear_bytes, fin_bytes = 2 * 4 * nct, 10 * ncell
@@ -268,12 +332,12 @@ def main():
             "streaming": streaming,
             "secondary": secondary,
         }
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     vol.close()
     if result is not None:
-        print(json.dumps(result), flush=True)
+        os.write(json_fd, (json.dumps(result) + "\n").encode())
 
 
 def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16):
