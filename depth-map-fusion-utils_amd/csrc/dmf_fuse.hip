@@ -1282,7 +1282,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   const int64_t ppose = (int64_t)pkx * pky;
   const int64_t max_pairs_ray = 1 + (bg.nb[0] - 1) + (bg.nb[1] - 1) + (bg.nb[2] - 1);
   const int64_t ray_cap = (int64_t)UINT32_MAX / max_pairs_ray;
-  const int64_t PB = std::min<int64_t>(P, ray_cap / (ppose * 64));
+  int64_t PB = std::min<int64_t>(P, ray_cap / (ppose * 64));
+  if (const char* e = getenv("DMF_BK_BATCH_POSES")) {  // test hook: cap the poses per batch
+    const int64_t cap = (int64_t)atoll(e);
+    if (cap > 0) PB = std::min<int64_t>(PB, cap);
+  }
   if (PB < 1) return fail(DMF_ERR_RANGE, "image too large for one brick fusion batch");
   const int span = std::max(64, (bg.nbricks + 63) / 64);  // packets per workgroup of passes A/B
   const size_t hist_bytes = sizeof(uint32_t) * (size_t)bg.nbricks;

@@ -637,3 +637,68 @@ def test_fuse_lds_box_kernel(oracle, engine, dmf):
     finally:
         _lib.check(L.dmf_fuse_set_variant(0))
     assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
+
+
+def test_fuse_brick_vs_lds_box_full_size(dmf):
+    """Size-independent check at the bench's grid (512^3, 8 frames of 640x480): the brick
+    pipeline (default) and k_fuse_l<12, 1280> (variant 31) are independent exact
+    implementations of the same DDA spec and must agree counter for counter; every update
+    is either a hit or a miss, and there is one hit per ray ending inside the grid."""
+    import ctypes as C
+    from dmf_amd import _lib, scene
+    L = _lib.load()
+    P = 8
+    poses = np.ascontiguousarray(scene.fibonacci_poses(P, seed=1234), np.float32)
+    depth = np.ascontiguousarray(scene.render_frames(scene.intrinsics(640, 480), 640, 480, poses), np.uint16)
+    cam = _lib.make_camera(scene.intrinsics(640, 480), 480, 640)
+    prm = _lib.default_fuse_params(dmin_mm=scene.DEPTH_MIN_MM, dmax_mm=scene.DEPTH_MAX_MM)
+    vol = dmf.VoxelVolume()
+    vol.setDimensions(*Hh.BOUNDS)
+    vol.setVolumeSize(512, 512, 512)
+    vol.constructVolume()
+    h = vol._h
+    nct = C.c_int64()
+    _lib.check(L.dmf_fuse_counter_cells(h, C.addressof(nct)))
+    nt = nct.value
+
+    def dmalloc(nbytes):
+        p = C.c_void_p()
+        _lib.check(L.dmf_device_malloc(h, C.addressof(p), nbytes))
+        return p.value
+    dd, dp, dc, ds = dmalloc(depth.nbytes), dmalloc(poses.nbytes), dmalloc(8 * nt), dmalloc(64)
+    _lib.check(L.dmf_memcpy_h2d(h, dd, depth.ctypes.data, depth.nbytes))
+    _lib.check(L.dmf_memcpy_h2d(h, dp, poses.ctypes.data, poses.nbytes))
+    out = {}
+    try:
+        for variant in (0, 31):
+            _lib.check(L.dmf_fuse_set_variant(variant))
+            _lib.check(L.dmf_memset_device(h, dc, 0, 8 * nt))
+            _lib.check(L.dmf_memset_device(h, ds, 0, 64))
+            _lib.check(L.dmf_fuse_depth_device(h, C.addressof(cam), dd, dp, P, C.addressof(prm), dc, dc + 4 * nt, ds))
+            cnt = np.empty(2 * nt, np.int32)
+            st = np.empty(8, np.uint64)
+            _lib.check(L.dmf_memcpy_d2h(h, cnt.ctypes.data, dc, cnt.nbytes))
+            _lib.check(L.dmf_memcpy_d2h(h, st.ctypes.data, ds, st.nbytes))
+            out[variant] = (cnt, st)
+    finally:
+        _lib.check(L.dmf_fuse_set_variant(0))
+        for ptr_ in (dd, dp, dc, ds):
+            L.dmf_device_free(h, ptr_)
+    (c0, s0), (c1, s1) = out[0], out[31]
+    assert np.array_equal(s0[:4], s1[:4]) and s0[3] == 0 and s0[0] > 10 ** 8
+    assert np.array_equal(c0, c1)
+    assert int(c0.astype(np.int64).sum()) == int(s0[0])  # hits + misses == cell updates
+    assert int(c0[:nt].astype(np.int64).sum()) == int(s0[2])  # one hit per ray ending inside
+
+
+def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch):
+    """The brick pipeline split into several pose batches (DMF_BK_BATCH_POSES=2 over 5
+    frames: batches of 2, 2, 1) accumulates the same counters as the oracle."""
+    poses, depth, _ = Hh.frames()
+    poses, depth = poses[:5], depth[:5]
+    ov = Hh.oracle_volume(oracle, n=80, clouds=[])
+    ho, mo, so = oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
+    gv = Hh.gpu_volume(n=80, clouds=[])
+    monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
+    hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
+    assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
