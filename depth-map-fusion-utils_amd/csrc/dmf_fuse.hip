@@ -719,8 +719,8 @@ struct BkGeom {
 };
 
 constexpr int kBkThreads = 1024;
-constexpr int kBkPassThreads = 256;
-constexpr int kBkUnroll = 8;  // phase F steps between refill checks (4: +1-2 %, 3: +3 %)  // passes A/B: 4 waves per workgroup, several workgroups per CU
+constexpr int kBkPassThreads = 256;  // passes A/B: 4 waves per workgroup, several workgroups per CU
+constexpr int kBkUnroll = 8;         // phase F steps between refill checks (4: +1-2 %, 3: +3 %)
 constexpr uint32_t kBkPartMax = 65535;  // pairs per part: 16-bit miss / hit fields never carry
 // LDS box of phase F: cell (x, y, z) of the brick at word x*kSx + y*kSy + z.  The skew
 // (kSy = 33, kSx = 32*33 + 1) puts the cell in bank (x + y + z) mod 32 instead of z alone,
