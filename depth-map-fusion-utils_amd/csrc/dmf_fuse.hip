@@ -719,7 +719,9 @@ struct BkGeom {
 };
 
 constexpr int kBkThreads = 1024;
-constexpr int kBkPassThreads = 256;  // passes A/B: 4 waves per workgroup, several workgroups per CU
+// passes A/B: 256-lane workgroups (several per CU) while the LDS brick histogram is small;
+// 1024 lanes when it is large (over 8192 bricks: one workgroup per CU by LDS)
+constexpr int kBkPassThreads = 256, kBkPassThreadsBig = 1024, kBkBigHist = 8192;
 constexpr int kBkUnroll = 8;         // phase F steps between refill checks (4: +1-2 %, 3: +3 %)
 constexpr uint32_t kBkPartMax = 65535;  // pairs per part: 16-bit miss / hit fields never carry
 // LDS box of phase F: cell (x, y, z) of the brick at word x*kSx + y*kSy + z.  The skew
@@ -788,7 +790,7 @@ __device__ inline uint32_t hist_take_agg(uint32_t* hist, int b) {
 }
 
 // Pass A.  Workgroup = 4 waves over a span of 8x8 packets; ray index = packet * 64 + lane.
-__global__ __launch_bounds__(kBkPassThreads) void k_bk_rays(Geom g, CamP cam, const uint16_t* __restrict__ depth,
+__global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam, const uint16_t* __restrict__ depth,
                                                         const PoseX* __restrict__ poses, int dmin, int dmax,
                                                         int packets_x, int packets_pose, int64_t npackets, int span,
                                                         BkGeom bg, ulonglong2* __restrict__ rays,
@@ -887,7 +889,7 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
 // bk::counts_at; E = E(0) + c_a K_b - c_b K_a (exact mod 2^32, |E| < 2^29); the cell
 // count of a pair is the next entry index minus its own (the ray's last brick: up to and
 // including the end cell).
-__global__ __launch_bounds__(kBkPassThreads) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
+__global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
                                                          const uint32_t* __restrict__ wg_base, uint4* __restrict__ pa,
@@ -1263,6 +1265,16 @@ static bool brick_path_ok(const Geom& g) {
   return g.n[0] <= 1024 && g.n[1] <= 1024 && g.n[2] <= 1024 && bg.nbricks <= 32768;
 }
 
+// Default choice (variant 0): the brick pipeline pays a per-ray cost (passes A/B) that
+// the shorter rays of small grids do not amortise.  Measured on MI355X (640x480 frames):
+// 256^3 k_fuse_l 2.58 ms vs brick 2.86 ms (64 frames); 512^3 brick 9.4 vs 10.2 ms (128
+// frames); 1024^3 brick 13.0 vs 17.5 ms (32 frames).
+static bool brick_preferred(const Geom& g) {
+  return std::max(g.n[0], std::max(g.n[1], g.n[2])) >= 384;
+}
+
+static std::atomic<const char*> g_last_kernel{nullptr};
+
 static int cu_count(int device) {
   static std::atomic<int> cached{0};
   int n = cached.load();
@@ -1288,7 +1300,10 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     if (cap > 0) PB = std::min<int64_t>(PB, cap);
   }
   if (PB < 1) return fail(DMF_ERR_RANGE, "image too large for one brick fusion batch");
-  const int span = std::max(64, (bg.nbricks + 63) / 64);  // packets per workgroup of passes A/B
+  const int ab_threads = bg.nbricks > kBkBigHist ? kBkPassThreadsBig : kBkPassThreads;
+  // packets per workgroup of passes A/B (>= 16 per wave; the histogram's zero + flush
+  // amortised over >= 64 packets per 1k bricks)
+  const int span = std::max(16 * (ab_threads / 64), (bg.nbricks + 63) / 64);
   const size_t hist_bytes = sizeof(uint32_t) * (size_t)bg.nbricks;
   static std::atomic<bool> attr_set{false};
   if (!attr_set.load()) {
@@ -1316,7 +1331,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     const unsigned nwg = (unsigned)((npk + span - 1) / span);
     DMF_HIP(hipMemsetAsync(cnt, 0, hist_bytes, v->stream));
     DMF_HIP(hipMemsetAsync(ctlp, 0, sizeof(unsigned long long) * 4, v->stream));
-    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(kBkPassThreads), hist_bytes, v->stream, g, cp,
+    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(ab_threads), hist_bytes, v->stream, g, cp,
                        d_depth + (size_t)p0 * cp.H * cp.W, tab + p0, prm->dmin_mm, prm->dmax_mm, pkx, (int)ppose, npk,
                        span, bg, (ulonglong2*)rays, cnt, (uint32_t*)wgb, st);
     DMF_LAUNCH_CHECK();
@@ -1331,7 +1346,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     void *pra, *prb;
     DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * (size_t)hc[0], &pra));
     DMF_TRY(scratch(v, kScBkPairsB, sizeof(uint2) * (size_t)hc[0], &prb));
-    hipLaunchKernelGGL(k_bk_pairs, dim3(nwg), dim3(kBkPassThreads), hist_bytes, v->stream, npk, span, bg,
+    hipLaunchKernelGGL(k_bk_pairs, dim3(nwg), dim3(ab_threads), hist_bytes, v->stream, npk, span, bg,
                        (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra, (uint2*)prb);
     DMF_LAUNCH_CHECK();
     const unsigned nf = (unsigned)std::min<unsigned long long>((unsigned long long)ncu, hc[1]);
@@ -1369,8 +1384,8 @@ using namespace dmf;
 
 extern "C" {
 
-const char* dmf_fuse_kernel(void) {
-  switch (fuse_variant()) {
+static const char* variant_name(int v) {
+  switch (v) {
     case 1: return "dmf::k_fuse_direct";
     case 24: return "dmf::k_fuse_r<10, 1280, 1>";
     case 30: return "dmf::k_fuse_l<10, 1280>";
@@ -1385,9 +1400,15 @@ const char* dmf_fuse_kernel(void) {
   }
 }
 
+const char* dmf_fuse_kernel(void) {
+  const char* k = g_last_kernel.load();
+  return k ? k : variant_name(fuse_variant());
+}
+
 int dmf_fuse_set_variant(int32_t variant) {
   if (!is_known_variant(variant)) return fail(DMF_ERR_INVALID, "unknown fusion variant %d", variant);
   g_fuse_variant.store(variant, std::memory_order_relaxed);
+  g_last_kernel.store(nullptr);
   return DMF_OK;
 }
 
@@ -1427,7 +1448,9 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
   const int pkx = (cp.W + 7) / 8;
   // default (variant 0): the brick-owned pipeline where it applies (<= 1024 cells per
   // axis), the LDS-box kernel k_fuse_l<12, 1280> otherwise
-  if ((fuse_variant() == 0 || is_brick_variant(fuse_variant())) && brick_path_ok(g)) {
+  const int fv = fuse_variant();
+  if (brick_path_ok(g) && (is_brick_variant(fv) || (fv == 0 && brick_preferred(g)))) {
+    g_last_kernel.store(variant_name(fv));
     DMF_TRY(fuse_bricks(v, cp, g, d_depth, tab, P, prm, d_hits, d_misses, st));
     if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
     DMF_LAUNCH_CHECK();
@@ -1450,6 +1473,7 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
     case 33: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1536>), 1); break;
     default: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1280>), 1); break;
   }
+  g_last_kernel.store(is_brick_variant(fv) || fv == 0 ? "dmf::k_fuse_l<12, 1280>" : variant_name(fv));
 #undef DMF_FUSE_LAUNCH_R
   DMF_LAUNCH_CHECK();
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));

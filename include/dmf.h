@@ -91,14 +91,16 @@ void dmf_fuse_params_default(dmf_fuse_params* p);
  * dstar the smallest float whose host-libm acosf passes (the function the reference
  * binary calls).  Host-only; no GPU needed. */
 int dmf_angle_threshold(float* dstar);
-/* Diagnostic: name of the (dominant) fusion kernel dmf_fuse_depth* launches for grids of
- * <= 1024 cells per axis (DMF_FUSE_VARIANT / dmf_fuse_set_variant). */
+/* Diagnostic: name of the (dominant) fusion kernel the most recent dmf_fuse_depth* call
+ * of this process launched; before any call (or after dmf_fuse_set_variant), the kernel
+ * the selected variant uses on a 512^3 grid. */
 const char* dmf_fuse_kernel(void);
-/* Diagnostic / A-B: select the fusion implementation for this process.  0 = default =
- * 40 = brick-owned pipeline (k_bk_rays, k_bk_scan, k_bk_pairs, k_bk_fuse; DESIGN.md
- * §5.6); 41-43 = its refill variants; 1 = one device atomic per update; 24, 30-33 =
- * LDS-box kernels (k_fuse_r / k_fuse_l).  Grids over 1024 cells per axis always use
- * k_fuse_l<12, 1280>.  Results are identical for every variant.  The brick pipeline
+/* Diagnostic / A-B: select the fusion implementation for this process.  0 = default:
+ * the brick-owned pipeline (k_bk_rays, k_bk_scan, k_bk_pairs, k_bk_fuse)
+ * when the longest grid axis has 384..1024 cells, k_fuse_l<12, 1280> otherwise; 40 = the
+ * brick pipeline whenever it applies (<= 1024 cells per axis); 41-43 = its refill
+ * variants; 1 = one device atomic per update; 24, 30-33 = LDS-box kernels (k_fuse_r /
+ * k_fuse_l).  Grids over 1024 cells per axis always use k_fuse_l<12, 1280>.  Results are identical for every variant.  The brick pipeline
  * synchronises the volume's stream once per batch (it sizes the pair lists on the host). */
 int dmf_fuse_set_variant(int32_t variant);
 

@@ -692,13 +692,20 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
 
 
 def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch):
-    """The brick pipeline split into several pose batches (DMF_BK_BATCH_POSES=2 over 5
+    """The brick pipeline (variant 40) split into several pose batches (DMF_BK_BATCH_POSES=2 over 5
     frames: batches of 2, 2, 1) accumulates the same counters as the oracle."""
     poses, depth, _ = Hh.frames()
     poses, depth = poses[:5], depth[:5]
     ov = Hh.oracle_volume(oracle, n=80, clouds=[])
     ho, mo, so = oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
     gv = Hh.gpu_volume(n=80, clouds=[])
+    from dmf_amd import _lib
+    L = _lib.load()
     monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
-    hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
+    _lib.check(L.dmf_fuse_set_variant(40))  # the brick pipeline at this small grid
+    try:
+        hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
+        assert L.dmf_fuse_kernel().decode() == "dmf::k_bk_fuse<16, 8, false>"
+    finally:
+        _lib.check(L.dmf_fuse_set_variant(0))
     assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
