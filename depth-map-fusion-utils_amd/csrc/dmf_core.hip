@@ -56,6 +56,8 @@ int scratch(dmf_volume* v, int k, size_t bytes, void** out) {
 CamP cam_params(const dmf_camera* c) {
   CamP p;
   p.fx = c->K[0]; p.cx = c->K[2]; p.fy = c->K[4]; p.cy = c->K[5];
+  p.rfx = 1.0 / p.fx;
+  p.rfy = 1.0 / p.fy;
   p.H = c->height; p.W = c->width;
   return p;
 }

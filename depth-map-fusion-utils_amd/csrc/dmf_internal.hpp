@@ -39,8 +39,30 @@ struct Geom {
 // Camera.hpp:26 fx=K[0], cx=K[2], fy=K[4], cy=K[5] promoted to double.
 struct CamP {
   double fx, cx, fy, cy;
+  double rfx, rfy;  // RN(1/fx), RN(1/fy) (host division) for div_rn
   int H, W;
 };
+
+// Correctly rounded n / d from y = RN(1/d) (d > 0 normal): Markstein's final step
+// q0 = RN(n*y), r = n - d*q0 (exact by fma), q = RN(q0 + r*y).  Bit-identical to n / d in
+// the checked magnitude ranges (tools/fastdiv_selftest.cpp: 2.7e9 quotients over the
+// projection and reverse-march domains, 0 mismatches); outside them (and for NaN) it
+// divides; +-0 keeps its sign through q0.  Replaces the ~10-instruction IEEE division
+// sequence by one multiply and two fmas per sample.
+__device__ inline double div_rn(double n, double d, double y) {
+  const double q0 = n * y;
+  const double an = fabs(n);
+  if (!(an >= 0x1p-900 && an <= 0x1p900)) return n == 0.0 ? q0 : n / d;
+  const double r = fma(-d, q0, n);
+  return fma(r, y, q0);
+}
+__device__ inline float div_rn(float n, float d, float y) {
+  const float q0 = n * y;
+  const float an = fabsf(n);
+  if (!(an >= 0x1p-40f && an <= 0x1p40f)) return n == 0.0f ? q0 : n / d;
+  const float r = fmaf(-d, q0, n);
+  return fmaf(r, y, q0);
+}
 
 // Forward (camera->world) pose and its Eigen Affine inverse, row-major 3x4.
 struct PoseX {
@@ -78,8 +100,8 @@ __host__ __device__ inline void inverse_pose(const float* T, float* R) {
 // Camera.hpp:24-31 projectPoint: double math, narrowed to float.
 __device__ inline void project(const CamP& c, int r, int col, int depth_mm, float o[3]) {
   const double z = depth_mm * 0.001;
-  const double x = z * ((double)col - c.cx) / (c.fx);
-  const double y = z * ((double)r - c.cy) / (c.fy);
+  const double x = div_rn(z * ((double)col - c.cx), c.fx, c.rfx);  // (z * (col - cx)) / fx
+  const double y = div_rn(z * ((double)r - c.cy), c.fy, c.rfy);
   o[0] = (float)x;
   o[1] = (float)y;
   o[2] = (float)z;

@@ -35,9 +35,9 @@ __device__ inline void wave_add_u64(unsigned long long* dst, unsigned long long 
 // (Eigen evaluates the double depth as float; RayTracingEngine.hpp:82, :173).
 __device__ inline void march_sample(const float cen[3], const float v[3], int depth, float p[3]) {
   const float fd = (float)depth;
-  p[0] = cen[0] + ((v[0] * fd) / 1000.0f);
-  p[1] = cen[1] + ((v[1] * fd) / 1000.0f);
-  p[2] = cen[2] + ((v[2] * fd) / 1000.0f);
+  p[0] = cen[0] + div_rn(v[0] * fd, 1000.0f, 1.0f / 1000.0f);
+  p[1] = cen[1] + div_rn(v[1] * fd, 1000.0f, 1.0f / 1000.0f);
+  p[2] = cen[2] + div_rn(v[2] * fd, 1000.0f, 1.0f / 1000.0f);
 }
 
 // The reverse 1 mm march (RayTracingEngine.hpp:81-103 / :172-200).  Returns true if
@@ -903,9 +903,9 @@ __global__ void k_will_collide(Geom g, const uint32_t* __restrict__ occ, const f
   for (int depth = 1; !collided; depth++) {
     if ((double)depth > lim) break;
     const float fd = (float)depth;
-    const float px = a[0] + ((v[0] * fd) / 1000.0f);
-    const float py = a[1] + ((v[1] * fd) / 1000.0f);
-    const float pz = a[2] + ((v[2] * fd) / 1000.0f);
+    const float px = a[0] + div_rn(v[0] * fd, 1000.0f, 1.0f / 1000.0f);
+    const float py = a[1] + div_rn(v[1] * fd, 1000.0f, 1.0f / 1000.0f);
+    const float pz = a[2] + div_rn(v[2] * fd, 1000.0f, 1.0f / 1000.0f);
     if (!valid_points(g, px, py, pz)) continue;
     const int x = bin_axis(g, 0, px), y = bin_axis(g, 1, py), z = bin_axis(g, 2, pz);
     if (!valid_coords(g, x, y, z)) continue;
@@ -950,9 +950,9 @@ __global__ __launch_bounds__(64 * kCostWaves) void k_cost_map(Geom g, const uint
     bool hit = false;
     if ((double)depth <= lim) {
       const float fd = (float)depth;
-      const float px = a[0] + ((v[0] * fd) / 1000.0f);
-      const float py = a[1] + ((v[1] * fd) / 1000.0f);
-      const float pz = a[2] + ((v[2] * fd) / 1000.0f);
+      const float px = a[0] + div_rn(v[0] * fd, 1000.0f, 1.0f / 1000.0f);
+      const float py = a[1] + div_rn(v[1] * fd, 1000.0f, 1.0f / 1000.0f);
+      const float pz = a[2] + div_rn(v[2] * fd, 1000.0f, 1.0f / 1000.0f);
       if (valid_points(g, px, py, pz)) {
         const int x = bin_axis(g, 0, px), y = bin_axis(g, 1, py), z = bin_axis(g, 2, pz);
         hit = valid_coords(g, x, y, z) && occ_test(occ, lin_index(g, x, y, z));
