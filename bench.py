@@ -313,7 +313,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int64",
+            "dtype": "int32",  # exact integer DDA (int32 walk state) and int32 hit/miss counters
             "data": "synthetic: analytic sphere+box+ground scene rendered to uint16 mm depth, Fibonacci poses r=0.7m",
             "config": {"workload": f"config4-shard: {P} poses/GPU x {WIDTH}x{HEIGHT} depth -> {grid}^3 int16 "
                                    f"log-odds (int32 hit/miss counters)",
