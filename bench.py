@@ -260,7 +260,6 @@ def main():
     bytes_launch = BYTES_PER_UPDATE * upd_launch + BYTES_PER_DEPTH * P * HEIGHT * WIDTH
     achieved = bytes_launch / (fuse_ms * 1e-3) / 1e9
 
-    # sanity: occupancy from hits equals GPU-binned back-projection (reference binning)
     result = None
     if rank == 0:
         secondary = {}
