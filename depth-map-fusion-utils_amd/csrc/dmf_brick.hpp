@@ -93,22 +93,20 @@ __host__ __device__ inline bool ev_before(const QRay& r, int a, int64_t Ha, int 
   return L < R || (L == R && a < b);
 }
 
-// floor(X / Y) for 0 <= X < 2^41, 0 < Y < 2^29 with a small quotient (< 2^20):
-// float estimate (relative error < 2^-21) and one exact correction step.
+// floor(X / Y) for 0 <= X < 2^41, 0 < Y < 2^29 with a small quotient: count_at's quotient
+// counts b-crossings up to a crossing event of the same ray, so it is <= n_b + 1 <= 2^11.
+// Float estimate (relative error < 2^-21, so within 1 of the floor) and one exact
+// correction in either direction.
 __host__ __device__ inline int64_t small_quot(int64_t X, int64_t Y) {
   const float xf = (float)(int32_t)(X >> 20) * 1048576.0f + (float)(int32_t)(X & 0xfffff);
   const float yf = (float)(int32_t)Y;
 #if defined(__HIP_DEVICE_COMPILE__)
-  // v_rcp_f32 (1 ulp): the estimate stays within 1 of floor(X/Y); the steps below fix it
-  int64_t q = (int64_t)(xf * __builtin_amdgcn_rcpf(yf));
+  int32_t q = (int32_t)(xf * __builtin_amdgcn_rcpf(yf));  // v_rcp_f32: 1 ulp
 #else
-  int64_t q = (int64_t)(xf / yf);
+  int32_t q = (int32_t)(xf / yf);
 #endif
-  int64_t rm = X - q * Y;
-  if (rm < 0) { --q; rm += Y; }
-  if (rm < 0) { --q; rm += Y; }
-  if (rm >= Y) { ++q; rm -= Y; }
-  if (rm >= Y) { ++q; }
+  const int64_t rm = X - (int64_t)q * Y;
+  q += rm < 0 ? -1 : (rm >= Y ? 1 : 0);
   return q;
 }
 
