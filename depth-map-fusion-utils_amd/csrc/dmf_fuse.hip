@@ -738,11 +738,12 @@ __host__ __device__ constexpr uint32_t bk_lds_off(uint32_t x, uint32_t y, uint32
 
 __device__ inline int bk_index(const BkGeom& bg, int x, int y, int z) { return (x * bg.nb[1] + y) * bg.nb[2] + z; }
 
-// Coarse walk of one ray: calls f(brick index) for every brick it passes, in order.
+// Coarse walk of one ray: calls f(brick index, axis of the boundary crossed to enter it
+// (-1 for the first brick), brick coordinates) for every brick it passes, in order.
 template <class F>
 __device__ inline void bk_coarse(const BkGeom& bg, const bk::QRay& R, F&& f) {
   int b0 = R.cs[0] >> bk::kLog, b1 = R.cs[1] >> bk::kLog, b2 = R.cs[2] >> bk::kLog;
-  f(bk_index(bg, b0, b1, b2), -1);
+  f(bk_index(bg, b0, b1, b2), -1, b0, b1, b2);
   bk::Coarse cw;
   bk::coarse_init(R, cw);
   for (int t = 0; t < cw.total; ++t) {
@@ -750,7 +751,7 @@ __device__ inline void bk_coarse(const BkGeom& bg, const bk::QRay& R, F&& f) {
     b0 += a == 0 ? R.st[0] : 0;
     b1 += a == 1 ? R.st[1] : 0;
     b2 += a == 2 ? R.st[2] : 0;
-    f(bk_index(bg, b0, b1, b2), a);
+    f(bk_index(bg, b0, b1, b2), a, b0, b1, b2);
   }
 }
 
@@ -822,7 +823,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
       bk::decode_ray(A, B, R);
       upd += (unsigned long long)(R.nsteps + 1);
       nhit += inside ? 1 : 0;
-      bk_coarse(bg, R, [&](int b, int) { hist_add_agg(hist, b); });
+      bk_coarse(bg, R, [&](int b, int, int, int, int) { hist_add_agg(hist, b); });
     }
     nvalid += valid ? 1 : 0;
     rays[pk * 64 + l] = rec;
@@ -935,21 +936,23 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets
     };
     // the end cell (brick-local): the last cell of the ray's last pair
     const uint32_t endc = bk_lds_off((uint32_t)R.ce[0] & m5, (uint32_t)R.ce[1] & m5, (uint32_t)R.ce[2] & m5);
-    auto first_k = [&](int a) {
-      const int32_t o = R.cs[a] & (bk::kB - 1);
-      return R.st[a] > 0 ? bk::kB - 1 - o : o;
+    // fine-crossing index of the boundary crossed (axis a) to enter brick coordinate nb:
+    // moving up, cell nb*32 is reached by crossing nb*32 - cs - 1; moving down, cell
+    // nb*32 + 31 by crossing cs - nb*32 - 32.  (Derived from the brick coordinate, not
+    // carried per axis: per-axis counters indexed by a became a scratch array.)
+    auto boundary_k = [&](int ax, int nb) {
+      return R.st[ax] > 0 ? (nb << bk::kLog) - R.cs[ax] - 1 : R.cs[ax] - (nb << bk::kLog) - bk::kB;
     };
-    int32_t kb0 = first_k(0), kb1 = first_k(1), kb2 = first_k(2);
     const int32_t c00[3] = {0, 0, 0};
     uint4 cur = entry(c00);
     uint32_t slot = 0;
-    bk_coarse(bg, R, [&](int b, int a) {
+    bk_coarse(bg, R, [&](int b, int a, int bx, int by, int bz) {
       if (a >= 0) {
         int32_t c[3];
         // constant axis in each call: no dynamically indexed (scratch) arrays
-        if (a == 0) { bk::counts_at(R, 0, kb0, c); kb0 += bk::kB; }
-        else if (a == 1) { bk::counts_at(R, 1, kb1, c); kb1 += bk::kB; }
-        else { bk::counts_at(R, 2, kb2, c); kb2 += bk::kB; }
+        if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
+        else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
+        else bk::counts_at(R, 2, boundary_k(2, bz), c);
         const uint32_t lc = last_before(c, a);
         cur.w |= lc << 18;
         pa[slot] = cur;
