@@ -60,6 +60,19 @@ def make_inputs(rank, world, P_local, cache_dir="/tmp/dmf_bench_cache"):
     return poses, depth
 
 
+def workload_name(grid, P, world):
+    """Which BASELINE.json config the run reproduces (per-GPU shard for the 8-GPU ones)."""
+    if (WIDTH, HEIGHT, grid) == (640, 480, 256) and P * world == 64:
+        return "config2"
+    if (WIDTH, HEIGHT, grid) == (1280, 720, 512) and P * world == 256:
+        return "config3"
+    if (WIDTH, HEIGHT, grid) == (1280, 720, 1024):
+        return "config5-shard"
+    if (WIDTH, HEIGHT, grid) == (640, 480, 512):
+        return "config4-shard"
+    return "custom"
+
+
 def cpu_baseline(K, poses, depth, n_frames, grid, threads=1):
     """Oracle (CPU restatement; threads > 1 = its OpenMP row-parallel variant) on a
     bounded sample of the same workload."""
@@ -99,7 +112,11 @@ def main():
     ap.add_argument("--poses-per-gpu", type=int, default=POSES_PER_GPU)
     ap.add_argument("--cpu-frames", type=int, default=8, help="frames in the CPU-oracle baseline sample (0=skip)")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--image", default="640x480", choices=["640x480", "1280x720"],
+                    help="depth frame size (BASELINE configs 1/2/4: 640x480; 3/5: 1280x720)")
     args = ap.parse_args()
+    global WIDTH, HEIGHT
+    WIDTH, HEIGHT = (int(v) for v in args.image.split("x"))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -302,7 +319,7 @@ def main():
                            "flushed_cell_atomics": int(st[6]),
                            "updates_per_flushed_atomic": float(st[0]) / max(float(st[6]), 1.0)}
         result = {
-            "metric": "ray-voxel updates/sec (3D-DDA log-odds fusion, 512^3 grid, 640x480 depth)",
+            "metric": f"ray-voxel updates/sec (3D-DDA log-odds fusion, {grid}^3 grid, {WIDTH}x{HEIGHT} depth)",
             "value": updates / elapsed,
             "unit": "ray-voxel updates/s",
             "n_gpus": world,
@@ -314,7 +331,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",  # exact integer DDA (int32 walk state) and int32 hit/miss counters
             "data": "synthetic: analytic sphere+box+ground scene rendered to uint16 mm depth, Fibonacci poses r=0.7m",
-            "config": {"workload": f"config4-shard: {P} poses/GPU x {WIDTH}x{HEIGHT} depth -> {grid}^3 int16 "
+            "config": {"workload": f"{workload_name(grid, P, world)}: {P} poses/GPU x {WIDTH}x{HEIGHT} depth -> "
+                                   f"{grid}^3 int16 "
                                    f"log-odds (int32 hit/miss counters)",
                        "grid": grid, "image": f"{WIDTH}x{HEIGHT}", "poses_per_gpu": P, "global_poses": P * world,
                        "parallelism": f"pose-sharded dp{world} + RCCL all-reduce(sum) of counters"},
