@@ -155,7 +155,7 @@ def main():
     nct = nct.value  # tiled counter layout
     counters = torch.zeros(2 * nct, dtype=torch.int32, device=dev)  # [hits | misses]: one all-reduce
     logodds = torch.empty(ncell, dtype=torch.int16, device=dev)
-    stats = torch.zeros(8, dtype=torch.int64, device=dev)
+    stats = torch.zeros(16, dtype=torch.int64, device=dev)  # 8 used; diagnostic builds add 7..15
     pcam, pprm = C.addressof(cam), C.addressof(prm)
 
     # N > 1: the merge of step i (RCCL all-reduce on its own stream) overlaps the fusion of
@@ -313,6 +313,13 @@ def main():
                            "flushed_cells": int(st[6]) // args.steps,
                            "updates_per_pair": float(st[0]) / max(float(st[4]), 1.0),
                            "updates_per_flushed_cell": float(st[0]) / max(float(st[6]), 1.0)}
+            if st[7] > 0:  # diagnostic build (DMF_EXP_STATS): F wave blocks, lanes active, refills
+                diagnostics.update({"f_blocks": int(st[7]) // args.steps, "f_refills": int(st[9]) // args.steps,
+                                    "f_lane_util": float(st[8]) / max(64.0 * float(st[7]), 1.0),
+                                    "f_wave_cycles": {"refill": int(st[10]) // args.steps, "walk": int(st[11]) // args.steps,
+                                                      "flush": int(st[12]) // args.steps,
+                                                      "lifetime_sum": int(st[14]) // args.steps,
+                                                      "lifetime_max_wave": int(st[13])}})
         else:
             pipeline = [kname]
             diagnostics = {"lds_rounds": int(st[4]), "fallback_rounds": int(st[5]),

@@ -44,9 +44,16 @@ int scratch(dmf_volume* v, int k, size_t bytes, void** out) {
   if ((int)v->scratch.size() <= k) v->scratch.resize(k + 1, {nullptr, 0});
   auto& s = v->scratch[k];
   if (s.second < bytes) {
-    if (s.first) DMF_HIP(hipFree(s.first));
-    size_t nb = std::max<size_t>(bytes + bytes / 4, 256);
-    DMF_HIP(hipMalloc(&s.first, nb));
+    // forget the old slot before allocating: a failed hipMalloc must leave the slot
+    // empty (size 0), never a stale size with a freed or null pointer
+    void* old = s.first;
+    s.first = nullptr;
+    s.second = 0;
+    if (old) DMF_HIP(hipFree(old));
+    const size_t nb = std::max<size_t>(bytes + bytes / 4, 256);
+    void* p = nullptr;
+    DMF_HIP(hipMalloc(&p, nb));
+    s.first = p;
     s.second = nb;
   }
   *out = s.first;

@@ -722,7 +722,6 @@ constexpr int kBkThreads = 1024;
 // passes A/B: 256-lane workgroups (several per CU) while the LDS brick histogram is small;
 // 1024 lanes when it is large (over 8192 bricks: one workgroup per CU by LDS)
 constexpr int kBkPassThreads = 256, kBkPassThreadsBig = 1024, kBkBigHist = 8192;
-constexpr int kBkUnroll = 8;         // phase F steps between refill checks (4: +1-2 %, 3: +3 %)
 constexpr uint32_t kBkPartMax = 65535;  // pairs per part: 16-bit miss / hit fields never carry
 // LDS box of phase F: cell (x, y, z) of the brick at word x*kSx + y*kSy + z.  The skew
 // (kSy = 33, kSx = 32*33 + 1) puts the cell in bank (x + y + z) mod 32 instead of z alone,
@@ -735,6 +734,9 @@ constexpr int kBkBoxWords = bk::kB * kBkSx;               // 33824 words
 __host__ __device__ constexpr uint32_t bk_lds_off(uint32_t x, uint32_t y, uint32_t z) {
   return (x * kBkSx + y * kBkSy + z) * 4u;
 }
+
+// word index of the same cell (< 33824: 16 bits in the pair record)
+__host__ __device__ constexpr uint32_t bk_lds_word(uint32_t x, uint32_t y, uint32_t z) { return x * kBkSx + y * kBkSy + z; }
 
 __device__ inline int bk_index(const BkGeom& bg, int x, int y, int z) { return (x * bg.nb[1] + y) * bg.nb[2] + z; }
 
@@ -883,13 +885,22 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
 // Pass B.  Same spans as pass A; the workgroup counts its pairs per brick, reserves one
 // contiguous range per brick, then writes one self-contained 24-B record per pair (the
 // fine walk's state at the brick entry, so phase F makes ONE coalesced load per pair
-// and never touches the ray records):
-//   pa = {E01, E02, E12 at entry, cell | cells << 15 | ends << 22 | neg_x << 23 | ...}
-//   pb = {adq0 | adq2[0:14) << 18, adq1 | adq2[14:18) << 18}
+// and never touches the ray records).  Record (s = steps inside the brick = cells - 1,
+// 0..93; word offsets into phase F's skewed box, < 33824):
+//   pa = {E01 | s[0:2) << 30, E02 | s[2:4) << 30, E12 | s[4:6) << 30, entry word | last word << 16}
+//   pb = {adq0 | adq2[0:14) << 18, adq1 | adq2[14:18) << 18 | neg x,y,z << 22 | s[6] << 25 | ends << 26}
+// with each E as a 30-bit two's-complement field: |E| < 2^28 for a moving pair of a grid
+// <= 1024 cells/axis, and a pair with a non-moving axis keeps a constant E of which only
+// the sign is used (stored as +-(2^29 - 1)).
 // Entry crossing counts at a brick boundary event (axis a, fine crossing k) come from
-// bk::counts_at; E = E(0) + c_a K_b - c_b K_a (exact mod 2^32, |E| < 2^29); the cell
-// count of a pair is the next entry index minus its own (the ray's last brick: up to and
+// bk::counts_at; E = E(0) + c_a K_b - c_b K_a (exact mod 2^32); a pair's steps are the
+// next entry's crossing index minus its own, minus one (the ray's last brick: up to and
 // including the end cell).
+__device__ inline uint32_t bk_e30(int32_t e) {
+  const int32_t lim = (1 << 29) - 1;
+  return (uint32_t)(e > lim ? lim : (e < -lim ? -lim : e)) & 0x3fffffffu;
+}
+
 __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
@@ -916,26 +927,34 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets
     const uint32_t signs = (R.st[0] < 0 ? 1u << 22 : 0u) | (R.st[1] < 0 ? 1u << 23 : 0u) | (R.st[2] < 0 ? 1u << 24 : 0u);
     const uint2 wb0 = make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
                                  (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18) | signs);
-    // entry state of the pair being built
+    // entry state of the pair being built (E fields without the step bits)
     auto entry = [&](const int32_t c[3]) {
       uint4 e;
-      e.x = e01 + (uint32_t)c[0] * K1 - (uint32_t)c[1] * K0;
-      e.y = e02 + (uint32_t)c[0] * K2 - (uint32_t)c[2] * K0;
-      e.z = e12 + (uint32_t)c[1] * K2 - (uint32_t)c[2] * K1;
+      e.x = bk_e30((int32_t)(e01 + (uint32_t)c[0] * K1 - (uint32_t)c[1] * K0));
+      e.y = bk_e30((int32_t)(e02 + (uint32_t)c[0] * K2 - (uint32_t)c[2] * K0));
+      e.z = bk_e30((int32_t)(e12 + (uint32_t)c[1] * K2 - (uint32_t)c[2] * K1));
       const uint32_t x = (uint32_t)(R.cs[0] + R.st[0] * c[0]) & m5, y = (uint32_t)(R.cs[1] + R.st[1] * c[1]) & m5,
                      z = (uint32_t)(R.cs[2] + R.st[2] * c[2]) & m5;
-      e.w = bk_lds_off(x, y, z);
+      e.w = bk_lds_word(x, y, z);
       return e;
     };
-    // brick-local index of the cell before the crossing (axis a) that produced counts c
+    // brick-local word of the cell before the crossing (axis a) that produced counts c
     auto last_before = [&](const int32_t c[3], int a) {
       const uint32_t x = (uint32_t)(R.cs[0] + R.st[0] * (c[0] - (a == 0))) & m5,
                      y = (uint32_t)(R.cs[1] + R.st[1] * (c[1] - (a == 1))) & m5,
                      z = (uint32_t)(R.cs[2] + R.st[2] * (c[2] - (a == 2))) & m5;
-      return bk_lds_off(x, y, z);
+      return bk_lds_word(x, y, z);
+    };
+    auto put = [&](uint32_t slot, uint4 e, uint32_t last, uint32_t steps, bool ends) {
+      e.x |= (steps & 3u) << 30;
+      e.y |= ((steps >> 2) & 3u) << 30;
+      e.z |= ((steps >> 4) & 3u) << 30;
+      e.w |= last << 16;
+      pa[slot] = e;
+      pb[slot] = make_uint2(wb0.x, wb0.y | ((steps >> 6) << 25) | (ends ? 1u << 26 : 0u));
     };
     // the end cell (brick-local): the last cell of the ray's last pair
-    const uint32_t endc = bk_lds_off((uint32_t)R.ce[0] & m5, (uint32_t)R.ce[1] & m5, (uint32_t)R.ce[2] & m5);
+    const uint32_t endc = bk_lds_word((uint32_t)R.ce[0] & m5, (uint32_t)R.ce[1] & m5, (uint32_t)R.ce[2] & m5);
     // fine-crossing index of the boundary crossed (axis a) to enter brick coordinate nb:
     // moving up, cell nb*32 is reached by crossing nb*32 - cs - 1; moving down, cell
     // nb*32 + 31 by crossing cs - nb*32 - 32.  (Derived from the brick coordinate, not
@@ -945,6 +964,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets
     };
     const int32_t c00[3] = {0, 0, 0};
     uint4 cur = entry(c00);
+    int32_t idx = 0;  // crossings before the current pair's first cell
     uint32_t slot = 0;
     bk_coarse(bg, R, [&](int b, int a, int bx, int by, int bz) {
       if (a >= 0) {
@@ -953,17 +973,14 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets
         if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
         else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
         else bk::counts_at(R, 2, boundary_k(2, bz), c);
-        const uint32_t lc = last_before(c, a);
-        cur.w |= lc << 18;
-        pa[slot] = cur;
-        pb[slot] = make_uint2(wb0.x, wb0.y | ((lc >> 14) << 25));
+        const int32_t nidx = c[0] + c[1] + c[2];
+        put(slot, cur, last_before(c, a), (uint32_t)(nidx - idx - 1), false);
         cur = entry(c);
+        idx = nidx;
       }
       slot = hist_take_agg(hist, b);
     });
-    cur.w |= endc << 18;
-    pa[slot] = cur;
-    pb[slot] = make_uint2(wb0.x, wb0.y | ((endc >> 14) << 25) | (R.end_inside ? 1u << 29 : 0u));
+    put(slot, cur, endc, (uint32_t)(R.nsteps - idx), R.end_inside);
   }
 }
 
@@ -978,11 +995,20 @@ __device__ inline uint32_t bk_order(uint32_t k, uint32_t n) {
   return k < n1 ? (k % S_ORDER) * per + k / S_ORDER : k;
 }
 
+// Bit select with an all-ones / all-zero mask: m ? a : b (one v_bfi_b32, no SGPR mask).
+__device__ inline int32_t bsel(int32_t m, int32_t a, int32_t b) { return (a & m) | (b & ~m); }
+
 // Phase F (persistent; a work queue of parts, every workgroup exits when it is empty).
 // Each lane walks one pair at a time; a wave refills its idle lanes when >= REFILL are
 // idle, from per-lane records prefetched one refill ahead (their load latency is hidden
 // behind the walk of the current pairs).
-template <int REFILL, int S_ORDER, bool BATCH>
+//
+// The walk runs in blocks of UNROLL steps with no branch and no scalar mask work inside:
+// a lane with `rem` steps left adds to its cell while u < rem and to a private dummy word
+// past the box otherwise (its state keeps moving, harmlessly: 8 extra steps change |E|
+// by < 2^30).  The DDA selection works on VGPR masks: the E fields are kept biased by -1
+// so that (E' >> 31) is all-ones exactly when E <= 0, and every select is a bit select.
+template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, int CHUNK, bool BR>
 __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const uint4* __restrict__ pa,
                                                         const uint2* __restrict__ pb,
                                                         const uint32_t* __restrict__ off,
@@ -991,14 +1017,25 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
                                                         unsigned long long* __restrict__ ctl,
                                                         int32_t* __restrict__ hits, int32_t* __restrict__ misses,
                                                         unsigned long long* __restrict__ stats) {
-  __shared__ uint32_t box[kBkBoxWords + 4];  // counters (skewed), then 4 control words
+  // counters (skewed), 4 control words, then one dummy word per lane
+  __shared__ uint32_t box[kBkBoxWords + 4 + 64];
   uint32_t* sh = box + kBkBoxWords;
   stats = stat_slot(stats);
   const int tid = threadIdx.x, l = tid & 63;
+  const int dummy = (kBkBoxWords + 4 + l) * 4;
   for (int i = tid; i < kBkBoxWords; i += blockDim.x) box[i] = 0;
   const uint32_t nparts = (uint32_t)ctl[1];
   const Tiles tl = tiles_of(g.n);
   unsigned long long npairs = 0, nparts_done = 0, nflush = 0;
+#if defined(DMF_EXP_STATS)
+  unsigned long long nblocks = 0, nlanes = 0, nrefill = 0, t_refill = 0, t_walk = 0, t_flush = 0;
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#define DMF_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
+#define DMF_TACC(acc, x) acc += __builtin_amdgcn_s_memtime() - (x)
+#else
+#define DMF_T(x)
+#define DMF_TACC(acc, x)
+#endif
   for (;;) {
     if (tid == 0) {
       sh[0] = (uint32_t)atomicAdd(&ctl[2], 1ull);
@@ -1023,141 +1060,168 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       npairs += n;
       ++nparts_done;
     }
-    // walk state (K negated once per pair: the step is adds and selects only)
-    int32_t E01 = 0, E02 = 0, E12 = 0, K1 = 0, K2 = 0, nK0 = 0, nK1 = 0;
-    int cur = 0, cend = 0, dX = 0, dY = 0, dZ = 0;  // LDS byte offsets; idle lane: cur == cend
-    auto decode = [&](const uint4& ra, const uint2& rb) {
-      E01 = (int32_t)ra.x;
-      E02 = (int32_t)ra.y;
-      E12 = (int32_t)ra.z;
-      const uint32_t w = ra.w;
+    // walk state per slot (biased E, K negated once per pair: the step is adds and bit
+    // selects).  NSLOT pairs per lane walk interleaved: independent dependency chains in
+    // one basic block, so a wave keeps issuing while one chain waits on its last result.
+    int32_t E01[NSLOT], E02[NSLOT], E12[NSLOT], K1[NSLOT], K2[NSLOT], nK0[NSLOT], nK1[NSLOT];
+    // BR (branchy walk): a slot is active while cur != cend (its last cell); otherwise while
+    // rem > 0, with the steps past the end sent to the lane's dummy word
+    int cur[NSLOT], rem[NSLOT], cend[NSLOT], dX[NSLOT], dY[NSLOT], dZ[NSLOT];
+    uint4 ca[NSLOT];
+    uint2 cb[NSLOT];
+    bool fok[NSLOT];
+#pragma unroll
+    for (int q = 0; q < NSLOT; ++q) {
+      E01[q] = E02[q] = E12[q] = K1[q] = K2[q] = nK0[q] = nK1[q] = 0;
+      cur[q] = rem[q] = cend[q] = dX[q] = dY[q] = dZ[q] = 0;
+      ca[q] = make_uint4(0, 0, 0, 0);
+      cb[q] = make_uint2(0, 0);
+      fok[q] = false;
+    }
+    auto decode = [&](int q) {
+      const uint4 ra = ca[q];
+      const uint2 rb = cb[q];
+      E01[q] = __builtin_amdgcn_sbfe((int32_t)ra.x, 0, 30) - 1;
+      E02[q] = __builtin_amdgcn_sbfe((int32_t)ra.y, 0, 30) - 1;
+      E12[q] = __builtin_amdgcn_sbfe((int32_t)ra.z, 0, 30) - 1;
       const uint32_t a0 = rb.x & 0x3ffffu, a1 = rb.y & 0x3ffffu, a2 = (rb.x >> 18) | (((rb.y >> 18) & 15u) << 14);
-      nK0 = -(int32_t)(a0 << 9);
-      K1 = (int32_t)(a1 << 9);
-      K2 = (int32_t)(a2 << 9);
-      nK1 = -K1;
-      cur = (int)(w & 0x3ffffu);
-      cend = (int)((w >> 18) | (((rb.y >> 25) & 15u) << 14));
-      dX = (rb.y >> 22) & 1u ? -(4 * kBkSx) : 4 * kBkSx;
-      dY = (rb.y >> 23) & 1u ? -(4 * kBkSy) : 4 * kBkSy;
-      dZ = (rb.y >> 24) & 1u ? -4 : 4;
+      nK0[q] = -(int32_t)(a0 << 9);
+      K1[q] = (int32_t)(a1 << 9);
+      K2[q] = (int32_t)(a2 << 9);
+      nK1[q] = -K1[q];
+      cur[q] = (int)(ra.w & 0xffffu) * 4;
+      cend[q] = (int)(ra.w >> 16) * 4;
+      rem[q] = (int)((ra.x >> 30) | ((ra.y >> 30) << 2) | ((ra.z >> 30) << 4) | (((rb.y >> 25) & 1u) << 6));
+      dX[q] = (rb.y >> 22) & 1u ? -(4 * kBkSx) : 4 * kBkSx;
+      dY[q] = (rb.y >> 23) & 1u ? -(4 * kBkSy) : 4 * kBkSy;
+      dZ[q] = (rb.y >> 24) & 1u ? -4 : 4;
       // the pair's last cell: a hit when the ray ends there inside the grid, else a miss
-      atomicAdd((uint32_t*)((char*)box + cend), (rb.y >> 29) & 1u ? 0x10000u : 1u);
+      atomicAdd(&box[ra.w >> 16], (rb.y >> 26) & 1u ? 0x10000u : 1u);
     };
-    // BATCH: two 64-record batches per wave; `c` is handed out to idle lanes (ds_bpermute
-    // from the lane holding the record) while `x` is in flight.  Otherwise: one record
-    // per lane (in c), prefetched one refill ahead.
-    uint4 ca = make_uint4(0, 0, 0, 0), xa = ca;
-    uint2 cb = make_uint2(0, 0), xb = cb;
-    int c_n = 0, c_pos = 0, x_n = 0;
-    bool fok = false, more = true;
-    auto load_batch = [&](uint4& ra, uint2& rb) -> int {
-      uint32_t base0 = 0;
-      if (l == 0) base0 = atomicAdd(&sh[1], 64u);
-      const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
-      const int cntb = base >= n ? 0 : (int)min(64u, n - base);
-      if (l < cntb) {
-        const uint32_t i = p0 + bk_order<S_ORDER>(base + (uint32_t)l, n);
-        ra = pa[i];
-        rb = pb[i];
-      }
-      return cntb;
-    };
-    auto prefetch = [&](uint64_t need) {  // lanes in `need` allocate and load their next record
-      const int nn = __builtin_popcountll(need);
-      uint32_t base0 = 0;
-      if (l == 0) base0 = atomicAdd(&sh[1], (uint32_t)nn);
-      const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
-      if (base + (uint32_t)nn >= n) more = false;
-      if ((need >> l) & 1ull) {
-        const uint32_t k = base + (uint32_t)lane_prefix(need);
-        fok = k < n;
-        if (fok) {
-          const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
-          ca = pa[i];
-          cb = pb[i];
+    bool more = true, last_chunk = false;
+    uint32_t wcur = 0, wend = 0;  // CHUNK > 0: the wave's current index range
+    // lanes in need[q] allocate and load the next record of slot q (one LDS allocation
+    // for all slots)
+    auto prefetch = [&](const uint64_t* need) {
+      int nn = 0;
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) nn += __builtin_popcountll(need[q]);
+      uint32_t base, avail = (uint32_t)nn, nbase = 0, roff = 0;
+      if (CHUNK == 0) {  // one LDS allocation per refill
+        uint32_t base0 = 0;
+        if (l == 0) base0 = atomicAdd(&sh[1], (uint32_t)nn);
+        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
+        if (base + (uint32_t)nn >= n) more = false;
+      } else {  // wave-private chunks of CHUNK indices: an LDS allocation (and its
+                // lgkmcnt drain behind the wave's queued adds) only every CHUNK pairs
+        base = wcur;
+        avail = wend - wcur;
+        if (avail < (uint32_t)nn) {
+          uint32_t c0 = 0;
+          if (l == 0) c0 = atomicAdd(&sh[1], (uint32_t)CHUNK);
+          nbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)c0);
+          wcur = nbase + ((uint32_t)nn - avail);
+          wend = nbase + CHUNK;
+          if (nbase + CHUNK >= n) last_chunk = true;
+        } else {
+          wcur += (uint32_t)nn;
         }
+        if (last_chunk && wcur >= n) more = false;
+      }
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) {
+        if ((need[q] >> l) & 1ull) {
+          const uint32_t rk = roff + (uint32_t)lane_prefix(need[q]);  // rank among this refill's takers
+          const uint32_t k = CHUNK == 0 ? base + (uint32_t)lane_prefix(need[q])
+                                        : (rk < avail ? base + rk : nbase + (rk - avail));
+          fok[q] = k < n;
+          if (fok[q]) {
+            const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
+            ca[q] = pa[i];
+            cb[q] = pb[i];
+          }
+        }
+        base += (uint32_t)__builtin_popcountll(need[q]);
+        roff += (uint32_t)__builtin_popcountll(need[q]);
       }
     };
-    auto adopt = [&](uint64_t take, int src) {  // BATCH: lanes in `take` adopt lane `src` of c
-      const int ad = src << 2;
-      uint4 ra;
-      uint2 rb;
-      ra.x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)ca.x);
-      ra.y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)ca.y);
-      ra.z = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)ca.z);
-      ra.w = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)ca.w);
-      rb.x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)cb.x);
-      rb.y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)cb.y);
-      if ((take >> l) & 1ull) decode(ra, rb);
-    };
-    if constexpr (BATCH) {
-      c_n = load_batch(ca, cb);
-      x_n = c_n == 64 ? load_batch(xa, xb) : 0;
-    } else {
-      prefetch(~0ull);
+    {
+      uint64_t all[NSLOT];
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) all[q] = ~0ull;
+      prefetch(all);
     }
     for (;;) {
-      uint64_t act = __builtin_amdgcn_ballot_w64(cur != cend);
-      if constexpr (BATCH) {
-        if (__builtin_popcountll(act) <= 64 - REFILL && c_pos < c_n) {
-          const uint64_t idle = ~act;
-          const int need = 64 - __builtin_popcountll(act);
-          const int k = lane_prefix(idle);  // rank of this lane among the idle ones
-          const int avail = c_n - c_pos;
-          adopt(idle & __builtin_amdgcn_ballot_w64(k < avail), min(c_pos + k, 63));
-          if (need < avail) {
-            c_pos += need;
-          } else {  // batch c exhausted: x becomes c, the next batch is loaded into x
-            ca = xa;
-            cb = xb;
-            c_n = x_n;
-            c_pos = 0;
-            x_n = c_n == 64 ? load_batch(xa, xb) : 0;
-            const int rest = need - avail;
-            if (rest > 0 && c_n > 0) {
-              const int k2 = k - avail;
-              adopt(idle & __builtin_amdgcn_ballot_w64(k2 >= 0 && k2 < c_n), min(max(k2, 0), 63));
-              c_pos = min(rest, c_n);
+      int nact = 0;
+      bool any_act = false;
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) {
+        const uint64_t a = __builtin_amdgcn_ballot_w64(BR ? cur[q] != cend[q] : rem[q] > 0);
+        nact += __builtin_popcountll(a);
+        any_act |= a != 0;
+      }
+      DMF_T(tr0);
+      if (nact <= 64 * NSLOT - REFILL) {
+        uint64_t take[NSLOT];
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < NSLOT; ++q) {
+          take[q] = __builtin_amdgcn_ballot_w64((BR ? cur[q] == cend[q] : rem[q] <= 0) && fok[q]);
+          any |= take[q] != 0;
+        }
+        if (any) {
+#if defined(DMF_EXP_STATS)
+          if (l == 0) ++nrefill;
+#endif
+#pragma unroll
+          for (int q = 0; q < NSLOT; ++q) {
+            if ((BR ? cur[q] == cend[q] : rem[q] <= 0) && fok[q]) {
+              decode(q);
+              fok[q] = false;
             }
           }
-          act = __builtin_amdgcn_ballot_w64(cur != cend);
+          if (more) prefetch(take);
+          any_act = false;
+#pragma unroll
+          for (int q = 0; q < NSLOT; ++q)
+            any_act |= __builtin_amdgcn_ballot_w64(BR ? cur[q] != cend[q] : rem[q] > 0) != 0;
         }
-        if (!act) {
-          if (c_pos >= c_n) break;
-          continue;
-        }
-      } else {
-        if (__builtin_popcountll(act) <= 64 - REFILL) {
-          const uint64_t take = __builtin_amdgcn_ballot_w64(cur == cend && fok);
-          if (take) {
-            if (cur == cend && fok) {
-              decode(ca, cb);
-              fok = false;
-            }
-            if (more) prefetch(take);
-            act = __builtin_amdgcn_ballot_w64(cur != cend);
-          }
-        }
-        if (!act) {
-          if (!__builtin_amdgcn_ballot_w64(fok)) break;
-          continue;
+      }
+      DMF_TACC(t_refill, tr0);
+      if (!any_act) {
+        bool pending = false;
+#pragma unroll
+        for (int q = 0; q < NSLOT; ++q) pending |= __builtin_amdgcn_ballot_w64(fok[q]) != 0;
+        if (!pending) break;
+        continue;
+      }
+      DMF_T(tw0);
+#if defined(DMF_EXP_STATS)
+      if (l == 0) ++nblocks;
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q)
+        nlanes += (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(BR ? cur[q] != cend[q] : rem[q] > 0));
+#endif
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+        for (int q = 0; q < NSLOT; ++q) {
+          if (BR && cur[q] == cend[q]) continue;
+          atomicAdd((uint32_t*)((char*)box + (BR || u < rem[q] ? cur[q] : dummy)), 1u);
+          const bool b10 = E01[q] >= 0;              // E01 > 0 (biased): T1 < T0
+          const bool s2 = (b10 ? E12[q] : E02[q]) >= 0;  // T2 first
+          const bool s1 = !s2 && b10, s0 = !s2 && !b10;
+          E01[q] += s0 ? K1[q] : (s1 ? nK0[q] : 0);
+          E02[q] += s0 ? K2[q] : (s2 ? nK0[q] : 0);
+          E12[q] += s1 ? K2[q] : (s2 ? nK1[q] : 0);
+          cur[q] += s2 ? dZ[q] : (s1 ? dY[q] : dX[q]);
         }
       }
 #pragma unroll
-      for (int u = 0; u < kBkUnroll; ++u) {
-        if (cur != cend) {
-          atomicAdd((uint32_t*)((char*)box + cur), 1u);
-          const bool b10 = E01 > 0;
-          const bool s2 = (b10 ? E12 : E02) > 0;
-          const bool s1 = !s2 && b10, s0 = !s2 && !b10;
-          E01 += s0 ? K1 : (s1 ? nK0 : 0);
-          E02 += s0 ? K2 : (s2 ? nK0 : 0);
-          E12 += s1 ? K2 : (s2 ? nK1 : 0);
-          cur += s2 ? dZ : (s1 ? dY : dX);
-        }
-      }
+      for (int q = 0; q < NSLOT; ++q) rem[q] -= UNROLL;
+      DMF_TACC(t_walk, tw0);
     }
+    DMF_T(tf0);
     __syncthreads();
     // flush: e -> 2x2x4 tile (e >> 4) of the brick, cell (e & 15) as in the tiled layout,
     // so 16 lanes cover one 64-B counter line
@@ -1180,10 +1244,24 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       }
     }
     __syncthreads();
+    DMF_TACC(t_flush, tf0);
   }
   if (stats) {
     for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
     if (l == 0 && nflush) atomicAdd(&stats[6], nflush);
+#if defined(DMF_EXP_STATS)
+    if (l == 0) {  // diagnostic: wave blocks, active lanes at block start, refills
+      atomicAdd(&stats[7], nblocks);
+      atomicAdd(&stats[8], nlanes);
+      atomicAdd(&stats[9], nrefill);
+      atomicAdd(&stats[10], t_refill);
+      atomicAdd(&stats[11], t_walk);
+      atomicAdd(&stats[12], t_flush);
+      const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+      atomicMax(&stats[13], t_end - t_start);  // longest workgroup lifetime
+      atomicAdd(&stats[14], t_end - t_start);  // sum over waves of lifetimes
+    }
+#endif
     if (tid == 0) {
       if (npairs) atomicAdd(&stats[4], npairs);
       if (nparts_done) atomicAdd(&stats[5], nparts_done);
@@ -1356,15 +1434,15 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                        (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra, (uint2*)prb);
     DMF_LAUNCH_CHECK();
     const unsigned nf = (unsigned)std::min<unsigned long long>((unsigned long long)ncu, hc[1]);
-#define DMF_BK_FUSE(R, S, B)                                                                                     \
-  hipLaunchKernelGGL((k_bk_fuse<R, S, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg, (const uint4*)pra, \
+#define DMF_BK_FUSE(R, S, U, N, C, B)                                                                                   \
+  hipLaunchKernelGGL((k_bk_fuse<R, S, U, N, C, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg, (const uint4*)pra, \
                      (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt, (const uint32_t*)part_pref, ctlp,  \
                      d_hits, d_misses, st)
     switch (fuse_variant()) {
-      case 41: DMF_BK_FUSE(16, 8, true); break;
-      case 42: DMF_BK_FUSE(32, 8, false); break;
-      case 43: DMF_BK_FUSE(8, 8, false); break;
-      default: DMF_BK_FUSE(16, 8, false); break;
+      case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
+      case 42: DMF_BK_FUSE(32, 8, 8, 2, 0, false); break;
+      case 43: DMF_BK_FUSE(16, 8, 8, 1, 256, true); break;
+      default: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
     }
 #undef DMF_BK_FUSE
     DMF_LAUNCH_CHECK();
@@ -1398,11 +1476,11 @@ static const char* variant_name(int v) {
     case 31: return "dmf::k_fuse_l<12, 1280>";
     case 32: return "dmf::k_fuse_l<14, 1536>";
     case 33: return "dmf::k_fuse_l<12, 1536>";
-    case 40: return "dmf::k_bk_fuse<16, 8, false>";
-    case 41: return "dmf::k_bk_fuse<16, 8, true>";
-    case 42: return "dmf::k_bk_fuse<32, 8, false>";
-    case 43: return "dmf::k_bk_fuse<8, 8, false>";
-    default: return "dmf::k_bk_fuse<16, 8, false>";  // grids over 1024 cells per axis: k_fuse_l<12, 1280>
+    case 40: return "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>";
+    case 41: return "dmf::k_bk_fuse<16, 8, 8, 1, 0, false>";
+    case 42: return "dmf::k_bk_fuse<32, 8, 8, 2, 0, false>";
+    case 43: return "dmf::k_bk_fuse<16, 8, 8, 1, 256, true>";
+    default: return "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>";  // grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
 }
 

@@ -56,7 +56,11 @@ enum ScratchSlot {
 // Striped statistics: kernels add into slot (block % kStatSlots) of a zeroed buffer
 // of kStatSlots x kStatWidth counters (one hot address per counter serialises at the
 // memory side); stats_end() sums the slots into the caller's counters.
+#if defined(DMF_EXP_STATS)
+constexpr int kStatSlots = 256, kStatWidth = 16;  // diagnostic builds: extra counters 7..15
+#else
 constexpr int kStatSlots = 256, kStatWidth = 8;
+#endif
 int stats_begin(dmf_volume* v, unsigned long long** striped);
 int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int ncounters);
 __device__ inline unsigned long long* stat_slot(unsigned long long* base) {

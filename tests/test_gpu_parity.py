@@ -705,7 +705,7 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch):
     _lib.check(L.dmf_fuse_set_variant(40))  # the brick pipeline at this small grid
     try:
         hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
-        assert L.dmf_fuse_kernel().decode() == "dmf::k_bk_fuse<16, 8, false>"
+        assert L.dmf_fuse_kernel().decode() == "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>"
     finally:
         _lib.check(L.dmf_fuse_set_variant(0))
     assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)

@@ -8,6 +8,16 @@ NAME=$1; shift
 OUT=build_exp/$NAME
 mkdir -p "$OUT"
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-function -I../include -Icsrc"
-/opt/rocm/bin/hipcc $FLAGS "$@" -c csrc/dmf_fuse.hip -o "$OUT/dmf_fuse.o"
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libdmf.so" build/dmf_core.o build/dmf_trace.o "$OUT/dmf_fuse.o" build/dmf_ogrid.o -Wl,-soname,libdmf.so
+# ALL=1: rebuild every object with the extra flags (needed when they change shared headers)
+OBJS=""
+for f in dmf_core dmf_trace dmf_fuse dmf_ogrid; do
+  if [ "$f" = dmf_fuse ] || [ -n "$ALL" ]; then
+    /opt/rocm/bin/hipcc $FLAGS "$@" -c csrc/$f.hip -o "$OUT/$f.o" &
+    OBJS="$OBJS $OUT/$f.o"
+  else
+    OBJS="$OBJS build/$f.o"
+  fi
+done
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT/libdmf.so" $OBJS -Wl,-soname,libdmf.so
 echo "$OUT/libdmf.so"
