@@ -5,9 +5,11 @@
 into a replicated 512^3 grid, N=8 -> 1024 poses).
 
 One step = clear the int32 hit/miss counters, fuse the rank's 128 depth frames
-(back-projection + exact integer 3D-DDA, libdmf.so brick pipeline k_bk_*), RCCL
-all-reduce(SUM) of the counters across ranks (N>1), finalize to the clamped int16
-log-odds grid (k_finalize).  Inputs are resident in HBM before timing starts.
+(back-projection + exact integer 3D-DDA, libdmf.so brick pipeline k_bk_*), merge the
+ranks' counters (N>1: RCCL reduce-scatter, slab finalize, all-gather of the int16 slabs,
+libdmf dmf_fuse_merge_finalize_device) or finalize (N=1) to the clamped int16 log-odds
+grid.  The merge of step i overlaps the fusion of step i+1 (dmf_amd.schedule).  Inputs
+are resident in HBM before timing starts.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 through
 torch.distributed.run (one rank per GPU, RCCL over xGMI).  Rank 0 prints ONE JSON line.
@@ -32,6 +34,7 @@ sys.path[:0] = [ROOT, PKG]
 import dmf_amd  # noqa: E402
 from dmf_amd import _lib, scene  # noqa: E402
 from dmf_amd import dist as D  # noqa: E402
+from dmf_amd import schedule as S  # noqa: E402
 
 GRID = 512
 WIDTH, HEIGHT = 640, 480
@@ -68,6 +71,8 @@ def workload_name(grid, P, world):
         return "config3"
     if (WIDTH, HEIGHT, grid) == (1280, 720, 1024):
         return "config5-shard"
+    if (WIDTH, HEIGHT, grid) == (640, 480, 512) and P * world == 1024 and world == 1:
+        return "config4-anchor (all 1024 poses on one GPU)"
     if (WIDTH, HEIGHT, grid) == (640, 480, 512):
         return "config4-shard"
     return "custom"
@@ -89,6 +94,33 @@ def cpu_baseline(K, poses, depth, n_frames, grid, threads=1):
                             dmax=scene.DEPTH_MAX_MM, hits=hits, misses=misses, threads=threads)
     dt = time.perf_counter() - t0
     return float(st[0]) / dt, float(st[1]) / dt, dt
+
+
+def pmc_traffic(grid, poses, image, kernel):
+    """HBM bytes per fusion launch measured by rocprofv3 PMC passes of this exact
+    configuration and kernel (profiles/pmc_traffic.json, written by tools/pmc_summary.py
+    from tools/profile_round.sh runs; FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), or
+    (None, None) when this configuration has not been profiled."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        table = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    for e in table:
+        if (e.get("grid"), e.get("poses"), e.get("image"), e.get("kernel")) == (grid, poses, image, kernel):
+            return e.get("hbm_bytes_per_launch"), e.get("profile")
+    return None, None
+
+
+def one_rccl_mapped():
+    """libdmf's RCCL calls take torch's communicator pointer: both must be the same
+    librccl instance (same soname, loaded once by torch).  True if exactly one is mapped."""
+    try:
+        maps = open("/proc/self/maps").read().splitlines()
+    except OSError:
+        return False
+    paths = {ln.split()[-1] for ln in maps if "librccl" in ln}
+    return len(paths) == 1
 
 
 def host_threads():
@@ -124,8 +156,7 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local_rank)
-    force_pipe = os.environ.get("DMF_BENCH_PIPELINE") == "1" and "RANK" in os.environ
-    if world > 1 or force_pipe:
+    if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     grid = args.grid
@@ -150,123 +181,94 @@ def main():
 
     d_depth = torch.from_numpy(depth.view(np.int16)).to(dev)
     d_poses = torch.from_numpy(np.ascontiguousarray(poses, np.float32)).to(dev)
-    nct = C.c_int64()
-    _lib.check(L.dmf_fuse_counter_cells(vol._h, C.addressof(nct)))
-    nct = nct.value  # tiled counter layout
-    counters = torch.zeros(2 * nct, dtype=torch.int32, device=dev)  # [hits | misses]: one all-reduce
-    logodds = torch.empty(ncell, dtype=torch.int16, device=dev)
+    # tiled counters padded to whole tile rows per rank: [hits | misses]
+    npad = C.c_int64()
+    _lib.check(L.dmf_fuse_counter_cells_padded(vol._h, world, C.addressof(npad)))
+    npad = npad.value
+    nlo = C.c_int64()
+    _lib.check(L.dmf_fuse_logodds_cells_padded(vol._h, world, C.addressof(nlo)))
+    logodds = torch.empty(nlo.value, dtype=torch.int16, device=dev)
     stats = torch.zeros(16, dtype=torch.int64, device=dev)  # 8 used; diagnostic builds add 7..15
     pcam, pprm = C.addressof(cam), C.addressof(prm)
+    # all fusion scratch allocated up front: the timed calls neither allocate nor sync
+    _lib.check(L.dmf_fuse_reserve(vol._h, pcam, P, 0))
 
-    # N > 1: the merge of step i (RCCL all-reduce on its own stream) overlaps the fusion of
-    # step i+1 on the compute stream; counters are double-buffered and step i is finalized
-    # behind fuse(i+1).  N = 1 has no collective and runs the plain sequence.
-    # (DMF_BENCH_PIPELINE=1 forces the pipelined schedule, e.g. under a world-1 RCCL group.)
-    pipelined = world > 1 or force_pipe
-    comm = torch.cuda.Stream(dev) if pipelined else None
-    bufs = [counters, torch.zeros_like(counters)] if pipelined else [counters]
-    pending = []  # (buffer, all-reduce-done event) of the step awaiting its finalize
-    ev = []
+    # The step schedule (dmf_amd.schedule.run_steps, tested on CPU under random stream
+    # orders): clear + fuse on the compute stream; the merge of step i on the comm stream,
+    # overlapping the fusion of step i+1 (two counter buffers).  Merge = libdmf's
+    # reduce-scatter / slab finalize / all-gather over torch's RCCL communicator (N > 1),
+    # or the plain finalize (N = 1: no collective).
+    merge_mode = os.environ.get("DMF_BENCH_MERGE", "rs")
+    comm_ptr = None
+    if world > 1:
+        dist.barrier()  # connects the RCCL communicator
+        if merge_mode == "rs" and one_rccl_mapped():
+            comm_ptr = D.torch_comm_ptr(device=dev)
+        else:
+            merge_mode = "torch"
+    bufs = [torch.zeros(2 * npad, dtype=torch.int32, device=dev) for _ in range(2)]
+    rt = S.TorchRuntime(dev)  # the volume stays on the compute stream; merges name theirs
+    ev = {}
 
-    class Marks(dict):
-        """Timing events of one step; only recorded ones are read back."""
-        def mark(self, key, strm):
-            e = torch.cuda.Event(enable_timing=True)
-            e.record(strm)
-            self[key] = e
+    def clear(b):
+        bufs[b].zero_()
 
-    def fuse_into(c):
+    def fuse(b, i):
+        c = bufs[b]
         _lib.check(L.dmf_fuse_depth_device(vol._h, pcam, d_depth.data_ptr(), d_poses.data_ptr(), P, pprm,
-                                           c.data_ptr(), c.data_ptr() + 4 * nct, stats.data_ptr()))
+                                           c.data_ptr(), c.data_ptr() + 4 * npad, stats.data_ptr()))
 
-    def finalize(c):
-        _lib.check(L.dmf_fuse_finalize_device(vol._h, c.data_ptr(), c.data_ptr() + 4 * nct, pprm,
-                                              logodds.data_ptr()))
+    def merge(b, i):
+        c = bufs[b]
+        if comm_ptr is not None:
+            D.merge_finalize_device(vol, c, pprm, logodds, comm_ptr, rt.lanes["comm"].cuda_stream)
+        else:
+            if world > 1:
+                dist.all_reduce(c, op=dist.ReduceOp.SUM)  # fallback: torch's RCCL all-reduce
+            _lib.check(L.dmf_fuse_finalize_device(vol._h, c.data_ptr(), c.data_ptr() + 4 * npad, pprm,
+                                                  logodds.data_ptr()))
 
-    def finish_pending(rec=None):
-        if pending:
-            c, reduced = pending.pop()
-            stream.wait_event(reduced)
-            if rec is not None:
-                rec.mark("f0", stream)
-            finalize(c)
-            if rec is not None:
-                rec.mark("f1", stream)
+    def marks(i, name, lane):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(rt.lanes[lane])
+        ev.setdefault(i, {})[name] = e
 
-    def step(i, record=False):
-        # events: clear | fuse on the compute stream, all-reduce on its stream, finalize
-        r = Marks() if record else None
-        c = bufs[i % len(bufs)]
-        if record:
-            r.mark("c0", stream)
-        c.zero_()
-        if record:
-            r.mark("c1", stream)
-        fuse_into(c)
-        if record:
-            r.mark("c2", stream)
-        if not pipelined:
-            if record:
-                r.mark("a0", stream)
-            D.merge_counters(c)  # no collective at world 1
-            if record:
-                r.mark("a1", stream)
-                r.mark("f0", stream)
-            finalize(c)
-            if record:
-                r.mark("f1", stream)
-                ev.append(r)
-            return
-        fused = torch.cuda.Event()
-        fused.record(stream)
-        comm.wait_event(fused)
-        with torch.cuda.stream(comm):
-            if record:
-                r.mark("a0", comm)
-            dist.all_reduce(c, op=dist.ReduceOp.SUM)  # RCCL all-reduce(sum) of [hits | misses]
-            if record:
-                r.mark("a1", comm)
-            reduced = torch.cuda.Event()
-            reduced.record(comm)
-        finish_pending(r)  # finalize step i-1 behind fuse(i)
-        pending.append((c, reduced))
-        if record:
-            ev.append(r)
-
-    for i in range(args.warmup):
-        step(i)
-    finish_pending()
+    S.run_steps(rt, args.warmup, 2, clear, fuse, merge)
     torch.cuda.synchronize(dev)
     stats.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, record=True)
-    finish_pending()
+    S.run_steps(rt, args.steps, 2, clear, fuse, merge, marks=marks)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = stats.cpu().numpy()
+    ev = list(ev.values())
+    nct = npad
 
     def seg(a, b):
         v = [r[a].elapsed_time(r[b]) for r in ev if a in r and b in r]
         return float(np.mean(v)) if v else 0.0
-    clear_ms, fuse_ms, allreduce_ms = seg("c0", "c1"), seg("c1", "c2"), seg("a0", "a1")
-    finalize_ms = seg("f0", "f1")
-    breakdown = {"clear": clear_ms, "fuse": fuse_ms, "allreduce": allreduce_ms, "finalize": finalize_ms,
-                 "compute_only": clear_ms + fuse_ms + finalize_ms,
-                 "schedule": "all-reduce of step i overlapped with fuse of step i+1" if pipelined else "sequential"}
+    clear_ms, fuse_ms, merge_ms = seg("c0", "c1"), seg("c1", "c2"), seg("a0", "a1")
+    breakdown = {"clear": clear_ms, "fuse": fuse_ms, "merge": merge_ms,
+                 "merge_kind": {"rs": "RCCL reduce-scatter(hits, misses) + slab finalize + all-gather(int16) "
+                                      "(dmf_fuse_merge_finalize_device)",
+                                "torch": "torch RCCL all-reduce(sum) + finalize"}[merge_mode] if world > 1
+                 else "finalize (no collective at N=1)",
+                 "schedule": "merge of step i on the comm stream overlaps fuse of step i+1 (2 counter buffers)"}
     # grid-wide streaming passes, priced separately (SURVEY.md §8d): clear writes the
     # 2 tiled int32 counter arrays; finalize reads them and writes int16 log-odds
-    clear_bytes, fin_bytes = 2 * 4 * nct, 10 * ncell
+    clear_bytes = 2 * 4 * nct
     streaming = {
         "clear": {"ms": clear_ms, "bytes": clear_bytes, "GBps": clear_bytes / (clear_ms * 1e-3) / 1e9,
-                  "frac": clear_bytes / (clear_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
-        "finalize": {"ms": finalize_ms, "bytes": fin_bytes, "GBps": fin_bytes / (finalize_ms * 1e-3) / 1e9,
-                     "frac": fin_bytes / (finalize_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+                  "frac": clear_bytes / (clear_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+    if world == 1:
+        fin_bytes = 10 * ncell
+        streaming["finalize"] = {"ms": merge_ms, "bytes": fin_bytes, "GBps": fin_bytes / (merge_ms * 1e-3) / 1e9,
+                                 "frac": fin_bytes / (merge_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     if st[3] != 0:
         raise RuntimeError(f"DDA guard tripped {st[3]} times")
     elapsed = D.max_over_ranks(elapsed, device=dev)
@@ -282,21 +284,12 @@ def main():
         secondary = {}
         if not args.no_secondary:
             secondary = secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K)
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", "pmc_fuse_summary.json")
-        if os.path.exists(tpath):
-            try:
-                tj = json.load(open(tpath))
-                kname = L.dmf_fuse_kernel().decode()
-                if tj.get("grid") == grid and tj.get("poses") == P and tj.get("kernel") == kname:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic, traffic_src = pmc_traffic(grid, P, f"{WIDTH}x{HEIGHT}", L.dmf_fuse_kernel().decode())
         cpu = cpu_mt = None
         if args.cpu_frames > 0 and world == 1:
             ups, rps, dt = cpu_baseline(K, poses, depth, args.cpu_frames, grid)
             cpu = {"value": ups, "unit": "ray-voxel updates/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle fuse of {args.cpu_frames} of the {P} frames (640x480, {grid}^3), "
+                   "sample": f"oracle fuse of {args.cpu_frames} of the {P} frames ({WIDTH}x{HEIGHT}, {grid}^3), "
                              f"{dt:.1f}s single-threaded; Mrays/s {rps / 1e6:.3f}"}
             nt = host_threads()
             nf = min(P, 4 * args.cpu_frames)
@@ -342,12 +335,19 @@ def main():
                                    f"{grid}^3 int16 "
                                    f"log-odds (int32 hit/miss counters)",
                        "grid": grid, "image": f"{WIDTH}x{HEIGHT}", "poses_per_gpu": P, "global_poses": P * world,
-                       "parallelism": f"pose-sharded dp{world} + RCCL all-reduce(sum) of counters"},
+                       "parallelism": f"pose-sharded dp{world}" + (
+                           " + RCCL reduce-scatter / all-gather merge (libdmf)" if merge_mode == "rs" and world > 1
+                           else " + RCCL all-reduce(sum) merge" if world > 1 else "")},
             "mrays_per_s": rays / elapsed / 1e6,
             "fuse_diagnostics": diagnostics,
             "updates_per_ray": updates / max(rays, 1.0),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "basis": "effective (algorithmic): SURVEY.md 8d bytes, 4 B per cell update + 2 B per depth "
+                                  "pixel, over the fusion launch's HIP-event time; the brick pipeline accumulates "
+                                  "in LDS, so these bytes are a price, not its HBM traffic",
+                         "measured_frac": (traffic / (fuse_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                         "traffic_source": traffic_src,
                          "kernel": kname, "kernel_ms": fuse_ms, "pipeline": pipeline,
                          "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,

@@ -745,16 +745,31 @@ int dmf_volume_destroy(dmf_volume* v) {
   if (v->stream) (void)hipStreamSynchronize(v->stream);
   (void)hipDeviceSynchronize();
   free_state(v);
+  if (v->switch_ev) (void)hipEventDestroy(v->switch_ev);
   delete v;
   return DMF_OK;
   DMF_API_END
 }
 
+// Switching streams never blocks the host: the new stream waits (hipStreamWaitEvent) for
+// the work already enqueued on the old one, so scratch buffers in flight stay ordered.
+// A new stream that is capturing a graph is not made to wait on a non-captured event
+// (not permitted during capture): the capturing caller orders it (torch.cuda.graph
+// does, wait_stream before capture).
 int dmf_volume_set_stream(dmf_volume* v, void* s) {
   if (!v) return fail(DMF_ERR_INVALID, "null volume");
   DMF_TRY(activate(v));
-  if (v->stream != (hipStream_t)s) DMF_HIP(hipStreamSynchronize(v->stream));
-  v->stream = (hipStream_t)s;
+  const hipStream_t ns = (hipStream_t)s;
+  if (v->stream == ns) return DMF_OK;
+  hipStreamCaptureStatus cs_old = hipStreamCaptureStatusNone, cs_new = hipStreamCaptureStatusNone;
+  DMF_HIP(hipStreamIsCapturing(v->stream, &cs_old));
+  DMF_HIP(hipStreamIsCapturing(ns, &cs_new));
+  if (cs_new == hipStreamCaptureStatusNone && cs_old == hipStreamCaptureStatusNone) {
+    if (!v->switch_ev) DMF_HIP(hipEventCreateWithFlags(&v->switch_ev, hipEventDisableTiming));
+    DMF_HIP(hipEventRecord(v->switch_ev, v->stream));
+    DMF_HIP(hipStreamWaitEvent(ns, v->switch_ev, 0));
+  }
+  v->stream = ns;
   return DMF_OK;
 }
 

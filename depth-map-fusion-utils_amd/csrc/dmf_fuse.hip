@@ -1275,14 +1275,15 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
 // and writes them as one 8-B store; a wave covers 16 tiles along z, so each of its 4 rows
 // gets a contiguous 128-B run.  (One lane per 4 z-cells of a row read a quarter of each
 // 64-B line per wave and relied on L2 for the rest: 3.7 ms at 1024^3.)
+// Tiles [t0, t1) only (a rank's slab after a reduce-scatter).
 __global__ __launch_bounds__(256) void k_finalize(Geom g, const int32_t* __restrict__ hits,
                                                   const int32_t* __restrict__ misses, int l_hit, int l_miss,
-                                                  int l_min, int l_max, int16_t* __restrict__ out) {
+                                                  int l_min, int l_max, int16_t* __restrict__ out, int64_t t0,
+                                                  int64_t t1) {
   const Tiles tl = tiles_of(g.n);
-  const uint32_t ntx = (uint32_t)(g.n[0] + 1) >> 1;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // int4 index
+  const int64_t i = t0 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // int4 index
   const int64_t t = i >> 2;
-  if (t >= (int64_t)ntx * tl.ny * tl.nz) return;
+  if (t >= t1) return;
   const int q = (int)(i & 3);
   const int tz = (int)(t % tl.nz);
   const int64_t r = t / tl.nz;
@@ -1369,26 +1370,51 @@ static int cu_count(int device) {
   return n;
 }
 
-// Brick-owned fusion of P frames (kernels above), in pose batches whose ray indices fit
-// the pair record and whose pair offsets fit 32 bits.
-static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint16_t* d_depth, const PoseX* tab, int P,
-                       const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses, unsigned long long* st) {
-  const BkGeom bg = brick_geom(g);
-  const int pkx = (cp.W + 7) / 8, pky = (cp.H + 7) / 8;
-  const int64_t ppose = (int64_t)pkx * pky;
-  const int64_t max_pairs_ray = 1 + (bg.nb[0] - 1) + (bg.nb[1] - 1) + (bg.nb[2] - 1);
-  const int64_t ray_cap = (int64_t)UINT32_MAX / max_pairs_ray;
-  int64_t PB = std::min<int64_t>(P, ray_cap / (ppose * 64));
+// Pair-buffer budget of the brick pipeline.  The number of (ray, brick) pairs of a batch is
+// known only on the device (pass A), so the host sizes the pair lists by the geometric
+// bound rays x (1 + brick boundaries a grid-crossing ray can pass), and the fusion call
+// never reads anything back: no host synchronisation, no allocation once reserved
+// (dmf_fuse_reserve).  The bound is ~4-5x the pairs of typical scenes, so the per-volume
+// budget caps the poses per batch instead (default 48 GiB of MI355X's 288 GB; a 512^3 /
+// 640x480 128-frame call fits one batch).
+
+struct BkPlan {
+  BkGeom bg;
+  int pkx = 0, pky = 0;
+  int64_t ppose = 0, max_pairs_ray = 0, PB = 0;
+  int ab_threads = 0, span = 0;
+  size_t hist_bytes = 0, nwg_max = 0, pair_cap = 0;
+};
+
+static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, BkPlan& pl) {
+  pl.bg = brick_geom(g);
+  pl.pkx = (cp.W + 7) / 8;
+  pl.pky = (cp.H + 7) / 8;
+  pl.ppose = (int64_t)pl.pkx * pl.pky;
+  pl.max_pairs_ray = 1 + (pl.bg.nb[0] - 1) + (pl.bg.nb[1] - 1) + (pl.bg.nb[2] - 1);
+  const int64_t rays_pose = pl.ppose * 64;
+  const int64_t ray_cap = (int64_t)UINT32_MAX / pl.max_pairs_ray;  // pair offsets are 32-bit
+  const uint64_t per_pose = (uint64_t)rays_pose * (uint64_t)pl.max_pairs_ray * (sizeof(uint4) + sizeof(uint2));
+  int64_t PB = std::min<int64_t>(P, ray_cap / rays_pose);
+  PB = std::min<int64_t>(PB, (int64_t)(v->bk_budget / per_pose));
   if (const char* e = getenv("DMF_BK_BATCH_POSES")) {  // test hook: cap the poses per batch
     const int64_t cap = (int64_t)atoll(e);
     if (cap > 0) PB = std::min<int64_t>(PB, cap);
   }
-  if (PB < 1) return fail(DMF_ERR_RANGE, "image too large for one brick fusion batch");
-  const int ab_threads = bg.nbricks > kBkBigHist ? kBkPassThreadsBig : kBkPassThreads;
+  if (PB < 1) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion pair budget (dmf_fuse_reserve)");
+  pl.PB = PB;
+  pl.ab_threads = pl.bg.nbricks > kBkBigHist ? kBkPassThreadsBig : kBkPassThreads;
   // packets per workgroup of passes A/B (>= 16 per wave; the histogram's zero + flush
   // amortised over >= 64 packets per 1k bricks)
-  const int span = std::max(16 * (ab_threads / 64), (bg.nbricks + 63) / 64);
-  const size_t hist_bytes = sizeof(uint32_t) * (size_t)bg.nbricks;
+  pl.span = std::max(16 * (pl.ab_threads / 64), (pl.bg.nbricks + 63) / 64);
+  pl.hist_bytes = sizeof(uint32_t) * (size_t)pl.bg.nbricks;
+  pl.nwg_max = (size_t)((PB * pl.ppose + pl.span - 1) / pl.span);
+  pl.pair_cap = (size_t)(PB * rays_pose * pl.max_pairs_ray);
+  return DMF_OK;
+}
+
+// A/B histograms above 48 KiB of dynamic LDS need the attribute (once per process).
+static int bk_attributes() {
   static std::atomic<bool> attr_set{false};
   if (!attr_set.load()) {
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1397,47 +1423,59 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                                 (int)(sizeof(uint32_t) * 32768)));
     attr_set.store(true);
   }
-  void *rays, *bricks, *ctl, *wgb;
-  DMF_TRY(scratch(v, kScBkRays, sizeof(ulonglong2) * (size_t)(PB * ppose * 64), &rays));
-  DMF_TRY(scratch(v, kScBkBricks, sizeof(uint32_t) * (3 * (size_t)bg.nbricks + 4), &bricks));
-  DMF_TRY(scratch(v, kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
+  return DMF_OK;
+}
+
+// Every scratch buffer of a plan (allocates only when a slot is too small).
+static int bk_scratch(dmf_volume* v, const BkPlan& pl, void** rays, void** bricks, void** ctl, void** wgb, void** pra,
+                      void** prb) {
+  DMF_TRY(scratch(v, kScBkRays, sizeof(ulonglong2) * (size_t)(pl.PB * pl.ppose * 64), rays));
+  DMF_TRY(scratch(v, kScBkBricks, sizeof(uint32_t) * (3 * (size_t)pl.bg.nbricks + 4), bricks));
+  DMF_TRY(scratch(v, kScBkCtl, sizeof(unsigned long long) * 4, ctl));
   // per-workgroup base inside each brick (pass A -> pass B)
-  const size_t nwg_max = (size_t)((PB * ppose + span - 1) / span);
-  DMF_TRY(scratch(v, kScBkWgBase, sizeof(uint32_t) * nwg_max * (size_t)bg.nbricks, &wgb));
+  DMF_TRY(scratch(v, kScBkWgBase, sizeof(uint32_t) * pl.nwg_max * (size_t)pl.bg.nbricks, wgb));
+  DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * pl.pair_cap, pra));
+  DMF_TRY(scratch(v, kScBkPairsB, sizeof(uint2) * pl.pair_cap, prb));
+  return DMF_OK;
+}
+
+// Brick-owned fusion of P frames (kernels above), in pose batches sized by bk_plan.  Only
+// enqueues work: pass S leaves the pair and part counts on the device, pass B writes the
+// pairs below the planned bound, phase F reads the part count itself (its persistent
+// workgroups exit when the queue is empty).
+static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint16_t* d_depth, const PoseX* tab, int P,
+                       const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses, unsigned long long* st) {
+  BkPlan pl;
+  DMF_TRY(bk_plan(v, cp, g, P, pl));
+  const BkGeom& bg = pl.bg;
+  DMF_TRY(bk_attributes());
+  void *rays, *bricks, *ctl, *wgb, *pra, *prb;
+  DMF_TRY(bk_scratch(v, pl, &rays, &bricks, &ctl, &wgb, &pra, &prb));
   uint32_t* cnt = (uint32_t*)bricks;
   uint32_t* off = cnt + bg.nbricks;
   uint32_t* part_pref = off + bg.nbricks;  // nbricks + 1
   unsigned long long* ctlp = (unsigned long long*)ctl;
-  const int ncu = cu_count(v->device);
-  for (int64_t p0 = 0; p0 < P; p0 += PB) {
-    const int64_t pb = std::min<int64_t>(PB, P - p0);
-    const int64_t npk = pb * ppose;
-    const unsigned nwg = (unsigned)((npk + span - 1) / span);
-    DMF_HIP(hipMemsetAsync(cnt, 0, hist_bytes, v->stream));
+  const unsigned nf = (unsigned)cu_count(v->device);
+  for (int64_t p0 = 0; p0 < P; p0 += pl.PB) {
+    const int64_t pb = std::min<int64_t>(pl.PB, P - p0);
+    const int64_t npk = pb * pl.ppose;
+    const unsigned nwg = (unsigned)((npk + pl.span - 1) / pl.span);
+    DMF_HIP(hipMemsetAsync(cnt, 0, pl.hist_bytes, v->stream));
     DMF_HIP(hipMemsetAsync(ctlp, 0, sizeof(unsigned long long) * 4, v->stream));
-    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(ab_threads), hist_bytes, v->stream, g, cp,
-                       d_depth + (size_t)p0 * cp.H * cp.W, tab + p0, prm->dmin_mm, prm->dmax_mm, pkx, (int)ppose, npk,
-                       span, bg, (ulonglong2*)rays, cnt, (uint32_t*)wgb, st);
+    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, g, cp,
+                       d_depth + (size_t)p0 * cp.H * cp.W, tab + p0, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
+                       npk, pl.span, bg, (ulonglong2*)rays, cnt, (uint32_t*)wgb, st);
     DMF_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, v->stream, bg.nbricks, (const uint32_t*)cnt, off, part_pref,
                        ctlp);
     DMF_LAUNCH_CHECK();
-    unsigned long long hc[2];
-    DMF_HIP(hipMemcpyAsync(hc, ctlp, sizeof(hc), hipMemcpyDeviceToHost, v->stream));
-    DMF_HIP(hipStreamSynchronize(v->stream));
-    if (hc[0] > (unsigned long long)UINT32_MAX) return fail(DMF_ERR_RANGE, "brick fusion batch exceeds 2^32 pairs");
-    if (hc[0] == 0) continue;
-    void *pra, *prb;
-    DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * (size_t)hc[0], &pra));
-    DMF_TRY(scratch(v, kScBkPairsB, sizeof(uint2) * (size_t)hc[0], &prb));
-    hipLaunchKernelGGL(k_bk_pairs, dim3(nwg), dim3(ab_threads), hist_bytes, v->stream, npk, span, bg,
+    hipLaunchKernelGGL(k_bk_pairs, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk, pl.span, bg,
                        (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra, (uint2*)prb);
     DMF_LAUNCH_CHECK();
-    const unsigned nf = (unsigned)std::min<unsigned long long>((unsigned long long)ncu, hc[1]);
-#define DMF_BK_FUSE(R, S, U, N, C, B)                                                                                   \
-  hipLaunchKernelGGL((k_bk_fuse<R, S, U, N, C, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg, (const uint4*)pra, \
-                     (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt, (const uint32_t*)part_pref, ctlp,  \
-                     d_hits, d_misses, st)
+#define DMF_BK_FUSE(R, S, U, N, C, B)                                                                           \
+  hipLaunchKernelGGL((k_bk_fuse<R, S, U, N, C, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,            \
+                     (const uint4*)pra, (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt,           \
+                     (const uint32_t*)part_pref, ctlp, d_hits, d_misses, st)
     switch (fuse_variant()) {
       case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
       case 42: DMF_BK_FUSE(32, 8, 8, 2, 0, false); break;
@@ -1449,6 +1487,26 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   }
   return DMF_OK;
 }
+
+int finalize_tiles(dmf_volume* v, const int32_t* d_hits, const int32_t* d_misses, const dmf_fuse_params* prm,
+                   int16_t* d_out, int64_t t0, int64_t t1, hipStream_t stream) {
+  if (t1 <= t0) return DMF_OK;
+  const int64_t lanes = (t1 - t0) * 4;  // four lanes per 2x2x4 tile
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, v->geom(), d_hits,
+                     d_misses, prm->l_hit, prm->l_miss, prm->l_min, prm->l_max, d_out, t0, t1);
+  DMF_LAUNCH_CHECK();
+  return DMF_OK;
+}
+
+int tile_rows(const dmf_volume* v, int64_t* ntx, int64_t* tiles_per_row) {
+  const Geom g = v->geom();
+  const Tiles tl = tiles_of(g.n);
+  *ntx = (g.n[0] + 1) >> 1;
+  *tiles_per_row = (int64_t)tl.ny * tl.nz;
+  return DMF_OK;
+}
+
+static const dmf_fuse_params kDefaultParamsForCheck = {200, 1000, 847, -405, -2000, 3511};
 
 static int check_fuse(const dmf_volume* v, const dmf_camera* cam, int P, const dmf_fuse_params* prm) {
   DMF_TRY(require_constructed(v));
@@ -1494,6 +1552,28 @@ int dmf_fuse_set_variant(int32_t variant) {
   g_fuse_variant.store(variant, std::memory_order_relaxed);
   g_last_kernel.store(nullptr);
   return DMF_OK;
+}
+
+int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t max_scratch_bytes) {
+  DMF_API_BEGIN
+  DMF_TRY(check_fuse(v, cam, P, &kDefaultParamsForCheck));
+  if (max_scratch_bytes) v->bk_budget = max_scratch_bytes;
+  const CamP cp = cam_params(cam);
+  const Geom g = v->geom();
+  void* tab;
+  DMF_TRY(scratch(v, kScPoses, sizeof(PoseX) * (size_t)P, &tab));
+  unsigned long long* st;
+  DMF_TRY(stats_begin(v, &st));
+  if (brick_path_ok(g)) {
+    BkPlan pl;
+    DMF_TRY(bk_plan(v, cp, g, P, pl));
+    DMF_TRY(bk_attributes());
+    void *rays, *bricks, *ctl, *wgb, *pra, *prb;
+    DMF_TRY(bk_scratch(v, pl, &rays, &bricks, &ctl, &wgb, &pra, &prb));
+  }
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  return DMF_OK;
+  DMF_API_END
 }
 
 int dmf_fuse_counter_cells(const dmf_volume* v, int64_t* n) {
@@ -1618,12 +1698,7 @@ int dmf_fuse_finalize_device(dmf_volume* v, const int32_t* d_hits, const int32_t
   DMF_API_BEGIN
   DMF_TRY(require_constructed(v));
   if (!prm || !d_hits || !d_misses || !d_out) return fail(DMF_ERR_INVALID, "null argument");
-  const Geom g = v->geom();
-  const int64_t lanes = (int64_t)tiled_cells(g.n) / 4;  // four lanes per 2x2x4 tile
-  hipLaunchKernelGGL(k_finalize, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, v->stream, g, d_hits, d_misses,
-                     prm->l_hit, prm->l_miss, prm->l_min, prm->l_max, d_out);
-  DMF_LAUNCH_CHECK();
-  return DMF_OK;
+  return finalize_tiles(v, d_hits, d_misses, prm, d_out, 0, (int64_t)tiled_cells(v->geom().n) / 16, v->stream);
   DMF_API_END
 }
 

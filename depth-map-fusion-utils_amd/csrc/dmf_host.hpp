@@ -50,7 +50,8 @@ int scratch(dmf_volume* v, int k, size_t bytes, void** out);
 enum ScratchSlot {
   kScPoses = 0, kScHost0, kScHost1, kScHost2, kScOut0, kScOut1, kScOut2, kScOut3, kScTmp, kScSort0,
   kScSort1, kScSort2, kScSort3, kScCount, kScStats,
-  kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkWgBase, kScBkCtl  // brick-owned fusion (dmf_fuse.hip)
+  kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkWgBase, kScBkCtl,  // brick-owned fusion (dmf_fuse.hip)
+  kScOgP0, kScOgP1, kScOgFinal, kScOgOcc  // OccupancyGrid reorganization (dmf_ogrid.hip)
 };
 
 // Striped statistics: kernels add into slot (block % kStatSlots) of a zeroed buffer
@@ -71,6 +72,13 @@ __device__ inline unsigned long long* stat_slot(unsigned long long* base) {
 int pose_table(dmf_volume* v, const float* poses, int P, bool poses_on_device, PoseX** d_table);
 
 CamP cam_params(const dmf_camera* c);
+
+// Fusion finalize over tiled counters, tiles [t0, t1) (dmf_fuse.hip); the tiled layout's
+// x extent in 2-cell tile rows and tiles per row (a contiguous tile range of whole rows is
+// an x slab of the grid).
+int finalize_tiles(dmf_volume* v, const int32_t* d_hits, const int32_t* d_misses, const dmf_fuse_params* prm,
+                   int16_t* d_out, int64_t t0, int64_t t1, hipStream_t stream);
+int tile_rows(const dmf_volume* v, int64_t* ntx, int64_t* tiles_per_row);
 int check_camera(const dmf_camera* c);
 
 // Lazily (re)build the float-accumulated enumeration list (reverseRayTrace / rayTraceVolume).

@@ -198,6 +198,7 @@ struct DevVol {
 struct dmf_volume {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipEvent_t switch_ev = nullptr;  // orders a new stream after the old one (dmf_volume_set_stream)
   // reference fields (Volume.hpp:54-60)
   double xmin = 0, xmax = 0, ymin = 0, ymax = 0, zmin = 0, zmax = 0;
   double xcenter = 0, ycenter = 0, zcenter = 0;
@@ -239,6 +240,8 @@ struct dmf_volume {
   int32_t nax[3] = {0, 0, 0};
   uint32_t* d_enum = nullptr;  // occupied enumeration indices, enumeration order
   int64_t nenum = 0, enum_cap = 0, enum_hazards = 0;
+  // brick fusion pair-list budget (dmf_fuse_reserve)
+  uint64_t bk_budget = 48ull << 30;
   // scratch arena
   std::vector<std::pair<void*, size_t>> scratch;
 

@@ -10,6 +10,8 @@
 // 64-bit key voxel << 32 | point, keys are radix-sorted, and one lane folds each
 // voxel's events in order with the reference's float arithmetic (no FMA contraction).
 // Dense per-voxel state in the reference's x-major order, persistent across calls.
+// downloadReorganizedCloud (:200-286) is the same kind of racy loop: its sequential
+// result is computed by fixed-point rounds over sorted (target, source) keys (below).
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -158,6 +160,128 @@ __global__ void k_og_gather(const int32_t* __restrict__ sel, const int32_t* __re
   for (int a = 0; a < 3; ++a) { o[a] = centroid[3 * i + a]; o[3 + a] = normal[3 * i + a]; }
 }
 
+// ---- downloadReorganizedCloud (:200-286) ----------------------------------------
+// Sequential semantics (the reference's OpenMP loops race): voxels are visited x-major;
+// an occupied voxel s (with clean: count >= 100 at its turn) merges its CURRENT
+// reorganized state into the voxel t(s) holding its centroid.  Its current state P(s) is
+// its initial state folded with the merges of the voxels before it that targeted it, so
+// P depends only on lower indices.  Parallel form: iterate
+//   targets t_r(s) from P_r;  P_{r+1}(T) = init(T) folded with [P_r(s) : s < T, t_r(s) = T]
+// (sorted (T, s) keys, one lane per T, sources in index order) until P stops changing;
+// round r makes every voxel of dependency depth < r exact, so the fixed point is the
+// sequential result.  Then one final fold per target over ALL its sources in order gives
+// the reorganized grid (a source equal to its target reads P(T), which is exactly the
+// aliased state the reference reads: n + n, (c + c) / 2).
+struct OgS {
+  float n[3], c[3];
+  int32_t k;
+};
+
+__device__ inline void og_merge(OgS& d, const OgS& s) {  // :242-255
+  const float sum[3] = {d.n[0] + s.n[0], d.n[1] + s.n[1], d.n[2] + s.n[2]};
+  normalized(sum, d.n);
+  if (d.k == 0) {
+    d.c[0] = s.c[0]; d.c[1] = s.c[1]; d.c[2] = s.c[2];
+  } else {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) d.c[a] = (d.c[a] + s.c[a]) / 2.0f;
+    ++d.k;
+  }
+}
+
+__global__ void k_og_reorg_seed(int64_t n, const float* __restrict__ normal, const float* __restrict__ centroid,
+                                const int32_t* __restrict__ count, OgS* __restrict__ P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  OgS s;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { s.n[a] = normal[3 * i + a]; s.c[a] = centroid[3 * i + a]; }
+  s.k = count[i];
+  P[i] = s;
+}
+
+// Keys (t(s) << 32 | s) of the voxels that merge, from their current estimate P(s).
+__global__ void k_og_reorg_keys(OGeom g, int64_t n, const uint8_t* __restrict__ flags, const OgS* __restrict__ P,
+                                int clean, unsigned long long* __restrict__ keys, unsigned long long* __restrict__ cnt) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n || !(flags[s] & 1)) return;
+  const OgS st = P[s];
+  if (clean && st.k < 100) return;
+  int t[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) t[a] = to_int_x86(floor(((double)st.c[a] - g.mn[a]) / g.res[a]));  // :373-379
+  if (!og_valid(g, t[0], t[1], t[2])) return;
+  const uint64_t T = ((uint64_t)t[0] * g.n[1] + t[1]) * g.n[2] + t[2];
+  keys[atomicAdd(cnt, 1ull)] = (T << 32) | (uint64_t)s;
+}
+
+// One lane per target segment of the sorted keys.  FINAL = 0: the target's current state
+// (sources before it only) -> Pn; FINAL = 1: every source in order -> F, and occ[T] = 1.
+template <int FINAL>
+__global__ void k_og_reorg_fold(const unsigned long long* __restrict__ keys, int64_t ne, const OgS* __restrict__ init,
+                                const OgS* __restrict__ P, OgS* __restrict__ out, uint8_t* __restrict__ occ) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ne) return;
+  const uint64_t T = keys[e] >> 32;
+  if (e > 0 && (keys[e - 1] >> 32) == T) return;  // not the first key of its target
+  OgS d = init[T];
+  for (int64_t f = e; f < ne && (keys[f] >> 32) == T; ++f) {
+    const uint64_t s = keys[f] & 0xffffffffull;
+    if (!FINAL && s >= T) break;
+    og_merge(d, P[s]);
+  }
+  out[T] = d;
+  if (FINAL) occ[T] = 1;
+}
+
+__global__ void k_og_reorg_diff(int64_t n, const OgS* __restrict__ a, const OgS* __restrict__ b,
+                                unsigned int* __restrict__ changed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* x = (const uint32_t*)&a[i];
+  const uint32_t* y = (const uint32_t*)&b[i];
+  bool d = false;
+#pragma unroll
+  for (int w = 0; w < 7; ++w) d |= x[w] != y[w];
+  if (d) *changed = 1u;
+}
+
+// Fallback when the rounds do not settle (a dependency chain longer than the round
+// cap): the sequential loop itself, one lane.
+__global__ void k_og_reorg_serial(OGeom g, int64_t n, const uint8_t* __restrict__ flags, int clean,
+                                  OgS* __restrict__ R, uint8_t* __restrict__ occ) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  for (int64_t s = 0; s < n; ++s) {
+    if (!(flags[s] & 1)) continue;
+    const OgS st = R[s];
+    if (clean && st.k < 100) continue;
+    int t[3];
+    for (int a = 0; a < 3; ++a) t[a] = to_int_x86(floor(((double)st.c[a] - g.mn[a]) / g.res[a]));
+    if (!og_valid(g, t[0], t[1], t[2])) continue;
+    const int64_t T = ((int64_t)t[0] * g.n[1] + t[1]) * g.n[2] + t[2];
+    OgS d = R[T];
+    og_merge(d, st);
+    R[T] = d;
+    occ[T] = 1;
+  }
+}
+
+__global__ void k_og_select_reorg(const uint8_t* __restrict__ occ, int64_t n, int32_t* __restrict__ sel) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  sel[i] = occ[i] ? 1 : 0;
+}
+
+__global__ void k_og_gather_state(const int32_t* __restrict__ sel, const int32_t* __restrict__ pos, int64_t n,
+                                  const OgS* __restrict__ F, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !sel[i]) return;
+  float* o = out + 6 * (int64_t)pos[i];
+  const OgS f = F[i];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { o[a] = f.c[a]; o[3 + a] = f.n[a]; }
+}
+
 static OGeom og_geom(const dmf_ogrid* g) {
   OGeom o;
   for (int a = 0; a < 3; ++a) {
@@ -234,6 +358,88 @@ static int og_update(dmf_ogrid* g, const float* d_cloud, int64_t n_cloud, const 
     hipLaunchKernelGGL(k_og_occupy, dim3((unsigned)((n_cloud + 255) / 256)), dim3(256), 0, v->stream, og, d_cloud,
                        n_cloud, g->d_flags);
   DMF_LAUNCH_CHECK();
+  return DMF_OK;
+}
+
+static int og_sort_keys(dmf_volume* v, unsigned long long* kb, size_t ne, size_t ncell, unsigned long long** out) {
+  if (ne <= 1) { *out = kb; return DMF_OK; }
+  void* ob;
+  DMF_TRY(scratch(v, kScSort1, sizeof(unsigned long long) * ne, &ob));
+  int vbits = 1;
+  while ((1ull << vbits) < (unsigned long long)ncell) ++vbits;
+  size_t bytes = 0;
+  DMF_HIP(rocprim::radix_sort_keys(nullptr, bytes, kb, (unsigned long long*)ob, ne, 0, 32 + vbits, v->stream));
+  void* tmp;
+  DMF_TRY(scratch(v, kScTmp, bytes, &tmp));
+  DMF_HIP(rocprim::radix_sort_keys(tmp, bytes, kb, (unsigned long long*)ob, ne, 0, 32 + vbits, v->stream));
+  *out = (unsigned long long*)ob;
+  return DMF_OK;
+}
+
+// Reorganized grid (F, occ) of downloadReorganizedCloud(clean); see the kernels above.
+static int og_reorganize(dmf_ogrid* g, int clean, OgS** F_out, uint8_t** occ_out, int* rounds_out) {
+  dmf_volume* v = g->ctx;
+  const int64_t n = (int64_t)g->ncell;
+  const OGeom og = og_geom(g);
+  const dim3 grd((unsigned)((n + 255) / 256)), blk(256);
+  void *p0, *p1, *pf, *po, *kb, *cnt;
+  DMF_TRY(scratch(v, kScOgP0, sizeof(OgS) * n, &p0));
+  DMF_TRY(scratch(v, kScOgP1, sizeof(OgS) * n, &p1));
+  DMF_TRY(scratch(v, kScOgFinal, sizeof(OgS) * n, &pf));
+  DMF_TRY(scratch(v, kScOgOcc, (size_t)n + 8, &po));
+  DMF_TRY(scratch(v, kScSort0, sizeof(unsigned long long) * n, &kb));
+  DMF_TRY(scratch(v, kScCount, 64, &cnt));
+  OgS* init = (OgS*)pf;  // the initial state (stage 1 copy), kept until the final fold
+  OgS* cur = (OgS*)p0;
+  OgS* nxt = (OgS*)p1;
+  uint8_t* occ = (uint8_t*)po;
+  unsigned int* changed = (unsigned int*)((char*)cnt + 8);
+  hipLaunchKernelGGL(k_og_reorg_seed, grd, blk, 0, v->stream, n, g->d_normal, g->d_centroid, g->d_count, init);
+  DMF_LAUNCH_CHECK();
+  DMF_HIP(hipMemcpyAsync(cur, init, sizeof(OgS) * n, hipMemcpyDeviceToDevice, v->stream));
+  constexpr int kMaxRounds = 64;
+  unsigned long long* keys = nullptr;
+  unsigned long long ne = 0;
+  int r = 0;
+  bool settled = false;
+  for (; r < kMaxRounds && !settled; ++r) {
+    DMF_HIP(hipMemsetAsync(cnt, 0, 16, v->stream));
+    hipLaunchKernelGGL(k_og_reorg_keys, grd, blk, 0, v->stream, og, n, g->d_flags, cur, clean,
+                       (unsigned long long*)kb, (unsigned long long*)cnt);
+    DMF_LAUNCH_CHECK();
+    DMF_HIP(hipMemcpyAsync(&ne, cnt, 8, hipMemcpyDeviceToHost, v->stream));
+    DMF_HIP(hipStreamSynchronize(v->stream));
+    DMF_TRY(og_sort_keys(v, (unsigned long long*)kb, (size_t)ne, (size_t)n, &keys));
+    DMF_HIP(hipMemcpyAsync(nxt, init, sizeof(OgS) * n, hipMemcpyDeviceToDevice, v->stream));
+    if (ne)
+      hipLaunchKernelGGL(k_og_reorg_fold<0>, dim3((unsigned)((ne + 255) / 256)), blk, 0, v->stream, keys,
+                         (int64_t)ne, init, cur, nxt, occ);
+    DMF_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_og_reorg_diff, grd, blk, 0, v->stream, n, cur, nxt, changed);
+    DMF_LAUNCH_CHECK();
+    unsigned int ch = 0;
+    DMF_HIP(hipMemcpyAsync(&ch, changed, 4, hipMemcpyDeviceToHost, v->stream));
+    DMF_HIP(hipStreamSynchronize(v->stream));
+    std::swap(cur, nxt);
+    settled = ch == 0;  // cur == previous estimate: the targets (keys) are those of cur too
+  }
+  DMF_HIP(hipMemsetAsync(occ, 0, (size_t)n, v->stream));
+  if (settled) {
+    // final fold of every source into its target, from the initial state
+    DMF_HIP(hipMemcpyAsync(nxt, init, sizeof(OgS) * n, hipMemcpyDeviceToDevice, v->stream));
+    if (ne)
+      hipLaunchKernelGGL(k_og_reorg_fold<1>, dim3((unsigned)((ne + 255) / 256)), blk, 0, v->stream, keys,
+                         (int64_t)ne, init, cur, nxt, occ);
+    DMF_LAUNCH_CHECK();
+    *F_out = nxt;
+  } else {
+    DMF_HIP(hipMemcpyAsync(nxt, init, sizeof(OgS) * n, hipMemcpyDeviceToDevice, v->stream));
+    hipLaunchKernelGGL(k_og_reorg_serial, dim3(1), dim3(64), 0, v->stream, og, n, g->d_flags, clean, nxt, occ);
+    DMF_LAUNCH_CHECK();
+    *F_out = nxt;
+  }
+  *occ_out = occ;
+  if (rounds_out) *rounds_out = settled ? r : -1;
   return DMF_OK;
 }
 
@@ -363,18 +569,41 @@ int dmf_ogrid_state(const dmf_ogrid* g, float* normal, float* centroid, int32_t*
   DMF_API_END
 }
 
+int dmf_ogrid_set_state(dmf_ogrid* g, const float* normal, const float* centroid, const int32_t* count,
+                        const uint8_t* flags) {
+  DMF_API_BEGIN
+  DMF_TRY(og_ready(g));
+  hipStream_t s = g->ctx->stream;
+  if (normal) DMF_HIP(hipMemcpyAsync(g->d_normal, normal, sizeof(float) * 3 * g->ncell, hipMemcpyHostToDevice, s));
+  if (centroid) DMF_HIP(hipMemcpyAsync(g->d_centroid, centroid, sizeof(float) * 3 * g->ncell, hipMemcpyHostToDevice, s));
+  if (count) DMF_HIP(hipMemcpyAsync(g->d_count, count, sizeof(int32_t) * g->ncell, hipMemcpyHostToDevice, s));
+  if (flags) DMF_HIP(hipMemcpyAsync(g->d_flags, flags, g->ncell, hipMemcpyHostToDevice, s));
+  DMF_HIP(hipStreamSynchronize(s));
+  return DMF_OK;
+  DMF_API_END
+}
+
 int dmf_ogrid_download(dmf_ogrid* g, int32_t mode, float* out, int64_t cap, int64_t* n) {
   DMF_API_BEGIN
   DMF_TRY(og_ready(g));
   if (!n || (cap > 0 && !out)) return fail(DMF_ERR_INVALID, "null argument");
-  if (mode != 0 && mode != 1) return fail(DMF_ERR_INVALID, "mode must be 0 (downloadCloud) or 1 (downloadHQCloud)");
+  if (mode < 0 || mode > 3)
+    return fail(DMF_ERR_INVALID, "mode must be 0 (downloadCloud), 1 (downloadHQCloud), 2/3 (downloadReorganizedCloud "
+                                 "clean=false/true)");
   dmf_volume* v = g->ctx;
   const int64_t nc = (int64_t)g->ncell;
   void *sel, *pos, *buf;
   DMF_TRY(scratch(v, kScOut0, sizeof(int32_t) * (nc + 1), &sel));
   DMF_TRY(scratch(v, kScOut1, sizeof(int32_t) * (nc + 1), &pos));
   const dim3 grd((unsigned)((nc + 255) / 256));
-  hipLaunchKernelGGL(k_og_select, grd, dim3(256), 0, v->stream, g->d_flags, g->d_count, nc, mode, (int32_t*)sel);
+  OgS* F = nullptr;
+  if (mode >= 2) {
+    uint8_t* occ;
+    DMF_TRY(og_reorganize(g, mode == 3, &F, &occ, nullptr));
+    hipLaunchKernelGGL(k_og_select_reorg, grd, dim3(256), 0, v->stream, occ, nc, (int32_t*)sel);
+  } else {
+    hipLaunchKernelGGL(k_og_select, grd, dim3(256), 0, v->stream, g->d_flags, g->d_count, nc, mode, (int32_t*)sel);
+  }
   DMF_LAUNCH_CHECK();
   DMF_HIP(hipMemsetAsync((int32_t*)sel + nc, 0, sizeof(int32_t), v->stream));
   DMF_TRY(exclusive_scan_i32(v, (const int32_t*)sel, (int32_t*)pos, (size_t)nc + 1));
@@ -385,8 +614,12 @@ int dmf_ogrid_download(dmf_ogrid* g, int32_t mode, float* out, int64_t cap, int6
   if (total > cap) return fail(DMF_ERR_CAPACITY, "download needs %d points, capacity %lld", total, (long long)cap);
   if (total == 0) return DMF_OK;
   DMF_TRY(scratch(v, kScOut2, sizeof(float) * 6 * (size_t)total, &buf));
-  hipLaunchKernelGGL(k_og_gather, grd, dim3(256), 0, v->stream, (const int32_t*)sel, (const int32_t*)pos, nc,
-                     g->d_centroid, g->d_normal, (float*)buf);
+  if (F)
+    hipLaunchKernelGGL(k_og_gather_state, grd, dim3(256), 0, v->stream, (const int32_t*)sel, (const int32_t*)pos, nc,
+                       (const OgS*)F, (float*)buf);
+  else
+    hipLaunchKernelGGL(k_og_gather, grd, dim3(256), 0, v->stream, (const int32_t*)sel, (const int32_t*)pos, nc,
+                       g->d_centroid, g->d_normal, (float*)buf);
   DMF_LAUNCH_CHECK();
   DMF_HIP(hipMemcpyAsync(out, buf, sizeof(float) * 6 * (size_t)total, hipMemcpyDeviceToHost, v->stream));
   DMF_HIP(hipStreamSynchronize(v->stream));

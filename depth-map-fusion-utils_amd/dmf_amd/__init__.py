@@ -280,6 +280,21 @@ def _pose(T):
     return a
 
 
+def _poses(T):
+    """A stack of poses -> (P, 12) float32: each pose 3x4 or 4x4 (Eigen::Affine3f rows),
+    a single pose, or already flattened rows of 12; anything else is rejected."""
+    a = np.asarray(T, np.float32)
+    if a.ndim == 2 and a.shape in ((3, 4), (4, 4)):
+        a = a[None]
+    if a.ndim == 3 and a.shape[1:] in ((3, 4), (4, 4)):
+        return np.ascontiguousarray(a[:, :3, :].reshape(-1, 12))
+    if a.ndim == 2 and a.shape[1] == 12:
+        return np.ascontiguousarray(a)
+    if a.ndim == 1 and a.size in (12, 16):
+        return _pose(a)[None]
+    raise ValueError(f"poses must be (P, 3, 4), (P, 4, 4) or (P, 12) floats, got shape {a.shape}")
+
+
 class FuseParams:
     def __new__(cls, **kw):
         return _lib.default_fuse_params(**kw)
@@ -401,8 +416,15 @@ class RayTracingEngine:
         depth = np.ascontiguousarray(depth, np.uint16)
         if depth.ndim == 2:
             depth = depth[None]
-        poses = np.ascontiguousarray(np.asarray(poses, np.float32).reshape(-1, 12))
+        poses = _poses(poses)
+        H, W = self.cam_.height_, self.cam_.width_
+        if depth.shape != (poses.shape[0], H, W):
+            raise ValueError(f"depth must be (P, H, W) = ({poses.shape[0]}, {H}, {W}) uint16, got {depth.shape}")
         n = int(np.prod(volume.dims))
+        for name, a in (("hits", hits), ("misses", misses)):
+            if a is not None and not (isinstance(a, np.ndarray) and a.dtype == np.int32 and a.size == n
+                                      and a.flags.c_contiguous):
+                raise ValueError(f"{name} must be a contiguous int32 array of {n} cells (accumulated in place)")
         hits = np.zeros(n, np.int32) if hits is None else hits
         misses = np.zeros(n, np.int32) if misses is None else misses
         stats = np.zeros(3, np.int64)
@@ -512,3 +534,19 @@ class OccupancyGrid:
     def downloadHQCloud(self):
         """as downloadCloud for voxels with count > 100 (:283-318)."""
         return self._download(1)
+
+    def downloadReorganizedCloud(self, clean=False):
+        """(n, 6) of the reorganized grid (:200-286): every occupied voxel (with clean,
+        count >= 100) merges into the voxel holding its centroid, in the single-threaded
+        x-major order; occupied reorganized voxels, x-major."""
+        return self._download(3 if clean else 2)
+
+    def set_state(self, normal, centroid, count, flags):
+        """Write the dense voxels_ fields (normal, centroid (n, 3) float; count int32;
+        flags occupied | normal_found << 1) — the reference's public state."""
+        n = int(np.prod(self.dims))
+        nrm = np.ascontiguousarray(normal, np.float32).reshape(3 * n)
+        cen = np.ascontiguousarray(centroid, np.float32).reshape(3 * n)
+        cnt = np.ascontiguousarray(count, np.int32).reshape(n)
+        fl = np.ascontiguousarray(flags, np.uint8).reshape(n)
+        check(self._L.dmf_ogrid_set_state(self._h, ptr(nrm), ptr(cen), ptr(cnt), ptr(fl)))

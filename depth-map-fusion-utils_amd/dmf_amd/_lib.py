@@ -107,6 +107,16 @@ SIGNATURES = {
     "dmf_fuse_finalize_device": (C.c_int, [_vp, _p, _p, _p, _p]),
     "dmf_fuse_counter_cells": (C.c_int, [_vp, _p]),
     "dmf_fuse_counters_to_linear_device": (C.c_int, [_vp, _p, _p]),
+    "dmf_fuse_reserve": (C.c_int, [_vp, _p, _i32, C.c_uint64]),
+    "dmf_rccl_version": (C.c_int, [_p]),
+    "dmf_comm_unique_id": (C.c_int, [_p]),
+    "dmf_comm_init_rank": (C.c_int, [_p, _i32, _p, _i32, _i32]),
+    "dmf_comm_destroy": (C.c_int, [_vp]),
+    "dmf_fuse_counter_cells_padded": (C.c_int, [_vp, _i32, _p]),
+    "dmf_fuse_logodds_cells_padded": (C.c_int, [_vp, _i32, _p]),
+    "dmf_fuse_allreduce_device": (C.c_int, [_vp, _p, _i64, _vp, _vp]),
+    "dmf_fuse_merge_finalize_device": (C.c_int, [_vp, _p, _p, _p, _vp, _vp]),
+    "dmf_flags_allreduce": (C.c_int, [_vp, _vp, _vp]),
     "dmf_ogrid_create": (C.c_int, [_p, _i32]),
     "dmf_ogrid_destroy": (C.c_int, [_vp]),
     "dmf_ogrid_set_stream": (C.c_int, [_vp, _vp]),
@@ -116,6 +126,7 @@ SIGNATURES = {
     "dmf_ogrid_update_states_device": (C.c_int, [_vp, _p, _i64, _p, _i64]),
     "dmf_ogrid_state": (C.c_int, [_vp, _p, _p, _p, _p]),
     "dmf_ogrid_download": (C.c_int, [_vp, _i32, _p, _i64, _p]),
+    "dmf_ogrid_set_state": (C.c_int, [_vp, _p, _p, _p, _p]),
     "dmf_device_malloc": (C.c_int, [_vp, _p, C.c_size_t]),
     "dmf_device_free": (C.c_int, [_vp, _vp]),
     "dmf_memcpy_h2d": (C.c_int, [_vp, _vp, _p, C.c_size_t]),

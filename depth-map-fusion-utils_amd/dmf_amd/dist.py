@@ -78,3 +78,121 @@ def sharded_visibility(compute, poses, world, rank, group=None):
     a, b = shard_range(len(poses), world, rank)
     found, lists = compute(poses[a:b]) if b > a else ([], [])
     return gather_pose_lists(found, lists, group)
+
+
+# ---- merge + finalize (reduce-scatter / slab finalize / all-gather), DESIGN.md §7 ------
+# The fusion counters are tiled (2x2x4-cell tiles of 16 int32, tiles x-major; DESIGN.md
+# §6), so a contiguous range of whole tile rows (tx) is an x slab of the grid.  The
+# counter arrays are padded to world * rows_per_rank tile rows; rank r reduces and
+# finalizes rows [r*rows, (r+1)*rows) and the int16 slabs are all-gathered.  This moves
+# 2*4 B (hits, misses) + 2 B (log-odds) per cell instead of the all-reduce's 2*2*4 B.
+# The GPU path is libdmf's dmf_fuse_merge_finalize_device over an RCCL communicator; the
+# numpy/gloo functions below restate the same partition for CPU tests.
+
+def tile_rows(dims):
+    """(ntx, tiles per row) of the tiled counter layout of a grid (nx, ny, nz)."""
+    nx, ny, nz = dims
+    return (nx + 1) // 2, ((ny + 1) // 2) * ((nz + 3) // 4)
+
+
+def rows_per_rank(dims, world):
+    ntx, _ = tile_rows(dims)
+    return -(-ntx // world)
+
+
+def padded_counter_cells(dims, world):
+    """= dmf_fuse_counter_cells_padded: elements per tiled counter array."""
+    _, tpr = tile_rows(dims)
+    return rows_per_rank(dims, world) * world * tpr * 16
+
+
+def padded_logodds_cells(dims, world):
+    """= dmf_fuse_logodds_cells_padded."""
+    return rows_per_rank(dims, world) * world * 2 * dims[1] * dims[2]
+
+
+def to_tiled(lin, dims, n_pad):
+    """x-major int32 counters -> the tiled layout, zero-padded to n_pad elements."""
+    import numpy as np
+    nx, ny, nz = dims
+    px, py, pz = -(-nx // 2) * 2, -(-ny // 2) * 2, -(-nz // 4) * 4
+    g = np.zeros((px, py, pz), np.int32)
+    g[:nx, :ny, :nz] = np.asarray(lin, np.int32).reshape(nx, ny, nz)
+    # (tx, xi, ty, yi, tz, zi) -> (tx, ty, tz, xi, yi, zi)
+    t = g.reshape(px // 2, 2, py // 2, 2, pz // 4, 4).transpose(0, 2, 4, 1, 3, 5).reshape(-1)
+    out = np.zeros(n_pad, np.int32)
+    out[: t.size] = t
+    return out
+
+
+def finalize_tiles_np(hits_t, miss_t, dims, l_hit, l_miss, l_min, l_max, out, t0, t1):
+    """k_finalize over tiles [t0, t1) in numpy: writes out[x, y, z] (x-major int16)."""
+    import numpy as np
+    nx, ny, nz = dims
+    nty, ntz = (ny + 1) // 2, (nz + 3) // 4
+    for t in range(t0, t1):
+        tz, r = t % ntz, t // ntz
+        ty, tx = r % nty, r // nty
+        h = hits_t[16 * t: 16 * t + 16].astype(np.int64).reshape(2, 2, 4)
+        m = miss_t[16 * t: 16 * t + 16].astype(np.int64).reshape(2, 2, 4)
+        L = np.clip(h * l_hit + m * l_miss, l_min, l_max).astype(np.int16)
+        for xi in range(2):
+            for yi in range(2):
+                x, y = 2 * tx + xi, 2 * ty + yi
+                if x < nx and y < ny:
+                    z0 = 4 * tz
+                    k = min(4, nz - z0)
+                    out[(x * ny + y) * nz + z0: (x * ny + y) * nz + z0 + k] = L[xi, yi, :k]
+
+
+def merge_finalize_gloo(counters, dims, prm, logodds, group=None):
+    """CPU restatement of dmf_fuse_merge_finalize_device over a torch.distributed group:
+    counters = torch int32 [hits | misses] tiled, each padded_counter_cells(dims, world);
+    logodds = torch int16 of padded_logodds_cells(dims, world), filled on every rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    ntx, tpr = tile_rows(dims)
+    rows = rows_per_rank(dims, world)
+    n_pad = rows * world * tpr * 16
+    chunk = rows * tpr * 16
+    hits, miss = counters[:n_pad], counters[n_pad: 2 * n_pad]
+    for arr in (hits, miss):
+        part = torch.empty(chunk, dtype=torch.int32)
+        if world > 1:
+            dist.reduce_scatter_tensor(part, arr, group=group)
+        else:
+            part.copy_(arr[:chunk])
+        arr[rank * chunk: (rank + 1) * chunk] = part
+    r0, r1 = min(ntx, rank * rows), min(ntx, (rank + 1) * rows)
+    out = logodds.numpy()
+    finalize_tiles_np(hits.numpy(), miss.numpy(), dims, prm["l_hit"], prm["l_miss"], prm["l_min"], prm["l_max"],
+                      out, r0 * tpr, r1 * tpr)
+    slab = rows * 2 * dims[1] * dims[2]
+    if world > 1:
+        mine = logodds[rank * slab: (rank + 1) * slab].clone().view(torch.uint8)
+        allb = torch.empty(world * slab * 2, dtype=torch.uint8)
+        dist.all_gather_into_tensor(allb, mine, group=group)
+        logodds.copy_(allb.view(torch.int16))
+    return logodds
+
+
+def merge_finalize_device(vol, counters, prm_ptr, logodds, comm_ptr, stream_ptr=None):
+    """GPU: libdmf's dmf_fuse_merge_finalize_device over an RCCL communicator (e.g. torch's
+    ProcessGroupNCCL._comm_ptr()) on stream_ptr (None = the volume's stream)."""
+    from . import _lib
+    _lib.check(vol._L.dmf_fuse_merge_finalize_device(vol._h, counters.data_ptr(), prm_ptr, logodds.data_ptr(),
+                                                     comm_ptr, stream_ptr))
+
+
+def torch_comm_ptr(group=None, device=None):
+    """ncclComm_t of torch's NCCL(=RCCL) process group, as an int (connects it eagerly)."""
+    import torch
+    import torch.distributed as dist
+    pg = group or dist.distributed_c10d._get_default_group()
+    be = pg._get_backend(device or torch.device("cuda", torch.cuda.current_device()))
+    ptr = int(be._comm_ptr())
+    if ptr == 0:
+        raise RuntimeError("RCCL communicator not initialised (run a collective or eager_connect first)")
+    return ptr

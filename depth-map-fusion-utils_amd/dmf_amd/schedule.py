@@ -1,0 +1,121 @@
+"""The per-step fusion schedule of the pose-sharded engine, written once
+against a small stream runtime so the same code drives the GPU (torch/HIP streams and
+events) and a CPU simulator that executes the enqueued work in random stream-consistent
+orders (gloo collectives inside).
+
+One step on one rank:
+  compute lane:  [wait until buffer b's previous merge is done] clear(b) -> fuse(b, i)
+  comm lane:     [wait fuse(b, i)] merge(b, i)   (reduce-scatter + slab finalize +
+                                                  all-gather, or all-reduce + finalize)
+Counters are multi-buffered, so the merge of step i overlaps the fusion of step i+1; the
+last merge is waited for before the schedule returns (it is inside the timed region).
+"""
+from __future__ import annotations
+
+import random
+
+
+class TorchRuntime:
+    """HIP streams via torch: enqueue() calls the function on the host with the lane's
+    stream current, so the native calls it makes go to that stream (they take their
+    stream from the volume: the caller's `bind(lane)` hook sets it)."""
+
+    def __init__(self, device, bind=None):
+        import torch
+        self.torch = torch
+        self.device = device
+        self.bind = bind
+        self.lanes = {"compute": torch.cuda.current_stream(device), "comm": torch.cuda.Stream(device)}
+
+    def enqueue(self, lane, fn):
+        s = self.lanes[lane]
+        with self.torch.cuda.stream(s):
+            if self.bind is not None:
+                self.bind(s)
+            fn()
+
+    def record(self, lane):
+        e = self.torch.cuda.Event()
+        e.record(self.lanes[lane])
+        return e
+
+    def wait(self, lane, event):
+        self.lanes[lane].wait_event(event)
+
+    def drain(self):
+        if self.bind is not None:
+            self.bind(self.lanes["compute"])
+
+
+class _SimEvent:
+    __slots__ = ("done",)
+
+    def __init__(self):
+        self.done = False
+
+
+class SimRuntime:
+    """CPU stand-in for streams: each lane is a FIFO of work; drain() runs, at random,
+    any lane whose head is ready (an event wait is ready once the event's record ran).
+    A schedule that forgets a wait computes wrong results under some orders."""
+
+    def __init__(self, seed=0):
+        self.rng = random.Random(seed)
+        self.q = {"compute": [], "comm": []}
+
+    def enqueue(self, lane, fn):
+        self.q[lane].append(("run", fn))
+
+    def record(self, lane):
+        e = _SimEvent()
+        self.q[lane].append(("record", e))
+        return e
+
+    def wait(self, lane, event):
+        self.q[lane].append(("wait", event))
+
+    def drain(self):
+        while any(self.q.values()):
+            ready = [k for k, v in self.q.items() if v and (v[0][0] != "wait" or v[0][1].done)]
+            if not ready:
+                raise RuntimeError("schedule deadlock: every lane waits on an unrecorded event")
+            lane = self.rng.choice(ready)
+            kind, arg = self.q[lane].pop(0)
+            if kind == "run":
+                arg()
+            elif kind == "record":
+                arg.done = True
+
+
+def run_steps(rt, nsteps, nbuf, clear, fuse, merge, marks=None, reuse_wait=True):
+    """Enqueue `nsteps` steps on runtime `rt` and wait for the last merge.
+
+    clear(b), fuse(b, i), merge(b, i) enqueue (or, on the simulator, perform) the work of
+    step i on counter buffer b = i % nbuf.  marks(i, name, lane), if given, is called at
+    the step's phase boundaries (c0, c1, c2 on compute; a0, a1 on comm) for timing.
+    reuse_wait=False drops the buffer-reuse dependency (tests show it is needed)."""
+    merged = [None] * nbuf
+    last = None
+    for i in range(nsteps):
+        b = i % nbuf
+        if reuse_wait and merged[b] is not None:
+            rt.wait("compute", merged[b])
+        if marks:
+            marks(i, "c0", "compute")
+        rt.enqueue("compute", lambda b=b: clear(b))
+        if marks:
+            marks(i, "c1", "compute")
+        rt.enqueue("compute", lambda b=b, i=i: fuse(b, i))
+        if marks:
+            marks(i, "c2", "compute")
+        fused = rt.record("compute")
+        rt.wait("comm", fused)
+        if marks:
+            marks(i, "a0", "comm")
+        rt.enqueue("comm", lambda b=b, i=i: merge(b, i))
+        if marks:
+            marks(i, "a1", "comm")
+        merged[b] = last = rt.record("comm")
+    if last is not None:
+        rt.wait("compute", last)
+    rt.drain()

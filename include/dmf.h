@@ -100,8 +100,8 @@ const char* dmf_fuse_kernel(void);
  * when the longest grid axis has 384..1024 cells, k_fuse_l<12, 1280> otherwise; 40 = the
  * brick pipeline whenever it applies (<= 1024 cells per axis); 41-43 = its refill
  * variants; 1 = one device atomic per update; 24, 30-33 = LDS-box kernels (k_fuse_r /
- * k_fuse_l).  Grids over 1024 cells per axis always use k_fuse_l<12, 1280>.  Results are identical for every variant.  The brick pipeline
- * synchronises the volume's stream once per batch (it sizes the pair lists on the host). */
+ * k_fuse_l).  Grids over 1024 cells per axis always use k_fuse_l<12, 1280>.  Results are
+ * identical for every variant. */
 int dmf_fuse_set_variant(int32_t variant);
 
 /* ---- VoxelVolume  (Volume.hpp:50-255) ------------------------------------ */
@@ -109,7 +109,9 @@ int dmf_fuse_set_variant(int32_t variant);
 int dmf_volume_create(dmf_volume** out, int32_t device);
 /* VoxelVolume::~VoxelVolume()  Volume.hpp:80-87 */
 int dmf_volume_destroy(dmf_volume* v);
-/* All work of this handle is enqueued on `stream` (hipStream_t; NULL = default). */
+/* All work of this handle is enqueued on `stream` (hipStream_t; NULL = default).  The
+ * switch does not block the host: the new stream waits for the work already enqueued on
+ * the old one (skipped when either stream is capturing a graph). */
 int dmf_volume_set_stream(dmf_volume* v, void* hip_stream);
 int dmf_volume_synchronize(dmf_volume* v);
 /* setDimensions  Volume.hpp:89-100 */
@@ -233,6 +235,12 @@ int dmf_fuse_depth(dmf_volume* v, const dmf_camera* cam, const uint16_t* depth, 
 int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth,
                           const float* d_poses, int32_t P, const dmf_fuse_params* prm, int32_t* d_hits,
                           int32_t* d_misses, uint64_t* d_stats);
+/* Pre-allocate the fusion scratch for calls of up to P frames of `cam`'s size on this
+ * volume, so that dmf_fuse_depth_device then neither allocates nor synchronises (e.g. for
+ * hipGraph capture).  The brick pipeline sizes its (ray, brick) pair lists by a geometric
+ * bound and splits larger calls into pose batches that fit max_scratch_bytes (0 = keep the
+ * current budget; default 48 GiB).  Synchronises the stream once. */
+int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t max_scratch_bytes);
 /* Elements of one tiled counter array (>= xdim*ydim*zdim: dims padded to 2, 2, 4). */
 int dmf_fuse_counter_cells(const dmf_volume* v, int64_t* n);
 /* Tiled counters -> x-major int32 (xdim*ydim*zdim). */
@@ -243,6 +251,36 @@ int dmf_fuse_finalize(dmf_volume* v, const int32_t* hits, const int32_t* misses,
                       int16_t* logodds);
 int dmf_fuse_finalize_device(dmf_volume* v, const int32_t* d_hits, const int32_t* d_misses,
                              const dmf_fuse_params* prm, int16_t* d_logodds);
+
+/* ---- multi-GPU merge over RCCL ------------------------
+ * Poses shard across ranks, each rank fuses into its own replica of the counters, and
+ * the replicas merge with integer collectives (bit-identical to one rank fusing all
+ * poses).  `comm` is an ncclComm_t (RCCL) as void*: torch's ProcessGroupNCCL._comm_ptr()
+ * or one made with dmf_comm_init_rank.  Collectives (and the slab finalize) run on
+ * `stream` (hipStream_t; NULL = the volume's stream), e.g. a communication stream that
+ * overlaps the next fusion call on the volume's stream. */
+#define DMF_COMM_ID_BYTES 128
+int dmf_rccl_version(int32_t* version);
+/* ncclGetUniqueId into id[DMF_COMM_ID_BYTES] (rank 0; share it with the other ranks). */
+int dmf_comm_unique_id(void* id);
+int dmf_comm_init_rank(void** comm, int32_t nranks, const void* id, int32_t rank, int32_t device);
+int dmf_comm_destroy(void* comm);
+/* Tiled counter elements per array padded to whole tile rows per rank (>= the unpadded
+ * dmf_fuse_counter_cells), and the padded int16 log-odds grid (>= xdim*ydim*zdim) used by
+ * dmf_fuse_merge_finalize_device.  Counters = [hits | misses], each n_padded elements. */
+int dmf_fuse_counter_cells_padded(const dmf_volume* v, int32_t nranks, int64_t* n_padded);
+int dmf_fuse_logodds_cells_padded(const dmf_volume* v, int32_t nranks, int64_t* n_padded);
+/* In-place all-reduce(sum) of [hits | misses] (2*n_per_array int32). */
+int dmf_fuse_allreduce_device(dmf_volume* v, int32_t* d_counters, int64_t n_per_array, void* comm, void* stream);
+/* Merge + finalize: reduce-scatter(sum) of hits and of misses over whole tile rows, this
+ * rank finalizes its slab, all-gather of the int16 slabs: every rank ends with the full
+ * log-odds grid in d_logodds (x-major; the first xdim*ydim*zdim of the padded buffer).
+ * d_counters: padded [hits | misses]; afterwards only this rank's slab holds sums. */
+int dmf_fuse_merge_finalize_device(dmf_volume* v, int32_t* d_counters, const dmf_fuse_params* prm,
+                                   int16_t* d_logodds, void* comm, void* stream);
+/* Voxel::view / Voxel::good of the replicated occupied list: all-reduce(max) (the
+ * reverse/forward queries of a pose shard set flags idempotently). */
+int dmf_flags_allreduce(dmf_volume* v, void* comm, void* stream);
 
 /* ---- OccupancyGrid  (include/OccupancyGrid.hpp:50-318) ----------------------- */
 /* The reference's second fusion path.  updateStates is computed in the deterministic
@@ -264,8 +302,15 @@ int dmf_ogrid_update_states_device(dmf_ogrid* g, const float* d_cloud, int64_t n
 /* Dense state copies (any may be NULL): normal / centroid 3 floats per voxel, count,
  * flags (bit 0 occupied, bit 1 normal_found). */
 int dmf_ogrid_state(const dmf_ogrid* g, float* normal, float* centroid, int32_t* count, uint8_t* flags);
+/* Write the dense state (the reference's public voxels_ fields; any may be NULL). */
+int dmf_ogrid_set_state(dmf_ogrid* g, const float* normal, const float* centroid, const int32_t* count,
+                        const uint8_t* flags);
 /* mode 0 downloadCloud (:166-193), 1 downloadHQCloud (count > 100, :283-318): occupied
- * voxels in x-major order as (cx, cy, cz, nx, ny, nz).  DMF_ERR_CAPACITY (n set) if n > cap. */
+ * voxels in x-major order as (cx, cy, cz, nx, ny, nz).  Modes 2 / 3 downloadReorganizedCloud
+ * (:200-286) with clean = false / true: every occupied voxel (clean: count >= 100 at its
+ * turn) merges into the voxel holding its centroid, in the single-threaded x-major order
+ * the reference's OpenMP loop races over; the merged voxels, x-major.  DMF_ERR_CAPACITY
+ * (n set) if n > cap. */
 int dmf_ogrid_download(dmf_ogrid* g, int32_t mode, float* out, int64_t cap, int64_t* n);
 
 /* ---- device memory helpers for callers without their own allocator ---------- */

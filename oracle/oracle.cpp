@@ -1056,6 +1056,67 @@ int64_t orc_ogrid_download(const orc_ogrid* g, int mode, float* out, int64_t cap
   return n;
 }
 
+// Dense state upload (the reference's voxels_ fields are public; callers may write them).
+void orc_ogrid_set_state(orc_ogrid* g, const float* normal, const float* centroid, const int32_t* count,
+                         const uint8_t* flags) {
+  const size_t n = g->count.size();
+  std::memcpy(g->normal.data(), normal, sizeof(float) * 3 * n);
+  std::memcpy(g->centroid.data(), centroid, sizeof(float) * 3 * n);
+  std::memcpy(g->count.data(), count, sizeof(int32_t) * n);
+  for (size_t i = 0; i < n; ++i) {
+    g->occupied[i] = flags[i] & 1;
+    g->normal_found[i] = (flags[i] >> 1) & 1;
+  }
+}
+
+// :200-286 downloadReorganizedCloud(cloud, clean), in the single-threaded order its
+// OpenMP loops race over.  Stage 1 copies normal / centroid / count / normal_found into
+// voxels_reorganized_ (occupied stays false).  Stage 2, x-major: every voxel occupied in
+// voxels_ (and, with clean, whose reorganized count is >= 100 at its turn) merges its
+// CURRENT reorganized state into the reorganized voxel holding its centroid (the same
+// object when that is itself: n + n, (c + c) / 2).  Stage 3 emits the reorganized voxels
+// marked occupied, x-major, as (cx, cy, cz, nx, ny, nz).  Returns the count (writes <= cap).
+int64_t orc_ogrid_download_reorganized(const orc_ogrid* g, int clean, float* out, int64_t cap) {
+  const size_t n = g->count.size();
+  std::vector<float> nr(g->normal), cr(g->centroid);
+  std::vector<int32_t> kr(g->count);
+  std::vector<uint8_t> occ(n, 0);
+  for (int x = 0; x < g->xdim_; ++x)
+    for (int y = 0; y < g->ydim_; ++y)
+      for (int z = 0; z < g->zdim_; ++z) {
+        const size_t s = g->idx(x, y, z);
+        if (!g->occupied[s]) continue;
+        if (clean && kr[s] < 100) continue;
+        // getVoxelCoords(Vector3f) (:373-379): floor of the double quotient, int via cvttsd2si
+        const float c[3] = {cr[3 * s], cr[3 * s + 1], cr[3 * s + 2]};
+        const double q[3] = {std::floor(((double)c[0] - g->xmin_) / g->xres_),
+                             std::floor(((double)c[1] - g->ymin_) / g->yres_),
+                             std::floor(((double)c[2] - g->zmin_) / g->zres_)};
+        int t[3];
+        for (int a = 0; a < 3; ++a) t[a] = (q[a] >= -2147483648.0 && q[a] < 2147483648.0) ? (int)q[a] : INT32_MIN;
+        if (!g->valid_coords(t[0], t[1], t[2])) continue;
+        const size_t d = g->idx(t[0], t[1], t[2]);
+        const float sn[3] = {nr[3 * s], nr[3 * s + 1], nr[3 * s + 2]};  // source state (read first: may alias d)
+        occ[d] = 1;
+        const float sum[3] = {nr[3 * d] + sn[0], nr[3 * d + 1] + sn[1], nr[3 * d + 2] + sn[2]};
+        normalized(sum, &nr[3 * d]);
+        if (kr[d] == 0) {
+          for (int a = 0; a < 3; ++a) cr[3 * d + a] = c[a];
+        } else {
+          for (int a = 0; a < 3; ++a) cr[3 * d + a] = (cr[3 * d + a] + c[a]) / 2.0f;
+          ++kr[d];
+        }
+      }
+  int64_t m = 0;
+  for (size_t v = 0; v < n; ++v) {
+    if (!occ[v]) continue;
+    if (m < cap)
+      for (int a = 0; a < 3; ++a) { out[6 * m + a] = cr[3 * v + a]; out[6 * m + 3 + a] = nr[3 * v + a]; }
+    ++m;
+  }
+  return m;
+}
+
 // Clamped fixed-point log-odds (milli-logit units) from the exact counts.
 void orc_fuse_finalize(int64_t n, const int32_t* hits, const int32_t* misses, int l_hit, int l_miss,
                        int l_min, int l_max, int16_t* out) {

@@ -390,7 +390,9 @@ class OccupancyGrid:
                                 ("orc_ogrid_dims", None, [_vp, _i32p]),
                                 ("orc_ogrid_update", None, [_vp, _f32p, C.c_int64, _f32p, C.c_int64]),
                                 ("orc_ogrid_state", None, [_vp, _f32p, _f32p, _i32p, _u8p]),
-                                ("orc_ogrid_download", C.c_int64, [_vp, C.c_int, _f32p, C.c_int64])):
+                                ("orc_ogrid_download", C.c_int64, [_vp, C.c_int, _f32p, C.c_int64]),
+                                ("orc_ogrid_set_state", None, [_vp, _f32p, _f32p, _i32p, _u8p]),
+                                ("orc_ogrid_download_reorganized", C.c_int64, [_vp, C.c_int, _f32p, C.c_int64])):
             fn = getattr(L, name)
             fn.restype, fn.argtypes = res, args
         self._L = L
@@ -440,4 +442,20 @@ class OccupancyGrid:
         n = self._L.orc_ogrid_download(self._h, mode, np.zeros(6, np.float32), 0)
         out = np.zeros(6 * max(n, 1), np.float32)
         self._L.orc_ogrid_download(self._h, mode, out, n)
+        return out[:6 * n].reshape(-1, 6)
+
+    def set_state(self, normal, centroid, count, flags):
+        """Write the dense voxels_ fields (normal, centroid: (n, 3) float; count int32;
+        flags: occupied | normal_found << 1)."""
+        n = int(np.prod(self.dims))
+        self._L.orc_ogrid_set_state(self._h, np.ascontiguousarray(normal, np.float32).reshape(3 * n),
+                                    np.ascontiguousarray(centroid, np.float32).reshape(3 * n),
+                                    np.ascontiguousarray(count, np.int32).reshape(n),
+                                    np.ascontiguousarray(flags, np.uint8).reshape(n))
+
+    def downloadReorganizedCloud(self, clean=False):
+        """OccupancyGrid.hpp:200-286, single-threaded order."""
+        n = self._L.orc_ogrid_download_reorganized(self._h, int(bool(clean)), np.zeros(6, np.float32), 0)
+        out = np.zeros(6 * max(n, 1), np.float32)
+        self._L.orc_ogrid_download_reorganized(self._h, int(bool(clean)), out, n)
         return out[:6 * n].reshape(-1, 6)

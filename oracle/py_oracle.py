@@ -262,3 +262,43 @@ def collision_cost_map(vol, centres):
                 d = [f32(f32(centres[i][k]) - f32(centres[j][k])) for k in range(3)]
                 out[i, j] = int(f64(f32(math.sqrt(s3(f32(d[0] * d[0]), f32(d[1] * d[1]), f32(d[2] * d[2]))))) * 1000)
     return out
+
+
+def reorganized_cloud(dims, mins, res, normal, centroid, count, flags, clean):
+    """OccupancyGrid.hpp:200-286 downloadReorganizedCloud restated with Python lists and
+    float32 scalars (independent of oracle.cpp): x-major single-threaded order."""
+    nx, ny, nz = dims
+    N = nx * ny * nz
+    nr = [[f32(v) for v in normal[i]] for i in range(N)]
+    cr = [[f32(v) for v in centroid[i]] for i in range(N)]
+    kr = [int(c) for c in count]
+    occ = [False] * N
+    for s in range(N):
+        if not (int(flags[s]) & 1):
+            continue
+        if clean and kr[s] < 100:
+            continue
+        c = list(cr[s])
+        t = []
+        for a in range(3):
+            q = np.floor((np.float64(c[a]) - np.float64(mins[a])) / np.float64(res[a]))
+            t.append(int(q) if (np.isfinite(q) and -2147483648.0 <= q < 2147483648.0) else -2147483648)
+        if not all(0 <= t[a] < dims[a] for a in range(3)):
+            continue
+        d = (t[0] * ny + t[1]) * nz + t[2]
+        sn = list(nr[s])
+        occ[d] = True
+        sm = [nr[d][a] + sn[a] for a in range(3)]
+        q2 = s3(sm[0] * sm[0], sm[1] * sm[1], sm[2] * sm[2])
+        if q2 > f32(0):
+            rt = f32(np.sqrt(q2))
+            nr[d] = [sm[a] / rt for a in range(3)]
+        else:
+            nr[d] = sm
+        if kr[d] == 0:
+            cr[d] = c
+        else:
+            cr[d] = [(cr[d][a] + c[a]) / f32(2) for a in range(3)]
+            kr[d] += 1
+    out = [cr[v] + nr[v] for v in range(N) if occ[v]]
+    return np.array(out, np.float32).reshape(-1, 6)

@@ -1,0 +1,186 @@
+"""GPU: the C-ABI contract of the fusion path beyond parity.
+
+* dmf_fuse_depth_device only enqueues work (include/dmf.h): after dmf_fuse_reserve a
+  fusion call issued behind a long spin kernel returns while its stream is still busy
+  (no host synchronisation, no allocation), and the counters equal the oracle's.
+* The multi-GPU merge entry points (dmf_fuse_allreduce_device,
+  dmf_fuse_merge_finalize_device, dmf_flags_allreduce) over an RCCL communicator made by
+  libdmf itself (dmf_comm_init_rank) and over torch's ProcessGroupNCCL communicator, at
+  world size 1 (one GPU per box): merged log-odds equal the plain finalize; the world-2
+  partition and schedule are covered on CPU by tests/test_dist.py.
+"""
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import helpers as Hh
+from helpers import K
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(n=96, P=4):
+    import torch
+    import dmf_amd
+    from dmf_amd import _lib
+    L = _lib.load()
+    poses, depth, _ = Hh.frames()
+    poses = np.ascontiguousarray(poses[:P], np.float32)
+    depth = np.ascontiguousarray(depth[:P], np.uint16)
+    vol = dmf_amd.VoxelVolume()
+    vol.setDimensions(*Hh.BOUNDS)
+    vol.setVolumeSize(n, n, n)
+    vol.constructVolume()
+    dev = torch.device("cuda", 0)
+    d_depth = torch.from_numpy(depth.view(np.int16)).to(dev)
+    d_poses = torch.from_numpy(poses).to(dev)
+    cam = _lib.make_camera(K, 480, 640)
+    prm = _lib.default_fuse_params(dmin_mm=200, dmax_mm=1000)
+    return torch, L, _lib, vol, dev, d_depth, d_poses, cam, prm, poses, depth
+
+
+def _oracle_counts(oracle, depth, poses, n):
+    ov = Hh.oracle_volume(oracle, n=n, clouds=[])
+    return oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
+
+
+@pytest.mark.parametrize("n,variant", [(96, 40), (96, 31)])
+def test_fuse_device_never_blocks_the_host(oracle, n, variant):
+    """dmf_fuse_depth_device only enqueues (include/dmf.h; brick pipeline and the LDS-box
+    kernel): with its stream held busy by a ~1 s spin kernel, the call returns while the
+    stream is still busy (a host synchronisation inside would wait for the spin), and the
+    counters then equal the oracle's.  A second call needs no new allocation either
+    (dmf_fuse_reserve sized everything)."""
+    import time
+    torch, L, _lib, vol, dev, d_depth, d_poses, cam, prm, poses, depth = _setup(n)
+    P = poses.shape[0]
+    nct = C.c_int64()
+    _lib.check(L.dmf_fuse_counter_cells(vol._h, C.addressof(nct)))
+    nt = nct.value
+    counters = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
+    lin = torch.empty(n ** 3, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    vol.set_stream(s.cuda_stream)
+    _lib.check(L.dmf_fuse_set_variant(variant))
+    try:
+        _lib.check(L.dmf_fuse_reserve(vol._h, C.addressof(cam), P, 0))
+
+        def fuse():
+            _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(), P,
+                                               C.addressof(prm), counters.data_ptr(), counters.data_ptr() + 4 * nt,
+                                               None))
+        fuse()  # first call: module loads
+        torch.cuda.synchronize(dev)
+        counters.zero_()
+        for _ in range(2):
+            torch.cuda._sleep(2_000_000_000)  # ~1 s of spinning at 2.1-2.4 GHz on the stream
+            t0 = time.perf_counter()
+            fuse()
+            dt = time.perf_counter() - t0
+            busy = not s.query()
+            torch.cuda.synchronize(dev)
+            assert busy and dt < 0.3, (busy, dt)
+        ho, mo, _ = _oracle_counts(oracle, depth, poses, n)
+        for half, exp in ((0, ho), (1, mo)):
+            _lib.check(L.dmf_fuse_counters_to_linear_device(vol._h, counters.data_ptr() + 4 * nt * half,
+                                                            lin.data_ptr()))
+            torch.cuda.synchronize(dev)
+            assert np.array_equal(lin.cpu().numpy(), 2 * exp)
+    finally:
+        _lib.check(L.dmf_fuse_set_variant(0))
+
+
+def _fused_counters(torch, L, _lib, vol, dev, d_depth, d_poses, cam, prm, P, npad):
+    counters = torch.zeros(2 * npad, dtype=torch.int32, device=dev)
+    _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(), P,
+                                       C.addressof(prm), counters.data_ptr(), counters.data_ptr() + 4 * npad, None))
+    return counters
+
+
+@pytest.mark.parametrize("n", [96, 61])
+def test_merge_entry_points_dmf_comm_world1(n):
+    """dmf_comm_init_rank (world 1) + the three merge entry points: all-reduce leaves the
+    counters unchanged, merge-finalize gives the plain finalize, flags stay put."""
+    torch, L, _lib, vol, dev, d_depth, d_poses, cam, prm, poses, depth = _setup(n)
+    P = poses.shape[0]
+    vol.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ver = C.c_int32()
+    _lib.check(L.dmf_rccl_version(C.addressof(ver)))
+    assert ver.value > 20000
+    uid = (C.c_char * 128)()
+    _lib.check(L.dmf_comm_unique_id(C.addressof(uid)))
+    comm = C.c_void_p()
+    _lib.check(L.dmf_comm_init_rank(C.addressof(comm), 1, C.addressof(uid), 0, 0))
+    try:
+        npad, nlo, nct = C.c_int64(), C.c_int64(), C.c_int64()
+        _lib.check(L.dmf_fuse_counter_cells_padded(vol._h, 1, C.addressof(npad)))
+        _lib.check(L.dmf_fuse_logodds_cells_padded(vol._h, 1, C.addressof(nlo)))
+        _lib.check(L.dmf_fuse_counter_cells(vol._h, C.addressof(nct)))
+        assert npad.value >= nct.value and nlo.value >= n ** 3
+        c = _fused_counters(torch, L, _lib, vol, dev, d_depth, d_poses, cam, prm, P, npad.value)
+        ref_c = c.clone()
+        ref = torch.empty(n ** 3, dtype=torch.int16, device=dev)
+        _lib.check(L.dmf_fuse_finalize_device(vol._h, c.data_ptr(), c.data_ptr() + 4 * npad.value, C.addressof(prm),
+                                              ref.data_ptr()))
+        _lib.check(L.dmf_fuse_allreduce_device(vol._h, c.data_ptr(), npad.value, comm, None))
+        torch.cuda.synchronize(dev)
+        assert torch.equal(c, ref_c)
+        lo = torch.full((nlo.value,), 12345, dtype=torch.int16, device=dev)
+        side = torch.cuda.Stream(dev)  # the merge on a communication stream of its own
+        side.wait_stream(torch.cuda.current_stream(dev))
+        _lib.check(L.dmf_fuse_merge_finalize_device(vol._h, c.data_ptr(), C.addressof(prm), lo.data_ptr(), comm,
+                                                    side.cuda_stream))
+        torch.cuda.synchronize(dev)
+        assert torch.equal(lo[: n ** 3], ref)
+        # flags: integrate a cloud, set view/good by a query, all-reduce(max) at world 1
+        pts, nn = Hh.cloud()
+        vol.integratePointCloud(pts, nn)
+        from dmf_amd import RayTracingEngine, Camera
+        RayTracingEngine(Camera(K)).reverseRayTraceFast(vol, poses[0], True)
+        view0, good0 = vol.voxel_flags()
+        _lib.check(L.dmf_flags_allreduce(vol._h, comm, None))
+        view1, good1 = vol.voxel_flags()
+        assert np.array_equal(view0, view1) and np.array_equal(good0, good1) and view0.any()
+    finally:
+        _lib.check(L.dmf_comm_destroy(comm))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_merge_over_torch_process_group_world1():
+    """The bench's path: torch's ProcessGroupNCCL communicator pointer handed to libdmf
+    (one librccl instance in the process), merge-finalize == plain finalize."""
+    torch, L, _lib, vol, dev, d_depth, d_poses, cam, prm, poses, depth = _setup(80)
+    import torch.distributed as dist
+    from dmf_amd import dist as D
+    import bench
+    P = poses.shape[0]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        dist.barrier()
+        assert bench.one_rccl_mapped()
+        comm = D.torch_comm_ptr(device=dev)
+        vol.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        npad, nlo = C.c_int64(), C.c_int64()
+        _lib.check(L.dmf_fuse_counter_cells_padded(vol._h, 1, C.addressof(npad)))
+        _lib.check(L.dmf_fuse_logodds_cells_padded(vol._h, 1, C.addressof(nlo)))
+        c = _fused_counters(torch, L, _lib, vol, dev, d_depth, d_poses, cam, prm, P, npad.value)
+        ref = torch.empty(80 ** 3, dtype=torch.int16, device=dev)
+        _lib.check(L.dmf_fuse_finalize_device(vol._h, c.data_ptr(), c.data_ptr() + 4 * npad.value, C.addressof(prm),
+                                              ref.data_ptr()))
+        lo = torch.zeros(nlo.value, dtype=torch.int16, device=dev)
+        D.merge_finalize_device(vol, c, C.addressof(prm), lo, comm)
+        torch.cuda.synchronize(dev)
+        assert torch.equal(lo[: 80 ** 3], ref)
+    finally:
+        dist.destroy_process_group()

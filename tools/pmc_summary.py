@@ -38,14 +38,17 @@ bench = json.load(open(os.path.join(src, "bench_kt.json")))
 PIPE = ("dmf::k_bk_", "dmf::k_fuse")
 kernels = sorted({k for (k, c) in tot if k.startswith(PIPE)})
 if kernels:
+    # per fusion call (a call of a multi-batch config launches each kernel once per batch)
+    calls = int(bench["steps"]) + int(bench["warmup"])
+
     def per(k, c):
-        return tot.get((k, c), 0.0) / max(len(ndisp.get((k, c), ())), 1)
+        return tot.get((k, c), 0.0) / max(calls, 1)
     per_kernel = {k: {"fetch_bytes_raw": per(k, "FETCH_SIZE") * 1024, "write_bytes": per(k, "WRITE_SIZE") * 1024,
                       "hbm_bytes": (2 * per(k, "FETCH_SIZE") + per(k, "WRITE_SIZE")) * 1024} for k in kernels}
-    # k_bk_scan runs once per batch like the others: one launch of each per fusion call
     hbm = sum(v["hbm_bytes"] for v in per_kernel.values())
     summ = {"kernel": bench["roofline"]["kernel"], "pipeline": kernels, "grid": bench["config"]["grid"],
-            "poses": bench["config"]["poses_per_gpu"], "hbm_bytes_per_launch": hbm,
+            "poses": bench["config"]["poses_per_gpu"], "image": bench["config"]["image"],
+            "hbm_bytes_per_launch": hbm, "profile": dst,
             "per_kernel": per_kernel,
             "tcc_ea0_atomic_requests_per_launch": sum(per(k, "TCC_EA0_ATOMIC_sum") for k in kernels),
             "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
@@ -53,6 +56,15 @@ if kernels:
             "note": "traffic = sum over the pipeline's kernels of (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch; "
                     "FETCH doubled per MI355X_MICROARCH.md"}
     json.dump(summ, open(os.path.join(dst, "pmc_fuse_summary.json"), "w"), indent=1)
-    json.dump(summ, open(os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_fuse_summary.json"), "w"), indent=1)
+    # the bench's lookup table: one entry per (grid, poses, image, kernel)
+    tpath = os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json")
+    try:
+        table = json.load(open(tpath))
+    except (OSError, ValueError):
+        table = []
+    key = lambda e: (e.get("grid"), e.get("poses"), e.get("image"), e.get("kernel"))  # noqa: E731
+    table = [e for e in table if key(e) != key(summ)] + [
+        {k: summ[k] for k in ("grid", "poses", "image", "kernel", "hbm_bytes_per_launch", "profile")}]
+    json.dump(table, open(tpath, "w"), indent=1)
     print(json.dumps(summ, indent=1))
 shutil.copy(os.path.join(src, "bench_kt.json"), os.path.join(dst, "bench_under_rocprof.json"))
