@@ -200,16 +200,31 @@ def render(K, width, height, pose, dmin=DEPTH_MIN_MM, dmax=DEPTH_MAX_MM):
     return depth, nrm
 
 
-def render_frames(K, width, height, poses, dmin=DEPTH_MIN_MM, dmax=DEPTH_MAX_MM, normals=False):
+def render_frames(K, width, height, poses, dmin=DEPTH_MIN_MM, dmax=DEPTH_MAX_MM, normals=False, threads=None):
+    """Render P frames; frames are independent, so they render on a thread pool (numpy
+    releases the GIL in the per-frame array work).  threads=None: the job's CPU share
+    (OMP_NUM_THREADS, else os.cpu_count(), at most 16)."""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
     poses = np.asarray(poses, np.float32).reshape(-1, 12)
     P = poses.shape[0]
     depth = np.zeros((P, height, width), np.uint16)
     nrm = np.zeros((P, height, width, 3), np.float32) if normals else None
-    for i in range(P):
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(int(threads), 16, P))
+
+    def one(i):
         dd, nn = render(K, width, height, poses[i], dmin, dmax)
         depth[i] = dd
         if normals:
             nrm[i] = nn
+    if threads == 1:
+        for i in range(P):
+            one(i)
+    else:
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(one, range(P)))
     return (depth, nrm) if normals else depth
 
 

@@ -1,0 +1,207 @@
+"""GPU: the fusion path at the single-GPU BASELINE.json configurations.
+
+Each config is checked two ways:
+* bit-exact against the CPU oracle (oracle.cpp dda_ray, OpenMP rows) on a frame subset at
+  the config's FULL grid and image size;
+* at the config's full pose count, through size-independent properties: the default
+  dispatch and an independent exact implementation (brick pipeline vs k_fuse_l) agree
+  counter for counter; every cell update is a hit or a miss; there is one hit per ray
+  that ends inside the grid; the multi-batch brick path (pose batches sized by its pair
+  budget) equals a single batch.
+Configs: 2 = 640x480, 256^3, 64 poses; 3 = 1280x720, 512^3, 256 poses; 5's single-GPU
+shard = 1280x720, 1024^3 (32 of its 256 poses per GPU).  Config 4's shard (640x480,
+512^3, 128 poses) is the bench workload and tests/test_gpu_parity.py's full-size test.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import helpers as Hh
+
+pytestmark = pytest.mark.gpu
+
+
+class Fusion:
+    """Device-API fusion of resident frames on one volume (torch tensors)."""
+
+    def __init__(self, grid, W, H, P, seed=1234):
+        import torch
+        import dmf_amd
+        from dmf_amd import _lib, scene
+        self.torch, self._lib = torch, _lib
+        self.L = _lib.load()
+        self.dev = torch.device("cuda", 0)
+        self.K = scene.intrinsics(W, H)
+        self.poses = np.ascontiguousarray(scene.fibonacci_poses(P, seed=seed), np.float32)
+        self.depth = np.ascontiguousarray(scene.render_frames(self.K, W, H, self.poses), np.uint16)
+        self.vol = dmf_amd.VoxelVolume()
+        self.vol.setDimensions(*Hh.BOUNDS)
+        self.vol.setVolumeSize(grid, grid, grid)
+        self.vol.constructVolume()
+        self.vol.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
+        self.cam = _lib.make_camera(self.K, H, W)
+        self.prm = _lib.default_fuse_params(dmin_mm=scene.DEPTH_MIN_MM, dmax_mm=scene.DEPTH_MAX_MM)
+        nct = C.c_int64()
+        _lib.check(self.L.dmf_fuse_counter_cells(self.vol._h, C.addressof(nct)))
+        self.nt = nct.value
+        self.d_depth = torch.from_numpy(self.depth.view(np.int16)).to(self.dev)
+        self.d_poses = torch.from_numpy(self.poses).to(self.dev)
+        self.grid = grid
+
+    def run(self, variant=0, p0=0, p1=None, counters=None):
+        """Fuse frames [p0, p1) with `variant`; returns (tiled [hits | misses] int32 on the
+        device, stats[8] uint64, kernel name)."""
+        torch, L, _lib = self.torch, self.L, self._lib
+        p1 = self.poses.shape[0] if p1 is None else p1
+        c = torch.zeros(2 * self.nt, dtype=torch.int32, device=self.dev) if counters is None else counters
+        st = torch.zeros(8, dtype=torch.int64, device=self.dev)
+        _lib.check(L.dmf_fuse_set_variant(variant))
+        try:
+            _lib.check(L.dmf_fuse_depth_device(self.vol._h, C.addressof(self.cam), self.d_depth[p0].data_ptr(),
+                                               self.d_poses[p0].data_ptr(), p1 - p0, C.addressof(self.prm),
+                                               c.data_ptr(), c.data_ptr() + 4 * self.nt, st.data_ptr()))
+            name = L.dmf_fuse_kernel().decode()
+        finally:
+            _lib.check(L.dmf_fuse_set_variant(0))
+        torch.cuda.synchronize(self.dev)
+        return c, st.cpu().numpy().astype(np.uint64), name
+
+    def linear(self, c):
+        """Tiled device counters -> x-major host (hits, misses)."""
+        torch, L, _lib = self.torch, self.L, self._lib
+        lin = torch.empty(self.grid ** 3, dtype=torch.int32, device=self.dev)
+        out = []
+        for half in (0, 1):
+            _lib.check(L.dmf_fuse_counters_to_linear_device(self.vol._h, c.data_ptr() + 4 * self.nt * half,
+                                                            lin.data_ptr()))
+            torch.cuda.synchronize(self.dev)
+            out.append(lin.cpu().numpy())
+        return out
+
+
+def _oracle_subset(oracle, f, frames):
+    ov = oracle.Volume()
+    ov.setDimensions(*Hh.BOUNDS)
+    ov.setVolumeSize(f.grid, f.grid, f.grid)
+    ov.constructVolume()
+    from dmf_amd import scene
+    return oracle.fuse_depth(ov, f.K, f.depth[frames], f.poses[frames], dmin=scene.DEPTH_MIN_MM,
+                             dmax=scene.DEPTH_MAX_MM, threads=16)
+
+
+def _invariants(f, c, st):
+    hits = c[: f.nt].to(dtype=f.torch.int64).sum().item()
+    total = c.to(dtype=f.torch.int64).sum().item()
+    assert st[3] == 0  # DDA guard
+    assert total == int(st[0])  # every update is a hit or a miss
+    assert hits == int(st[2])   # one hit per ray ending inside the grid
+    assert int(st[1]) > 0 and int(st[0]) > int(st[1])
+
+
+@pytest.mark.parametrize("cfg", ["config2", "config3", "config5-shard"])
+def test_config_oracle_subset(oracle, cfg):
+    """Frame subset at the config's full grid and image size: bit-exact vs the oracle."""
+    grid, W, H, frames = {"config2": (256, 640, 480, [0, 21, 42, 63]),
+                          "config3": (512, 1280, 720, [0, 128]),
+                          "config5-shard": (1024, 1280, 720, [5])}[cfg]
+    P = {"config2": 64, "config3": 256, "config5-shard": 32}[cfg]
+    f = Fusion(grid, W, H, P)
+    ho, mo, so = _oracle_subset(oracle, f, frames)
+    c = f.torch.zeros(2 * f.nt, dtype=f.torch.int32, device=f.dev)
+    for p in frames:  # the default dispatch of this grid, one frame per call
+        c, st, _ = f.run(0, p, p + 1, counters=c)
+    hg, mg = f.linear(c)
+    assert np.array_equal(hg, ho) and np.array_equal(mg, mo)
+
+
+@pytest.mark.parametrize("cfg", ["config2", "config3", "config5-shard"])
+def test_config_full_poses(cfg):
+    """All of the config's poses (per GPU): default dispatch == the other exact kernel,
+    counter for counter, plus the counting invariants."""
+    grid, W, H, P = {"config2": (256, 640, 480, 64), "config3": (512, 1280, 720, 256),
+                     "config5-shard": (1024, 1280, 720, 32)}[cfg]
+    f = Fusion(grid, W, H, P)
+    c0, s0, k0 = f.run(0)
+    _invariants(f, c0, s0)
+    other = 31 if k0.startswith("dmf::k_bk_fuse") else 40
+    c1, s1, k1 = f.run(other)
+    assert k0 != k1
+    assert np.array_equal(s0[:4], s1[:4])
+    assert f.torch.equal(c0, c1)
+    if cfg == "config3":  # the default path splits 256 frames into pose batches
+        assert k0.startswith("dmf::k_bk_fuse")
+
+
+def test_config3_batches_equal_single_batch(monkeypatch):
+    """Config 3's frames through the brick pipeline in batches of 7 poses == the budget's
+    default batching (pose batches accumulate into the same counters)."""
+    f = Fusion(512, 1280, 720, 48, seed=99)
+    c0, s0, _ = f.run(40)
+    monkeypatch.setenv("DMF_BK_BATCH_POSES", "7")
+    c1, s1, _ = f.run(40)
+    assert np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
+
+
+def test_anisotropic_grid_over_8192_bricks(oracle):
+    """1024 x 1024 x 288 cells = 9216 bricks (> 8192: the 1024-lane A/B
+    workgroups with a 36 KiB LDS histogram) and unequal bricks per axis (bk_index, the
+    brick decode in k_bk_fuse): brick pipeline == k_fuse_l counter for counter, and == the
+    oracle on one frame."""
+    import torch
+    import dmf_amd
+    from dmf_amd import _lib, scene
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    K = scene.intrinsics(640, 480)
+    poses = np.ascontiguousarray(scene.fibonacci_poses(4, seed=3), np.float32)
+    depth = np.ascontiguousarray(scene.render_frames(K, 640, 480, poses), np.uint16)
+    dims = (1024, 1024, 288)
+    bounds = (-0.5, 0.5, -0.5, 0.5, -0.5, 0.5 * 288 / 1024 * 2 - 0.5)  # exact binary deltas
+    vol = dmf_amd.VoxelVolume()
+    vol.setDimensions(*bounds)
+    vol.setVolumeSize(*dims)
+    vol.constructVolume()
+    assert tuple(vol.dims) == dims
+    vol.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    cam = _lib.make_camera(K, 480, 640)
+    prm = _lib.default_fuse_params(dmin_mm=scene.DEPTH_MIN_MM, dmax_mm=scene.DEPTH_MAX_MM)
+    nct = C.c_int64()
+    _lib.check(L.dmf_fuse_counter_cells(vol._h, C.addressof(nct)))
+    nt = nct.value
+    d_depth = torch.from_numpy(depth.view(np.int16)).to(dev)
+    d_poses = torch.from_numpy(poses).to(dev)
+    out = {}
+    try:
+        for variant in (40, 31):
+            _lib.check(L.dmf_fuse_set_variant(variant))
+            c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
+            st = torch.zeros(8, dtype=torch.int64, device=dev)
+            _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(), 4,
+                                               C.addressof(prm), c.data_ptr(), c.data_ptr() + 4 * nt, st.data_ptr()))
+            torch.cuda.synchronize(dev)
+            out[variant] = (c, st.cpu().numpy(), L.dmf_fuse_kernel().decode())
+    finally:
+        _lib.check(L.dmf_fuse_set_variant(0))
+    (c0, s0, k0), (c1, s1, k1) = out[40], out[31]
+    assert k0.startswith("dmf::k_bk_fuse") and k1.startswith("dmf::k_fuse_l")
+    assert s0[0] > 10 ** 8 and np.array_equal(s0[:4], s1[:4]) and torch.equal(c0, c1)
+    # one frame against the oracle
+    ov = oracle.Volume()
+    ov.setDimensions(*bounds)
+    ov.setVolumeSize(*dims)
+    ov.constructVolume()
+    ho, mo, _ = oracle.fuse_depth(ov, K, depth[2:3], poses[2:3], dmin=scene.DEPTH_MIN_MM, dmax=scene.DEPTH_MAX_MM,
+                                  threads=16)
+    _lib.check(L.dmf_fuse_set_variant(40))
+    try:
+        c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
+        _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth[2].data_ptr(), d_poses[2].data_ptr(), 1,
+                                           C.addressof(prm), c.data_ptr(), c.data_ptr() + 4 * nt, None))
+    finally:
+        _lib.check(L.dmf_fuse_set_variant(0))
+    lin = torch.empty(int(np.prod(dims)), dtype=torch.int32, device=dev)
+    for half, exp in ((0, ho), (1, mo)):
+        _lib.check(L.dmf_fuse_counters_to_linear_device(vol._h, c.data_ptr() + 4 * nt * half, lin.data_ptr()))
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(lin.cpu().numpy(), exp)
