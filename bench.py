@@ -311,6 +311,7 @@ def main():
                                     "f_lane_util": float(st[8]) / max(64.0 * float(st[7]), 1.0),
                                     "f_wave_cycles": {"refill": int(st[10]) // args.steps, "walk": int(st[11]) // args.steps,
                                                       "flush": int(st[12]) // args.steps,
+                                                      "part_barrier": int(st[15]) // args.steps,
                                                       "lifetime_sum": int(st[14]) // args.steps,
                                                       "lifetime_max_wave": int(st[13])}})
         else:

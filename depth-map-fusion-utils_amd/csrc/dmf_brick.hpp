@@ -216,5 +216,71 @@ __host__ __device__ inline int coarse_next(Coarse& w) {
   return s2 ? 2 : (s1 ? 1 : 0);
 }
 
+// ---- Major-axis ("slab") form of the fine walk (phase F) ----
+//
+// Let M be an axis with the largest |dq| (its crossings are the most frequent: interval
+// 2Q/|dq_M| in tau = T / prod|dq|), m1 < m2 the other two.  Between two consecutive
+// M-crossings (a "slab") each minor axis crosses AT MOST ONCE: its interval 2Q/|dq_m| is
+// no shorter, and the half-open window (previous M-crossing, next M-crossing] holds one
+// point of any arithmetic sequence with that step (ties keep the x < y < z order).  So the
+// walk advances one slab at a time: minor m crosses in this slab iff its next crossing
+// comes before the next M-crossing, the two minors (if both cross) in their own order,
+// then M.  With pairwise E as in the fine walk, e_m = E_{M m} (sign-flipped when m < M)
+// and e_12 = E_{m1 m2}; the biased forms below make every test "b >= 0":
+//   b_m  = e_m + [m < M] - 1   >= 0  <=>  minor m crosses before the next M-crossing
+//   b_12 = e_12 - 1            >= 0  <=>  m2 crosses before m1 (m1 < m2: ties go to m1)
+// Updates per slab: b_m += K_m - (c_m ? K_M : 0);  b_12 += (c_1 ? K_2 : 0) - (c_2 ? K_1 : 0).
+// A non-moving minor keeps b_m = -(never); the b_12 of a pair with one is never consulted.
+
+// An axis with the largest |dq| (the lowest such index).
+__host__ __device__ inline int major_axis(const QRay& r) {
+  return r.adq[0] >= r.adq[1] ? (r.adq[0] >= r.adq[2] ? 0 : 2) : (r.adq[1] >= r.adq[2] ? 1 : 2);
+}
+
+__host__ __device__ inline int32_t pick3(int32_t v0, int32_t v1, int32_t v2, int a) {
+  return a == 0 ? v0 : (a == 1 ? v1 : v2);
+}
+
+// Slab state (b1, b2, b12) from the fine walk's pairwise E (exact int32 values, or the
+// +-kNever of a non-moving axis), major axis M.  No dynamic indexing (device scratch).
+__host__ __device__ inline void slab_from_pairwise(int M, int32_t E01, int32_t E02, int32_t E12, int32_t& b1,
+                                                   int32_t& b2, int32_t& b12) {
+  // M = 0: minors 1, 2;  M = 1: minors 0, 2;  M = 2: minors 0, 1
+  b1 = M == 0 ? (int32_t)((uint32_t)E01 - 1u) : (M == 1 ? (int32_t)(0u - (uint32_t)E01) : (int32_t)(0u - (uint32_t)E02));
+  b2 = M == 0 ? (int32_t)((uint32_t)E02 - 1u) : (M == 1 ? (int32_t)((uint32_t)E12 - 1u) : (int32_t)(0u - (uint32_t)E12));
+  b12 = (int32_t)((uint32_t)(M == 0 ? E12 : (M == 1 ? E02 : E01)) - 1u);
+}
+
+// Reference slab walk (CPU self-test and documentation of phase F's step): emits `cells`
+// cells starting at cell p[] with state (b1, b2, b12); K* = 2Q|dq| of the major / minors,
+// s* = their steps.  emit(x, y, z) per cell, in walk order.
+template <class F>
+__host__ __device__ inline void slab_walk(int M, int32_t b1, int32_t b2, int32_t b12, uint32_t KM, uint32_t K1,
+                                          uint32_t K2, const int32_t st[3], const int32_t p0[3], int cells, F&& emit) {
+  const int m1 = M == 0 ? 1 : 0, m2 = M == 2 ? 1 : 2;
+  int32_t p[3] = {p0[0], p0[1], p0[2]};
+  int rem = cells;
+  while (rem > 0) {
+    const bool c1 = b1 >= 0, c2 = b2 >= 0, o = b12 >= 0;
+    emit(p[0], p[1], p[2]);
+    --rem;
+    if (c1 && c2) {
+      const int f = o ? m2 : m1, s = o ? m1 : m2;
+      p[f] += st[f];
+      if (rem > 0) { emit(p[0], p[1], p[2]); --rem; }
+      p[s] += st[s];
+      if (rem > 0) { emit(p[0], p[1], p[2]); --rem; }
+    } else if (c1 || c2) {
+      const int f = c1 ? m1 : m2;
+      p[f] += st[f];
+      if (rem > 0) { emit(p[0], p[1], p[2]); --rem; }
+    }
+    p[M] += st[M];
+    b1 = (int32_t)((uint32_t)b1 + K1 - (c1 ? KM : 0u));
+    b2 = (int32_t)((uint32_t)b2 + K2 - (c2 ? KM : 0u));
+    b12 = (int32_t)((uint32_t)b12 + (c1 ? K2 : 0u) - (c2 ? K1 : 0u));
+  }
+}
+
 }  // namespace brick
 }  // namespace dmf

@@ -901,6 +901,10 @@ __device__ inline uint32_t bk_e30(int32_t e) {
   return (uint32_t)(e > lim ? lim : (e < -lim ? -lim : e)) & 0x3fffffffu;
 }
 
+// SLAB (phase F's major-axis walk, k_bk_fuse_s): the E fields hold the
+// slab state (b1, b2, b12) of dmf_brick.hpp instead of (E01, E02, E12), the |dq| fields are
+// in (major, minor1, minor2) order, and pb.y bits 27-28 name the major axis.
+template <bool SLAB>
 __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
@@ -925,14 +929,32 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets
     const uint32_t e01 = (uint32_t)bk::e0_pair(R, 0, 1), e02 = (uint32_t)bk::e0_pair(R, 0, 2),
                    e12 = (uint32_t)bk::e0_pair(R, 1, 2);
     const uint32_t signs = (R.st[0] < 0 ? 1u << 22 : 0u) | (R.st[1] < 0 ? 1u << 23 : 0u) | (R.st[2] < 0 ? 1u << 24 : 0u);
-    const uint2 wb0 = make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
-                                 (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18) | signs);
+    // SLAB: major axis M, minors m1 < m2; state and |dq| in (M, m1, m2) order
+    const int M = SLAB ? bk::major_axis(R) : 0;
+    const int m1 = M == 0 ? 1 : 0, m2 = M == 2 ? 1 : 2;
+    const uint32_t aM = (uint32_t)bk::pick3(R.adq[0], R.adq[1], R.adq[2], M),
+                   a1 = (uint32_t)bk::pick3(R.adq[0], R.adq[1], R.adq[2], m1),
+                   a2 = (uint32_t)bk::pick3(R.adq[0], R.adq[1], R.adq[2], m2);
+    const uint32_t KM = (uint32_t)(2 * bk::kQ) * aM, Km1 = (uint32_t)(2 * bk::kQ) * a1, Km2 = (uint32_t)(2 * bk::kQ) * a2;
+    int32_t sb1 = 0, sb2 = 0, sb12 = 0;
+    if (SLAB) bk::slab_from_pairwise(M, (int32_t)e01, (int32_t)e02, (int32_t)e12, sb1, sb2, sb12);
+    const uint2 wb0 = SLAB ? make_uint2(aM | ((a2 & 0x3fffu) << 18), a1 | ((a2 >> 14) << 18) | signs | ((uint32_t)M << 27))
+                           : make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
+                                        (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18) | signs);
     // entry state of the pair being built (E fields without the step bits)
     auto entry = [&](const int32_t c[3]) {
       uint4 e;
-      e.x = bk_e30((int32_t)(e01 + (uint32_t)c[0] * K1 - (uint32_t)c[1] * K0));
-      e.y = bk_e30((int32_t)(e02 + (uint32_t)c[0] * K2 - (uint32_t)c[2] * K0));
-      e.z = bk_e30((int32_t)(e12 + (uint32_t)c[1] * K2 - (uint32_t)c[2] * K1));
+      if (SLAB) {  // b = b(0) + c_M K_m - c_m K_M;  b12 = b12(0) + c_1 K_2 - c_2 K_1
+        const uint32_t cM = (uint32_t)bk::pick3(c[0], c[1], c[2], M), c1 = (uint32_t)bk::pick3(c[0], c[1], c[2], m1),
+                       c2 = (uint32_t)bk::pick3(c[0], c[1], c[2], m2);
+        e.x = bk_e30((int32_t)((uint32_t)sb1 + cM * Km1 - c1 * KM));
+        e.y = bk_e30((int32_t)((uint32_t)sb2 + cM * Km2 - c2 * KM));
+        e.z = bk_e30((int32_t)((uint32_t)sb12 + c1 * Km2 - c2 * Km1));
+      } else {
+        e.x = bk_e30((int32_t)(e01 + (uint32_t)c[0] * K1 - (uint32_t)c[1] * K0));
+        e.y = bk_e30((int32_t)(e02 + (uint32_t)c[0] * K2 - (uint32_t)c[2] * K0));
+        e.z = bk_e30((int32_t)(e12 + (uint32_t)c[1] * K2 - (uint32_t)c[2] * K1));
+      }
       const uint32_t x = (uint32_t)(R.cs[0] + R.st[0] * c[0]) & m5, y = (uint32_t)(R.cs[1] + R.st[1] * c[1]) & m5,
                      z = (uint32_t)(R.cs[2] + R.st[2] * c[2]) & m5;
       e.w = bk_lds_word(x, y, z);
@@ -1269,6 +1291,269 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
   }
 }
 
+// Phase F, slab walk (default).  Same part queue, LDS box, refill and
+// flush as k_bk_fuse, but a lane advances one SLAB per step (dmf_brick.hpp slab_walk):
+// the cells between two major-axis crossings, 1 + c1 + c2 of them, with one compare per
+// minor axis instead of a three-way DDA selection per cell.  Branch-free: the three LDS
+// adds of a slab are predicated on the cells the pair still owns (v = min(1 + c1 + c2,
+// r)); the state keeps moving harmlessly past the pair's end (unsigned arithmetic;
+// refilled or ignored).  The pair's last cell is added at adoption (hit or miss), so the
+// walk covers r = cells - 1.  NSLOT pairs per lane walk interleaved (independent
+// dependency chains: at 4 waves per SIMD a single chain leaves the SIMD idle between
+// its dependent instructions).  A wave refills when >= REFILL of its 64 * NSLOT slots
+// are idle, from per-slot records prefetched one refill ahead.
+template <int REFILL, int S_ORDER, int UNROLL, int NSLOT>
+__global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, const uint4* __restrict__ pa,
+                                                          const uint2* __restrict__ pb,
+                                                          const uint32_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ cnt,
+                                                          const uint32_t* __restrict__ part_pref,
+                                                          unsigned long long* __restrict__ ctl,
+                                                          int32_t* __restrict__ hits, int32_t* __restrict__ misses,
+                                                          unsigned long long* __restrict__ stats) {
+  __shared__ uint32_t box[kBkBoxWords + 4 + 64];  // counters (skewed), control words, diagnostic words
+  uint32_t* sh = box + kBkBoxWords;
+  stats = stat_slot(stats);
+  const int tid = threadIdx.x, l = tid & 63;
+  for (int i = tid; i < kBkBoxWords; i += blockDim.x) box[i] = 0;
+  const uint32_t nparts = (uint32_t)ctl[1];
+  const Tiles tl = tiles_of(g.n);
+  unsigned long long npairs = 0, nparts_done = 0, nflush = 0;
+#if defined(DMF_EXP_STATS)
+  // diagnostic build: wave blocks, slots active at block start, refills, and s_memtime
+  // cycles per phase (refill, walk, flush incl. its barriers, wait at the part-start barrier)
+  unsigned long long nblocks = 0, nlanes = 0, nrefill = 0, t_refill = 0, t_walk = 0, t_flush = 0, t_bar = 0;
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
+  char* const lds = (char*)box;
+  for (;;) {
+    if (tid == 0) {
+      sh[0] = (uint32_t)atomicAdd(&ctl[2], 1ull);
+      sh[1] = 0;
+    }
+    DMF_T(tb0);
+    __syncthreads();
+    DMF_TACC(t_bar, tb0);
+    const uint32_t t = sh[0];
+    if (t >= nparts) break;
+    int lo = 0, hi = bg.nbricks - 1;  // last brick b with part_pref[b] <= t
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (part_pref[mid] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const int b = lo;
+    const uint32_t np = part_pref[b + 1] - part_pref[b], j = t - part_pref[b], nb_pairs = cnt[b];
+    const uint32_t p0 = off[b] + (uint32_t)(((uint64_t)nb_pairs * j) / np);
+    const uint32_t n = (uint32_t)(((uint64_t)nb_pairs * (j + 1)) / np) - (uint32_t)(((uint64_t)nb_pairs * j) / np);
+    const int bz = b % bg.nb[2], by = (b / bg.nb[2]) % bg.nb[1], bx = b / (bg.nb[2] * bg.nb[1]);
+    const int lo0 = bx << bk::kLog, lo1 = by << bk::kLog, lo2 = bz << bk::kLog;
+    if (tid == 0) {
+      npairs += n;
+      ++nparts_done;
+    }
+    // per slot: slab state (unsigned: it may run past the pair's end), LDS byte offset
+    // and strides, cells left (r), the prefetched record (ca, cb) and whether it is valid
+    uint32_t b1[NSLOT], b2[NSLOT], b12[NSLOT], K1[NSLOT], K2[NSLOT], K1mM[NSLOT], K2mM[NSLOT], nK1[NSLOT];
+    uint32_t cur[NSLOT], dM[NSLOT], d1[NSLOT], d2[NSLOT];
+    int r[NSLOT];
+    uint4 ca[NSLOT];
+    uint2 cb[NSLOT];
+    bool fok[NSLOT];
+#pragma unroll
+    for (int q = 0; q < NSLOT; ++q) {
+      b1[q] = b2[q] = b12[q] = K1[q] = K2[q] = K1mM[q] = K2mM[q] = nK1[q] = 0;
+      cur[q] = dM[q] = d1[q] = d2[q] = 0;
+      r[q] = 0;
+      ca[q] = make_uint4(0, 0, 0, 0);
+      cb[q] = make_uint2(0, 0);
+      fok[q] = false;
+    }
+    auto decode = [&](int q) {
+      const uint4 ra = ca[q];
+      const uint2 rb = cb[q];
+      b1[q] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ra.x, 0, 30);
+      b2[q] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ra.y, 0, 30);
+      b12[q] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ra.z, 0, 30);
+      const uint32_t aM = rb.x & 0x3ffffu, a1 = rb.y & 0x3ffffu, a2 = (rb.x >> 18) | (((rb.y >> 18) & 15u) << 14);
+      const uint32_t KM = aM << 9;
+      K1[q] = a1 << 9;
+      K2[q] = a2 << 9;
+      K1mM[q] = K1[q] - KM;
+      K2mM[q] = K2[q] - KM;
+      nK1[q] = 0u - K1[q];
+      cur[q] = (ra.w & 0xffffu) * 4u;
+      r[q] = (int)((ra.x >> 30) | ((ra.y >> 30) << 2) | ((ra.z >> 30) << 4) | (((rb.y >> 25) & 1u) << 6));
+      const uint32_t sx = (rb.y >> 22) & 1u ? 0u - 4u * kBkSx : 4u * kBkSx;
+      const uint32_t sy = (rb.y >> 23) & 1u ? 0u - 4u * kBkSy : 4u * kBkSy;
+      const uint32_t sz = (rb.y >> 24) & 1u ? 0u - 4u : 4u;
+      const uint32_t M = (rb.y >> 27) & 3u;
+      dM[q] = M == 0 ? sx : (M == 1 ? sy : sz);
+      d1[q] = M == 0 ? sy : sx;
+      d2[q] = M == 2 ? sy : sz;
+      // the pair's last cell: a hit when the ray ends there inside the grid, else a miss
+      atomicAdd(&box[ra.w >> 16], (rb.y >> 26) & 1u ? 0x10000u : 1u);
+    };
+    bool more = true;
+    // lanes in need[q] take the next pair indices (one LDS counter atomic for all slots)
+    // and load their records into slot q
+    auto prefetch = [&](const uint64_t* need) {
+      uint32_t nn = 0;
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) nn += (uint32_t)__builtin_popcountll(need[q]);
+      uint32_t base0 = 0;
+      if (l == 0) base0 = atomicAdd(&sh[1], nn);
+      uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
+      if (base + nn >= n) more = false;
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) {
+        if ((need[q] >> l) & 1ull) {
+          const uint32_t k = base + (uint32_t)lane_prefix(need[q]);
+          fok[q] = k < n;
+          if (fok[q]) {
+            const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
+            ca[q] = pa[i];
+            cb[q] = pb[i];
+          }
+        }
+        base += (uint32_t)__builtin_popcountll(need[q]);
+      }
+    };
+    {
+      uint64_t all[NSLOT];
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) all[q] = ~0ull;
+      prefetch(all);
+    }
+    for (;;) {
+      int nact = 0;
+      bool any_act = false;
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) {
+        const uint64_t a = __builtin_amdgcn_ballot_w64(r[q] > 0);
+        nact += __builtin_popcountll(a);
+        any_act |= a != 0;
+      }
+      DMF_T(tr0);
+      if (nact <= 64 * NSLOT - REFILL) {
+        uint64_t take[NSLOT];
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < NSLOT; ++q) {
+          take[q] = __builtin_amdgcn_ballot_w64(r[q] <= 0 && fok[q]);
+          any |= take[q] != 0;
+        }
+        if (any) {
+#if defined(DMF_EXP_STATS)
+          if (l == 0) ++nrefill;
+#endif
+#pragma unroll
+          for (int q = 0; q < NSLOT; ++q) {
+            if (r[q] <= 0 && fok[q]) {
+              decode(q);
+              fok[q] = false;
+            }
+          }
+          if (more) prefetch(take);
+          any_act = false;
+#pragma unroll
+          for (int q = 0; q < NSLOT; ++q) any_act |= __builtin_amdgcn_ballot_w64(r[q] > 0) != 0;
+        }
+      }
+      DMF_TACC(t_refill, tr0);
+      if (!any_act) {
+        bool pending = false;
+#pragma unroll
+        for (int q = 0; q < NSLOT; ++q) pending |= __builtin_amdgcn_ballot_w64(fok[q]) != 0;
+        if (!pending) break;
+        continue;
+      }
+      DMF_T(tw0);
+#if defined(DMF_EXP_STATS)
+      if (l == 0) ++nblocks;
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) nlanes += (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(r[q] > 0));
+#endif
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+        for (int q = 0; q < NSLOT; ++q) {
+          const bool c1 = (int32_t)b1[q] >= 0, c2 = (int32_t)b2[q] >= 0, o = (int32_t)b12[q] >= 0;
+          // cells in this slab (1 + c1 + c2) and how many of them the pair still owns
+          const int nc = 3 + ((int32_t)b1[q] >> 31) + ((int32_t)b2[q] >> 31);
+          const int v = min(nc, r[q]);
+          const uint32_t x1 = c1 ? d1[q] : 0u, x2 = c2 ? d2[q] : 0u;
+          const uint32_t p1 = cur[q] + ((c2 && (!c1 || o)) ? d2[q] : x1), p2 = cur[q] + x1 + x2;
+#if defined(DMF_EXP_NOLDS)  // timing diagnostics only (wrong counts): no walk adds
+          asm volatile("" ::"v"(v), "v"(p1), "v"(p2));
+#elif defined(DMF_EXP_LDSLANE)  // timing diagnostics only: conflict-free per-lane words
+          {
+            const uint32_t dw = (uint32_t)(kBkBoxWords + 4 + l) * 4u;
+            asm volatile("" ::"v"(p1), "v"(p2));
+            if (v >= 1) atomicAdd((uint32_t*)(lds + dw), 1u);
+            if (v >= 2) atomicAdd((uint32_t*)(lds + dw), 1u);
+            if (v >= 3) atomicAdd((uint32_t*)(lds + dw), 1u);
+          }
+#else
+          if (v >= 1) atomicAdd((uint32_t*)(lds + cur[q]), 1u);
+          if (v >= 2) atomicAdd((uint32_t*)(lds + p1), 1u);
+          if (v >= 3) atomicAdd((uint32_t*)(lds + p2), 1u);
+#endif
+          cur[q] = p2 + dM[q];
+          b1[q] += c1 ? K1mM[q] : K1[q];
+          b2[q] += c2 ? K2mM[q] : K2[q];
+          b12[q] += (c1 ? K2[q] : 0u) + (c2 ? nK1[q] : 0u);
+          r[q] -= nc;
+        }
+      }
+      DMF_TACC(t_walk, tw0);
+    }
+    DMF_T(tf0);
+    __syncthreads();
+    // flush: as k_bk_fuse (one device atomic per non-zero cell and counter)
+    for (int e = tid; e < bk::kCells; e += blockDim.x) {
+      const int tile = e >> 4, w16 = e & 15;
+      const int tx = tile >> (2 * bk::kLog - 3), ty = (tile >> (bk::kLog - 2)) & ((bk::kB >> 1) - 1),
+                tz = tile & ((bk::kB >> 2) - 1);
+      const int lx = tx * 2 + (w16 >> 3), ly = ty * 2 + ((w16 >> 2) & 1), lz = tz * 4 + (w16 & 3);
+      const int li = lx * kBkSx + ly * kBkSy + lz;
+      const uint32_t v = box[li];
+      if (v) {
+        box[li] = 0;
+        const uint32_t ti = tiled_index(tl, lo0 + lx, lo1 + ly, lo2 + lz);
+        const int32_t mi = (int32_t)(v & 0xffffu), hv = (int32_t)(v >> 16);
+        if (mi) atomic_add_dev(&misses[ti], mi);
+        if (hv) atomic_add_dev(&hits[ti], hv);
+        ++nflush;
+      }
+    }
+    __syncthreads();
+    DMF_TACC(t_flush, tf0);
+  }
+  if (stats) {
+    for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
+    if (l == 0 && nflush) atomicAdd(&stats[6], nflush);
+#if defined(DMF_EXP_STATS)
+    if (l == 0) {
+      atomicAdd(&stats[7], nblocks);
+      atomicAdd(&stats[8], nlanes);
+      atomicAdd(&stats[9], nrefill);
+      atomicAdd(&stats[10], t_refill);
+      atomicAdd(&stats[11], t_walk);
+      atomicAdd(&stats[12], t_flush);
+      atomicAdd(&stats[15], t_bar);
+      const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+      atomicMax(&stats[13], t_end - t_start);
+      atomicAdd(&stats[14], t_end - t_start);
+    }
+#endif
+    if (tid == 0) {
+      if (npairs) atomicAdd(&stats[4], npairs);
+      if (nparts_done) atomicAdd(&stats[5], nparts_done);
+    }
+  }
+}
+
 // Tiled counters -> clamped int16 log-odds in the reference's x-major voxel order.
 // Four lanes per 2x2x4 tile: lane q of the tile reads int4 q of each counter line (the
 // 4 z-cells of row (x, y) = (2tx + q/2, 2ty + q%2); a wave's loads are 1 KB contiguous)
@@ -1333,7 +1618,9 @@ static int fuse_variant() {
   return v;
 }
 constexpr int kVariantBrick = 40;
-static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantBrick + 3; }
+constexpr int kVariantSlab = 44;  // 44..47: slab walk (k_bk_pairs<true> + k_bk_fuse_s); 40..43: per-cell walk
+static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantSlab + 3; }
+static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantSlab + 3); }
 static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
 
 static BkGeom brick_geom(const Geom& g) {
@@ -1419,7 +1706,9 @@ static int bk_attributes() {
   if (!attr_set.load()) {
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(sizeof(uint32_t) * 32768)));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs, hipFuncAttributeMaxDynamicSharedMemorySize,
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(uint32_t) * 32768)));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(sizeof(uint32_t) * 32768)));
     attr_set.store(true);
   }
@@ -1469,20 +1758,35 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, v->stream, bg.nbricks, (const uint32_t*)cnt, off, part_pref,
                        ctlp);
     DMF_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bk_pairs, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk, pl.span, bg,
-                       (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra, (uint2*)prb);
+    const int fv = fuse_variant();
+    if (is_slab_variant(fv))
+      hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk, pl.span, bg,
+                         (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra, (uint2*)prb);
+    else
+      hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk, pl.span,
+                         bg, (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra,
+                         (uint2*)prb);
     DMF_LAUNCH_CHECK();
 #define DMF_BK_FUSE(R, S, U, N, C, B)                                                                           \
   hipLaunchKernelGGL((k_bk_fuse<R, S, U, N, C, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,            \
                      (const uint4*)pra, (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt,           \
                      (const uint32_t*)part_pref, ctlp, d_hits, d_misses, st)
-    switch (fuse_variant()) {
+#define DMF_BK_FUSE_S(R, S, U, N)                                                                              \
+  hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg, (const uint4*)pra,     \
+                     (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt, (const uint32_t*)part_pref, ctlp, \
+                     d_hits, d_misses, st)
+    switch (fv) {
+      case 40: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
       case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
       case 42: DMF_BK_FUSE(32, 8, 8, 2, 0, false); break;
       case 43: DMF_BK_FUSE(16, 8, 8, 1, 256, true); break;
-      default: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
+      case 45: DMF_BK_FUSE_S(32, 8, 4, 2); break;
+      case 46: DMF_BK_FUSE_S(24, 8, 3, 2); break;
+      case 47: DMF_BK_FUSE_S(32, 8, 2, 2); break;
+      default: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // 0, 44
     }
 #undef DMF_BK_FUSE
+#undef DMF_BK_FUSE_S
     DMF_LAUNCH_CHECK();
   }
   return DMF_OK;
@@ -1538,7 +1842,10 @@ static const char* variant_name(int v) {
     case 41: return "dmf::k_bk_fuse<16, 8, 8, 1, 0, false>";
     case 42: return "dmf::k_bk_fuse<32, 8, 8, 2, 0, false>";
     case 43: return "dmf::k_bk_fuse<16, 8, 8, 1, 256, true>";
-    default: return "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>";  // grids over 1024 cells per axis: k_fuse_l<12, 1280>
+    case 45: return "dmf::k_bk_fuse_s<32, 8, 4, 2>";
+    case 46: return "dmf::k_bk_fuse_s<24, 8, 3, 2>";
+    case 47: return "dmf::k_bk_fuse_s<32, 8, 2, 2>";
+    default: return "dmf::k_bk_fuse_s<16, 8, 4, 1>";  // 0, 44; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
 }
 

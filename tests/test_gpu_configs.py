@@ -124,11 +124,14 @@ def test_config_full_poses(cfg):
     f = Fusion(grid, W, H, P)
     c0, s0, k0 = f.run(0)
     _invariants(f, c0, s0)
-    other = 31 if k0.startswith("dmf::k_bk_fuse") else 40
-    c1, s1, k1 = f.run(other)
-    assert k0 != k1
-    assert np.array_equal(s0[:4], s1[:4])
-    assert f.torch.equal(c0, c1)
+    # the other exact kernels: k_fuse_l (or the slab-walk brick pipeline when the default is
+    # k_fuse_l) and the per-cell-walk brick pipeline (variant 40)
+    for other in (31 if k0.startswith("dmf::k_bk_fuse") else 44, 40):
+        c1, s1, k1 = f.run(other)
+        assert k0 != k1
+        assert np.array_equal(s0[:4], s1[:4])
+        assert f.torch.equal(c0, c1)
+        del c1
     if cfg == "config3":  # the default path splits 256 frames into pose batches
         assert k0.startswith("dmf::k_bk_fuse")
 
@@ -137,9 +140,9 @@ def test_config3_batches_equal_single_batch(monkeypatch):
     """Config 3's frames through the brick pipeline in batches of 7 poses == the budget's
     default batching (pose batches accumulate into the same counters)."""
     f = Fusion(512, 1280, 720, 48, seed=99)
-    c0, s0, _ = f.run(40)
+    c0, s0, _ = f.run(44)
     monkeypatch.setenv("DMF_BK_BATCH_POSES", "7")
-    c1, s1, _ = f.run(40)
+    c1, s1, _ = f.run(44)
     assert np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
 
 
@@ -173,7 +176,7 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
     d_poses = torch.from_numpy(poses).to(dev)
     out = {}
     try:
-        for variant in (40, 31):
+        for variant in (44, 40, 31):
             _lib.check(L.dmf_fuse_set_variant(variant))
             c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
             st = torch.zeros(8, dtype=torch.int64, device=dev)
@@ -183,9 +186,10 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
             out[variant] = (c, st.cpu().numpy(), L.dmf_fuse_kernel().decode())
     finally:
         _lib.check(L.dmf_fuse_set_variant(0))
-    (c0, s0, k0), (c1, s1, k1) = out[40], out[31]
-    assert k0.startswith("dmf::k_bk_fuse") and k1.startswith("dmf::k_fuse_l")
+    (c0, s0, k0), (c1, s1, k1), (c2, s2, k2) = out[44], out[31], out[40]
+    assert k0.startswith("dmf::k_bk_fuse_s") and k1.startswith("dmf::k_fuse_l") and k2.startswith("dmf::k_bk_fuse<")
     assert s0[0] > 10 ** 8 and np.array_equal(s0[:4], s1[:4]) and torch.equal(c0, c1)
+    assert np.array_equal(s0[:4], s2[:4]) and torch.equal(c0, c2)
     # one frame against the oracle
     ov = oracle.Volume()
     ov.setDimensions(*bounds)
@@ -193,7 +197,7 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
     ov.constructVolume()
     ho, mo, _ = oracle.fuse_depth(ov, K, depth[2:3], poses[2:3], dmin=scene.DEPTH_MIN_MM, dmax=scene.DEPTH_MAX_MM,
                                   threads=16)
-    _lib.check(L.dmf_fuse_set_variant(40))
+    _lib.check(L.dmf_fuse_set_variant(44))
     try:
         c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
         _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth[2].data_ptr(), d_poses[2].data_ptr(), 1,

@@ -580,14 +580,15 @@ def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
             L.dmf_device_free(h, p_)
 
 
-@pytest.fixture(params=[40, 41, 42, 43])
+@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47])
 def brick_variant(dmf, request):
-    """Select a brick-owned fusion variant (DMF_FUSE_VARIANT 40-43: refill threshold
-    and pair order) for one test."""
+    """Select a brick-owned fusion variant for one test: DMF_FUSE_VARIANT 40-43 = the
+    per-cell walk (k_bk_fuse: refill threshold, pair order, interleaving), 44-47 = the
+    slab walk (k_bk_fuse_s, the default: unroll and refill threshold)."""
     from dmf_amd import _lib
     L = _lib.load()
     _lib.check(L.dmf_fuse_set_variant(request.param))
-    assert L.dmf_fuse_kernel().decode().startswith("dmf::k_bk_fuse<")
+    assert L.dmf_fuse_kernel().decode().startswith("dmf::k_bk_fuse_s<" if request.param >= 44 else "dmf::k_bk_fuse<")
     yield
     _lib.check(L.dmf_fuse_set_variant(0))
 
@@ -670,7 +671,7 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
     _lib.check(L.dmf_memcpy_h2d(h, dp, poses.ctypes.data, poses.nbytes))
     out = {}
     try:
-        for variant in (0, 31):
+        for variant in (0, 31, 40):
             _lib.check(L.dmf_fuse_set_variant(variant))
             _lib.check(L.dmf_memset_device(h, dc, 0, 8 * nt))
             _lib.check(L.dmf_memset_device(h, ds, 0, 64))
@@ -684,16 +685,17 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
         _lib.check(L.dmf_fuse_set_variant(0))
         for ptr_ in (dd, dp, dc, ds):
             L.dmf_device_free(h, ptr_)
-    (c0, s0), (c1, s1) = out[0], out[31]
-    assert np.array_equal(s0[:4], s1[:4]) and s0[3] == 0 and s0[0] > 10 ** 8
-    assert np.array_equal(c0, c1)
+    (c0, s0), (c1, s1), (c2, s2) = out[0], out[31], out[40]
+    assert np.array_equal(s0[:4], s1[:4]) and np.array_equal(s0[:4], s2[:4]) and s0[3] == 0 and s0[0] > 10 ** 8
+    assert np.array_equal(c0, c1) and np.array_equal(c0, c2)
     assert int(c0.astype(np.int64).sum()) == int(s0[0])  # hits + misses == cell updates
     assert int(c0[:nt].astype(np.int64).sum()) == int(s0[2])  # one hit per ray ending inside
 
 
 def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch):
-    """The brick pipeline (variant 40) split into several pose batches (DMF_BK_BATCH_POSES=2 over 5
-    frames: batches of 2, 2, 1) accumulates the same counters as the oracle."""
+    """The brick pipeline (variants 44 = slab walk, 40 = per-cell walk) split into several pose
+    batches (DMF_BK_BATCH_POSES=2 over 5 frames: batches of 2, 2, 1) accumulates the same
+    counters as the oracle."""
     poses, depth, _ = Hh.frames()
     poses, depth = poses[:5], depth[:5]
     ov = Hh.oracle_volume(oracle, n=80, clouds=[])
@@ -702,10 +704,11 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch):
     from dmf_amd import _lib
     L = _lib.load()
     monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
-    _lib.check(L.dmf_fuse_set_variant(40))  # the brick pipeline at this small grid
-    try:
-        hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
-        assert L.dmf_fuse_kernel().decode() == "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>"
-    finally:
-        _lib.check(L.dmf_fuse_set_variant(0))
-    assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
+    for variant, name in ((44, "dmf::k_bk_fuse_s<16, 8, 4, 1>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
+        _lib.check(L.dmf_fuse_set_variant(variant))  # the brick pipeline at this small grid
+        try:
+            hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
+            assert L.dmf_fuse_kernel().decode() == name
+        finally:
+            _lib.check(L.dmf_fuse_set_variant(0))
+        assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
