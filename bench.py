@@ -17,10 +17,15 @@ torch.distributed.run (one rank per GPU, RCCL over xGMI).  Rank 0 prints ONE JSO
 from __future__ import annotations
 
 import argparse
+import csv
 import ctypes as C
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -40,6 +45,9 @@ GRID = 512
 WIDTH, HEIGHT = 640, 480
 POSES_PER_GPU = 128
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMD-32 x one wave64 VALU instruction per 2 cycles at 2.4 GHz
+# (MI355X_MICROARCH.md "Wave scheduling"), in wave-instructions/s
+VALU_PEAK_WIPS = 256 * 4 * 2.4e9 / 2
 BYTES_PER_UPDATE = 4   # int16 read + int16 write per cell update
 BYTES_PER_DEPTH = 2    # uint16 depth read per pixel
 
@@ -96,20 +104,87 @@ def cpu_baseline(K, poses, depth, n_frames, grid, threads=1):
     return float(st[0]) / dt, float(st[1]) / dt, dt
 
 
-def pmc_traffic(grid, poses, image, kernel):
-    """HBM bytes per fusion launch measured by rocprofv3 PMC passes of this exact
-    configuration and kernel (profiles/pmc_traffic.json, written by tools/pmc_summary.py
-    from tools/profile_round.sh runs; FETCH_SIZE x2 + WRITE_SIZE per the MI355X guide), or
-    (None, None) when this configuration has not been profiled."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+# PMC passes of the live measurement (one rocprofv3 run each; FETCH_SIZE takes 3 of the 4
+# TCC slots and WRITE_SIZE 2, so they cannot share a pass: MI355X_MICROARCH.md §PMC slots)
+PMC_PASSES = (["FETCH_SIZE"], ["WRITE_SIZE"],
+              ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+               "SQ_LDS_BANK_CONFLICT", "TCC_HIT_sum", "TCC_MISS_sum"])
+
+
+def pmc_measure(args, log_dir=None):
+    """HBM traffic and instruction counts of THIS configuration, measured now: the same
+    workload (one step, one fusion call, the secondary kernels) re-run as a child process
+    under `rocprofv3 --pmc`, one pass per counter group.  Returns {kernel: {counter:
+    (total, dispatches)}} or None when rocprofv3 is unavailable or a pass fails (the bench
+    line then reports traffic null).  Traffic is corrected as MI355X_MICROARCH.md
+    prescribes for gfx950: bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024."""
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    tmp = tempfile.mkdtemp(prefix="dmf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    child = [sys.executable, os.path.abspath(__file__), "--pmc", "off", "--steps", "1", "--warmup", "0",
+             "--cpu-frames", "0", "--grid", str(args.grid), "--poses-per-gpu", str(args.poses_per_gpu),
+             "--image", args.image] + (["--no-secondary"] if args.no_secondary else [])
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.setdefault("TMPDIR", "/tmp")
+    out = {}
     try:
-        table = json.load(open(path))
-    except (OSError, ValueError):
-        return None, None
-    for e in table:
-        if (e.get("grid"), e.get("poses"), e.get("image"), e.get("kernel")) == (grid, poses, image, kernel):
-            return e.get("hbm_bytes_per_launch"), e.get("profile")
-    return None, None
+        for i, counters in enumerate(PMC_PASSES):
+            d = os.path.join(tmp, f"p{i}")
+            cmd = [prof, "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", "run", "--"] + child
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, timeout=300)
+            if r.returncode != 0:
+                log(f"pmc pass {counters} failed ({r.returncode}): {r.stderr.decode(errors='replace')[-400:]}")
+                return None
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if not files:
+                return None
+            for f in files:
+                for row in csv.DictReader(open(f)):
+                    k = row["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+                    if not k.startswith("dmf::"):
+                        continue
+                    e = out.setdefault(k, {}).setdefault(row["Counter_Name"], [0.0, set()])
+                    e[0] += float(row["Counter_Value"])
+                    e[1].add(row["Dispatch_Id"])
+        if log_dir:
+            shutil.copytree(tmp, log_dir, dirs_exist_ok=True)
+    except (OSError, subprocess.SubprocessError, ValueError, KeyError) as ex:
+        log(f"pmc measurement skipped: {ex}")
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return {k: {c: (v[0], len(v[1])) for c, v in cs.items()} for k, cs in out.items()}
+
+
+def pmc_total(pmc, kernels, counter):
+    """Sum over the kernels of a counter's total (all dispatches of the child run)."""
+    return sum(pmc.get(k, {}).get(counter, (0.0, 0))[0] for k in kernels)
+
+
+def pmc_per_dispatch(pmc, kernel, counter):
+    t, n = pmc.get(kernel, {}).get(counter, (0.0, 0))
+    return t / n if n else None
+
+
+def issue_roofline(pmc, kernel, ms):
+    """Issue-bound pricing of a march kernel (its occupancy bitmask is L2-resident, so HBM
+    bytes say nothing): VALU wave-instructions per launch / launch time vs the VALU issue
+    peak, with the L2 hit rate beside it."""
+    valu = pmc_per_dispatch(pmc, kernel, "SQ_INSTS_VALU") if pmc else None
+    if not valu or not ms:
+        return None
+    hit = pmc_per_dispatch(pmc, kernel, "TCC_HIT_sum") or 0.0
+    miss = pmc_per_dispatch(pmc, kernel, "TCC_MISS_sum") or 0.0
+    ach = valu / (ms * 1e-3)
+    return {"bound": "valu-issue", "achieved": ach, "peak": VALU_PEAK_WIPS, "unit": "wave-instr/s",
+            "frac": ach / VALU_PEAK_WIPS, "kernel": kernel, "valu_per_launch": valu,
+            "salu_per_launch": pmc_per_dispatch(pmc, kernel, "SQ_INSTS_SALU"),
+            "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None,
+            "hbm_bytes_per_launch": 1024.0 * (2.0 * (pmc_per_dispatch(pmc, kernel, "FETCH_SIZE") or 0.0)
+                                              + (pmc_per_dispatch(pmc, kernel, "WRITE_SIZE") or 0.0)),
+            "basis": "rocprofv3 PMC of the same workload in a child run; peak = 1024 SIMD-32 x 1 wave64 VALU "
+                     "instruction / 2 cycles x 2.4 GHz"}
 
 
 def one_rccl_mapped():
@@ -144,6 +219,12 @@ def main():
     ap.add_argument("--poses-per-gpu", type=int, default=POSES_PER_GPU)
     ap.add_argument("--cpu-frames", type=int, default=8, help="frames in the CPU-oracle baseline sample (0=skip)")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "off"],
+                    help="auto: at N=1, measure HBM traffic and instruction counts of this workload with "
+                         "rocprofv3 PMC passes (child runs) after the timed region")
+    ap.add_argument("--pmc-dir", default=None, help="keep the rocprofv3 PMC output here")
+    ap.add_argument("--cpu-reverse-poses", type=int, default=16,
+                    help="poses of the multi-core reverseRayTraceFast CPU sample (0 = skip both samples)")
     ap.add_argument("--image", default="640x480", choices=["640x480", "1280x720"],
                     help="depth frame size (BASELINE configs 1/2/4: 640x480; 3/5: 1280x720)")
     args = ap.parse_args()
@@ -220,11 +301,11 @@ def main():
 
     def merge(b, i):
         c = bufs[b]
-        if comm_ptr is not None:
+        if comm_ptr is not None or world == 1:
+            # N = 1: no communicator, the finalize alone (on the comm stream, behind fuse(i+1))
             D.merge_finalize_device(vol, c, pprm, logodds, comm_ptr, rt.lanes["comm"].cuda_stream)
         else:
-            if world > 1:
-                dist.all_reduce(c, op=dist.ReduceOp.SUM)  # fallback: torch's RCCL all-reduce
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)  # fallback: torch's RCCL all-reduce
             _lib.check(L.dmf_fuse_finalize_device(vol._h, c.data_ptr(), c.data_ptr() + 4 * npad, pprm,
                                                   logodds.data_ptr()))
 
@@ -283,8 +364,8 @@ def main():
     if rank == 0:
         secondary = {}
         if not args.no_secondary:
-            secondary = secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K)
-        traffic, traffic_src = pmc_traffic(grid, P, f"{WIDTH}x{HEIGHT}", L.dmf_fuse_kernel().decode())
+            secondary = secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses, depth,
+                                          cpu_poses=args.cpu_reverse_poses if world == 1 else 0)
         cpu = cpu_mt = None
         if args.cpu_frames > 0 and world == 1:
             ups, rps, dt = cpu_baseline(K, poses, depth, args.cpu_frames, grid)
@@ -300,8 +381,10 @@ def main():
         ms = elapsed / args.steps * 1e3
         kname = L.dmf_fuse_kernel().decode()
         if kname.startswith("dmf::k_bk_fuse"):
-            # brick-owned pipeline (DESIGN.md §5.6): kernel_ms spans all four launches
-            pipeline = ["dmf::k_bk_rays", "dmf::k_bk_scan", "dmf::k_bk_pairs", kname]
+            # brick-owned pipeline (DESIGN.md §5.6-5.7): kernel_ms spans all four launches
+            pipeline = ["dmf::k_bk_rays", "dmf::k_bk_scan",
+                        "dmf::k_bk_pairs<true>" if kname.startswith("dmf::k_bk_fuse_s") else "dmf::k_bk_pairs<false>",
+                        kname]
             diagnostics = {"pairs": int(st[4]) // args.steps, "parts": int(st[5]) // args.steps,
                            "flushed_cells": int(st[6]) // args.steps,
                            "updates_per_pair": float(st[0]) / max(float(st[4]), 1.0),
@@ -343,14 +426,13 @@ def main():
             "fuse_diagnostics": diagnostics,
             "updates_per_ray": updates / max(rays, 1.0),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "basis": "effective (algorithmic): SURVEY.md 8d bytes, 4 B per cell update + 2 B per depth "
                                   "pixel, over the fusion launch's HIP-event time; the brick pipeline accumulates "
                                   "in LDS, so these bytes are a price, not its HBM traffic",
-                         "measured_frac": (traffic / (fuse_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                         "traffic_source": traffic_src,
+                         "measured_frac": None, "traffic_source": None,
                          "kernel": kname, "kernel_ms": fuse_ms, "pipeline": pipeline,
-                         "algorithmic_bytes_per_launch": bytes_launch},
+                         "updates_per_launch": upd_launch, "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,
             "step_breakdown_ms": breakdown,
@@ -361,13 +443,85 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     vol.close()
+    del bufs, logodds, d_depth
+    torch.cuda.empty_cache()
+    if result is not None and world == 1 and args.pmc == "auto":
+        attach_pmc(result, pmc_measure(args, args.pmc_dir))
     if result is not None:
         os.write(json_fd, (json.dumps(result) + "\n").encode())
 
 
-def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16):
+def attach_pmc(result, pmc):
+    """Fill the bench line's measured fields from a pmc_measure() run: HBM traffic per
+    fusion launch (all kernels of the fusion call), VALU/SALU instructions per launch, and
+    the issue-bound pricing of the secondary march kernels."""
+    rf = result["roofline"]
+    if not pmc:
+        rf["traffic_source"] = "not measured (rocprofv3 unavailable or a PMC pass failed)"
+        return
+    fk = [k for k in pmc if k.startswith(("dmf::k_bk_", "dmf::k_fuse"))]
+    calls = 1  # the child run makes one fusion call (steps 1, warmup 0)
+    fetch, write = pmc_total(pmc, fk, "FETCH_SIZE"), pmc_total(pmc, fk, "WRITE_SIZE")
+    traffic = 1024.0 * (2.0 * fetch + write) / calls
+    valu = pmc_total(pmc, fk, "SQ_INSTS_VALU") / calls
+    rf["traffic"] = traffic
+    rf["measured_frac"] = traffic / (rf["kernel_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+    rf["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes of this configuration (child runs after "
+                            "the timed region), (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per fusion call, summed over "
+                            + ", ".join(sorted(fk)))
+    rf["per_kernel_hbm_bytes"] = {k: 1024.0 * (2.0 * pmc_total(pmc, [k], "FETCH_SIZE") + pmc_total(pmc, [k], "WRITE_SIZE"))
+                                  / calls for k in sorted(fk)}
+    rf["valu_per_launch"] = valu
+    rf["valu_issue_frac"] = valu / (rf["kernel_ms"] * 1e-3) / VALU_PEAK_WIPS
+    rf["valu_lane_slots_per_update"] = valu * 64.0 / max(rf["updates_per_launch"], 1.0)
+    sec = result.get("secondary") or {}
+    for name, prefix in (("reverse_ray_trace_fast", "dmf::k_reverse_q"), ("forward_first_hits", "dmf::k_forward")):
+        if name not in sec:
+            continue
+        ks = [k for k in pmc if k == prefix or k.startswith(prefix + "<")]
+        if ks:
+            sec[name]["roofline"] = issue_roofline(pmc, ks[0], sec[name].get("kernel_ms") or sec[name]["ms_per_batch"])
+
+
+def reverse_cpu_baseline(grid, K, poses, pts, nrm, n_threads, n_poses):
+    """The reference's own hot function on the host: oracle reverseRayTraceFast, a line-by-line
+    restatement in the reference's layout (vector<vector<vector<Voxel*>>>, unordered_set
+    lookups, 1 mm march) WITH the dead getNeighborHashes(K=5) work the reference does per
+    voxel (RayTracingEngine.hpp:136-226, 170-171), over the same integrated volume: one pose
+    single-threaded, then n_poses poses over n_threads threads (one pose per thread; the
+    reference itself is single-threaded).  Unit: voxel-pose evaluations/s (occupied voxels x
+    poses / s), the same as the GPU line beside it."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    ov = O.Volume()
+    ov.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    ov.setVolumeSize(grid, grid, grid)
+    ov.constructVolume()
+    ov.integratePointCloud(pts, nrm)
+    V = len(ov.occupied_cells_)
+    eng = O.Engine(K)
+    t0 = time.perf_counter()
+    eng.reverseRayTraceFast(ov, poses[0], False, dead_work=True)
+    dt1 = time.perf_counter() - t0
+    out = {"value": V / dt1, "unit": "voxel-pose evaluations/s", "cores": 1, "kind": "port",
+           "sample": f"oracle reverseRayTraceFast (reference layout, dead getNeighborHashes kept) of 1 of the "
+                     f"{len(poses)} poses over the same {V}-voxel volume, {dt1:.1f}s single-threaded"}
+    if n_poses > 0 and n_threads > 1:
+        sel = [poses[i % len(poses)] for i in range(n_poses)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(n_threads) as ex:  # ctypes calls release the GIL
+            list(ex.map(lambda T: eng.reverseRayTraceFast(ov, T, False, dead_work=True), sel))
+        dtm = time.perf_counter() - t0
+        out["multicore"] = {"value": V * n_poses / dtm, "unit": "voxel-pose evaluations/s", "cores": n_threads,
+                            "kind": "port", "sample": f"{n_poses} poses on {n_threads} threads (one pose per "
+                                                      f"thread), {dtm:.1f}s"}
+    return out
+
+
+def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses_h, depth_h, n_int=16, cpu_poses=16):
     """reverseRayTraceFast (RayTracingEngine.hpp:136-226) throughput for the same poses over a
-    volume integrated from n_int back-projected frames (march samples/s, voxel-rays/s)."""
+    volume integrated from n_int back-projected frames (march samples/s, voxel-rays/s), with
+    the reference-layout CPU port timed beside it (cpu_poses > 0)."""
     import ctypes as C
     H, W = HEIGHT, WIDTH
     xyz = torch.empty((n_int, H, W, 3), dtype=torch.float32, device=dev)
@@ -428,9 +582,8 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16
     fwd_samples = float(fst.cpu().numpy()[0])
     forward = {"rays": P * H * W, "ms_per_batch": fwd_ms, "march_samples_per_s": fwd_samples / (fwd_ms * 1e-3),
                "mrays_per_s": P * H * W / (fwd_ms * 1e-3) / 1e6,
-               "roofline": {"bound": "hbm", "achieved": 2.0 * fwd_samples / (fwd_ms * 1e-3) / 1e9,
-                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": 2.0 * fwd_samples / (fwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+               "roofline": None,  # issue-bound pricing from the PMC passes (attach_pmc)
+               "algorithmic_bytes_per_launch": 2.0 * fwd_samples}
     # set-cover consumer (Algorithms.hpp:38-86) over the same good sets
     sel = np.zeros(P, np.int32)
     nsel = C.c_int32()
@@ -462,6 +615,10 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16
     torch.cuda.synchronize(dev)
     cm_ms = h0.elapsed_time(h1)
     collided = int((cmap == 0x7FFFFFFF).sum().item())
+    rev_cpu = None
+    if cpu_poses > 0:
+        rev_cpu = reverse_cpu_baseline(vol.dims[0], K, poses_h, pts.cpu().numpy(), d_nrm.cpu().numpy(),
+                                       host_threads(), cpu_poses)
     return {"greedy_set_cover": {"candidates": P, "selected": int(nsel.value), "ms": cover_ms},
             "collision_cost_map": {"centres": Vc, "pairs": Vc * Vc, "collided_pairs": collided, "ms": cm_ms,
                                    "pairs_per_s": Vc * Vc / (cm_ms * 1e-3)},
@@ -470,8 +627,11 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, n_int=16
         "occupied_voxels": int(V), "poses": P, "ms_per_batch": ms,
         "first_call_ms": first_ms, "note": "first call after integration includes the brick distance field build",
         "march_samples_per_s": float(s[0]) / (ms * 1e-3), "voxel_rays_per_s": float(s[1]) / (ms * 1e-3),
-        "roofline": {"bound": "hbm", "achieved": bytes_launch / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": bytes_launch / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}}
+        "voxel_pose_evaluations_per_s": float(V) * P / (ms * 1e-3),
+        "cpu_baseline": rev_cpu,
+        "roofline": None,  # issue-bound pricing from the PMC passes (attach_pmc); the march reads an
+                           # L2-resident bitmask, so SURVEY 8d's 2 B per sample is reported, not a bound:
+        "algorithmic_bytes_per_launch": bytes_launch}}
 
 
 if __name__ == "__main__":

@@ -126,8 +126,8 @@ int dmf_fuse_merge_finalize_device(dmf_volume* v, int32_t* d_counters, const dmf
   DMF_TRY(require_constructed(v));
   const hipStream_t st = stream ? (hipStream_t)stream : v->stream;
   if (!d_counters || !prm || !d_logodds) return fail(DMF_ERR_INVALID, "null argument");
-  int nr, rk;
-  DMF_TRY(comm_shape(comm, &nr, &rk));
+  int nr = 1, rk = 0;
+  if (comm) DMF_TRY(comm_shape(comm, &nr, &rk));  // NULL: one rank, no collective
   int64_t ntx, tpr;
   tile_rows(v, &ntx, &tpr);
   const int64_t rows = rows_per_rank(v, nr);
@@ -135,16 +135,18 @@ int dmf_fuse_merge_finalize_device(dmf_volume* v, int32_t* d_counters, const dmf
   const size_t chunk = (size_t)(rows * tpr * 16);  // this rank's reduced slab of each
   int32_t* d_hits = d_counters;
   int32_t* d_miss = d_counters + n_pad;
-  DMF_NCCL(ncclGroupStart());
-  DMF_NCCL(ncclReduceScatter(d_hits, d_hits + rk * chunk, chunk, ncclInt32, ncclSum, (ncclComm_t)comm, st));
-  DMF_NCCL(ncclReduceScatter(d_miss, d_miss + rk * chunk, chunk, ncclInt32, ncclSum, (ncclComm_t)comm, st));
-  DMF_NCCL(ncclGroupEnd());
+  if (comm) {
+    DMF_NCCL(ncclGroupStart());
+    DMF_NCCL(ncclReduceScatter(d_hits, d_hits + rk * chunk, chunk, ncclInt32, ncclSum, (ncclComm_t)comm, st));
+    DMF_NCCL(ncclReduceScatter(d_miss, d_miss + rk * chunk, chunk, ncclInt32, ncclSum, (ncclComm_t)comm, st));
+    DMF_NCCL(ncclGroupEnd());
+  }
   // the rank's slab: tile rows [rk*rows, (rk+1)*rows) clipped to the grid
   const int64_t r0 = std::min<int64_t>(ntx, rk * rows), r1 = std::min<int64_t>(ntx, (rk + 1) * rows);
   DMF_TRY(finalize_tiles(v, d_hits, d_miss, prm, d_logodds, r0 * tpr, r1 * tpr, st));
   // int16 slabs of 2*rows x-rows each, gathered in rank order (bytes: RCCL has no int16)
   const size_t slab = (size_t)(rows * 2 * (int64_t)v->ydim * v->zdim) * sizeof(int16_t);
-  DMF_NCCL(ncclAllGather((const char*)d_logodds + rk * slab, d_logodds, slab, ncclUint8, (ncclComm_t)comm, st));
+  if (comm) DMF_NCCL(ncclAllGather((const char*)d_logodds + rk * slab, d_logodds, slab, ncclUint8, (ncclComm_t)comm, st));
   return DMF_OK;
   DMF_API_END
 }

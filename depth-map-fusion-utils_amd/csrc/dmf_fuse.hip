@@ -1618,9 +1618,9 @@ static int fuse_variant() {
   return v;
 }
 constexpr int kVariantBrick = 40;
-constexpr int kVariantSlab = 44;  // 44..47: slab walk (k_bk_pairs<true> + k_bk_fuse_s); 40..43: per-cell walk
-static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantSlab + 3; }
-static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantSlab + 3); }
+constexpr int kVariantSlab = 44;  // 44..49: slab walk (k_bk_pairs<true> + k_bk_fuse_s); 40..43: per-cell walk
+static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantSlab + 5; }
+static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantSlab + 5); }
 static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
 
 static BkGeom brick_geom(const Geom& g) {
@@ -1780,9 +1780,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
       case 42: DMF_BK_FUSE(32, 8, 8, 2, 0, false); break;
       case 43: DMF_BK_FUSE(16, 8, 8, 1, 256, true); break;
-      case 45: DMF_BK_FUSE_S(32, 8, 4, 2); break;
-      case 46: DMF_BK_FUSE_S(24, 8, 3, 2); break;
-      case 47: DMF_BK_FUSE_S(32, 8, 2, 2); break;
+      case 45: DMF_BK_FUSE_S(24, 8, 4, 1); break;
+      case 46: DMF_BK_FUSE_S(32, 8, 4, 1); break;
+      case 47: DMF_BK_FUSE_S(40, 8, 4, 1); break;
+      case 48: DMF_BK_FUSE_S(24, 8, 3, 1); break;
+      case 49: DMF_BK_FUSE_S(32, 8, 4, 2); break;
       default: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // 0, 44
     }
 #undef DMF_BK_FUSE
@@ -1842,9 +1844,11 @@ static const char* variant_name(int v) {
     case 41: return "dmf::k_bk_fuse<16, 8, 8, 1, 0, false>";
     case 42: return "dmf::k_bk_fuse<32, 8, 8, 2, 0, false>";
     case 43: return "dmf::k_bk_fuse<16, 8, 8, 1, 256, true>";
-    case 45: return "dmf::k_bk_fuse_s<32, 8, 4, 2>";
-    case 46: return "dmf::k_bk_fuse_s<24, 8, 3, 2>";
-    case 47: return "dmf::k_bk_fuse_s<32, 8, 2, 2>";
+    case 45: return "dmf::k_bk_fuse_s<24, 8, 4, 1>";
+    case 46: return "dmf::k_bk_fuse_s<32, 8, 4, 1>";
+    case 47: return "dmf::k_bk_fuse_s<40, 8, 4, 1>";
+    case 48: return "dmf::k_bk_fuse_s<24, 8, 3, 1>";
+    case 49: return "dmf::k_bk_fuse_s<32, 8, 4, 2>";
     default: return "dmf::k_bk_fuse_s<16, 8, 4, 1>";  // 0, 44; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
 }

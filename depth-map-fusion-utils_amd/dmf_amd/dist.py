@@ -180,7 +180,8 @@ def merge_finalize_gloo(counters, dims, prm, logodds, group=None):
 
 def merge_finalize_device(vol, counters, prm_ptr, logodds, comm_ptr, stream_ptr=None):
     """GPU: libdmf's dmf_fuse_merge_finalize_device over an RCCL communicator (e.g. torch's
-    ProcessGroupNCCL._comm_ptr()) on stream_ptr (None = the volume's stream)."""
+    ProcessGroupNCCL._comm_ptr(); None = a single rank: the finalize alone) on stream_ptr (None = the
+    volume's stream)."""
     from . import _lib
     _lib.check(vol._L.dmf_fuse_merge_finalize_device(vol._h, counters.data_ptr(), prm_ptr, logodds.data_ptr(),
                                                      comm_ptr, stream_ptr))

@@ -275,7 +275,8 @@ int dmf_fuse_allreduce_device(dmf_volume* v, int32_t* d_counters, int64_t n_per_
 /* Merge + finalize: reduce-scatter(sum) of hits and of misses over whole tile rows, this
  * rank finalizes its slab, all-gather of the int16 slabs: every rank ends with the full
  * log-odds grid in d_logodds (x-major; the first xdim*ydim*zdim of the padded buffer).
- * d_counters: padded [hits | misses]; afterwards only this rank's slab holds sums. */
+ * d_counters: padded [hits | misses]; afterwards only this rank's slab holds sums.
+ * comm = NULL: a single rank (no collective): the whole grid is finalized on `stream`. */
 int dmf_fuse_merge_finalize_device(dmf_volume* v, int32_t* d_counters, const dmf_fuse_params* prm,
                                    int16_t* d_logodds, void* comm, void* stream);
 /* Voxel::view / Voxel::good of the replicated occupied list: all-reduce(max) (the

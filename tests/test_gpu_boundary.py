@@ -135,6 +135,13 @@ def test_merge_entry_points_dmf_comm_world1(n):
                                                     side.cuda_stream))
         torch.cuda.synchronize(dev)
         assert torch.equal(lo[: n ** 3], ref)
+        # no communicator = a single rank: the finalize alone, on the given stream (bench N=1)
+        lo1 = torch.full((nlo.value,), 12345, dtype=torch.int16, device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        _lib.check(L.dmf_fuse_merge_finalize_device(vol._h, ref_c.data_ptr(), C.addressof(prm), lo1.data_ptr(), None,
+                                                    side.cuda_stream))
+        torch.cuda.synchronize(dev)
+        assert torch.equal(lo1[: n ** 3], ref)
         # flags: integrate a cloud, set view/good by a query, all-reduce(max) at world 1
         pts, nn = Hh.cloud()
         vol.integratePointCloud(pts, nn)
