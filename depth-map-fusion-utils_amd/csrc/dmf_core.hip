@@ -283,7 +283,7 @@ __global__ void k_enum_flags(Geom g, const uint32_t* __restrict__ occ, const flo
   if (!valid_coords(g, a, b, c)) {
     atomicAdd(hazards, 1ull);  // reference indexes voxels_ out of range here (UB)
   } else {
-    f = occ_test(occ, lin_index(g, a, b, c)) ? 1 : 0;
+    f = occ_test(occ, occ_bit(g, a, b, c)) ? 1 : 0;
   }
   flags[e] = f;
 }
@@ -390,7 +390,8 @@ __global__ void k_assign_slots(Geom g, const int32_t* __restrict__ plin, const i
   hash[slot] = hash_id(x, y, z);
   view[slot] = 0;
   good[slot] = 0;
-  atomicOr(&occ[(uint32_t)lin >> 5], 1u << ((uint32_t)lin & 31));
+  const uint32_t ob = occ_bit(g, x, y, z);
+  atomicOr(&occ[ob >> 5], 1u << (ob & 31));
   const uint32_t bl = ((uint32_t)(x >> bsh) * (uint32_t)nby + (uint32_t)(y >> bsh)) * (uint32_t)nbz + (uint32_t)(z >> bsh);
   atomicOr(&brick[bl >> 5], 1u << (bl & 31));
 }
@@ -819,8 +820,11 @@ int dmf_volume_construct(dmf_volume* v) {
   v->voxel_size = v->xdelta * v->ydelta * v->zdelta;
   v->ncell = (size_t)v->xdim * v->ydim * v->zdim;
   if (v->ncell >= (size_t)0x7fffffff) return fail(DMF_ERR_RANGE, "more than 2^31-1 cells");
-  DMF_HIP(hipMalloc((void**)&v->d_occ, sizeof(uint32_t) * ((v->ncell + 31) / 32 + 1)));
-  DMF_HIP(hipMemsetAsync(v->d_occ, 0, sizeof(uint32_t) * ((v->ncell + 31) / 32 + 1), v->stream));
+  const uint64_t nocc = occ_words(v->geom().n);
+  if (nocc * 32u > (uint64_t)UINT32_MAX)
+    return fail(DMF_ERR_RANGE, "occupancy bitmask over 2^32 bits (grid padded to 8-cell tiles)");
+  DMF_HIP(hipMalloc((void**)&v->d_occ, sizeof(uint32_t) * (nocc + 1)));
+  DMF_HIP(hipMemsetAsync(v->d_occ, 0, sizeof(uint32_t) * (nocc + 1), v->stream));
   {
     const char* e = getenv("DMF_BRICK_SHIFT");  // experiments only; default 8^3 bricks
     v->brick_shift = e ? std::max(0, std::min(5, atoi(e))) : kBrickShiftDefault;
@@ -1001,9 +1005,12 @@ int dmf_volume_export(const dmf_volume* v, int32_t* offsets, float* pts, float* 
   DMF_API_END
 }
 
-__global__ void k_occupancy_dense(const uint32_t* __restrict__ occ, size_t n, uint8_t* __restrict__ out) {
+__global__ void k_occupancy_dense(Geom g, const uint32_t* __restrict__ occ, size_t n, uint8_t* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = occ_test(occ, (uint32_t)i) ? 1 : 0;
+  if (i >= n) return;
+  const uint32_t nyz = (uint32_t)g.n[1] * (uint32_t)g.n[2];
+  const int x = (int)((uint32_t)i / nyz), y = (int)(((uint32_t)i / g.n[2]) % g.n[1]), z = (int)((uint32_t)i % g.n[2]);
+  out[i] = occ_test(occ, occ_bit(g, x, y, z)) ? 1 : 0;
 }
 
 int dmf_volume_occupancy(const dmf_volume* v, uint8_t* dense) {
@@ -1012,7 +1019,7 @@ int dmf_volume_occupancy(const dmf_volume* v, uint8_t* dense) {
   if (!dense) return fail(DMF_ERR_INVALID, "null output");
   void* d;
   DMF_TRY(scratch(v_mut(v), kScOut0, v->ncell, &d));
-  hipLaunchKernelGGL(k_occupancy_dense, dim3((unsigned)((v->ncell + 255) / 256)), dim3(256), 0, v->stream, v->d_occ,
+  hipLaunchKernelGGL(k_occupancy_dense, dim3((unsigned)((v->ncell + 255) / 256)), dim3(256), 0, v->stream, v->geom(), v->d_occ,
                      v->ncell, (uint8_t*)d);
   DMF_LAUNCH_CHECK();
   DMF_HIP(hipMemcpyAsync(dense, d, v->ncell, hipMemcpyDeviceToHost, v->stream));

@@ -148,8 +148,24 @@ __host__ __device__ inline uint64_t hash_id(int x, int y, int z) {
   return ((uint64_t)(int64_t)x << 40) ^ (uint64_t)(int64_t)(y << 20) ^ (uint64_t)(int64_t)z;
 }
 
-__device__ inline bool occ_test(const uint32_t* occ, uint32_t lin) {
-  return (occ[lin >> 5] >> (lin & 31)) & 1u;
+// Occupancy bitmask layout: 8x8x8-cell tiles of 512 bits (16 words = 64 B), tiles x-major
+// over the grid padded to whole tiles, bit (x&7)*64 + (y&7)*8 + (z&7) inside a tile.  A
+// march sample stays in one tile for several samples whatever the ray direction; with
+// x-major bits (one 128-B line = 1024 z-cells of one (x, y) column) a reverse march left
+// the line at nearly every sample: L2 hit rate 0.50 and 43 GB beyond L2 per 128-pose
+// reverseRayTraceFast launch at 512^3.
+__host__ __device__ inline uint32_t occ_bit(const Geom& g, int x, int y, int z) {
+  const uint32_t nty = ((uint32_t)g.n[1] + 7u) >> 3, ntz = ((uint32_t)g.n[2] + 7u) >> 3;
+  const uint32_t t = (((uint32_t)x >> 3) * nty + ((uint32_t)y >> 3)) * ntz + ((uint32_t)z >> 3);
+  return (t << 9) | (((uint32_t)x & 7u) << 6) | (((uint32_t)y & 7u) << 3) | ((uint32_t)z & 7u);
+}
+// 32-bit words of the tiled bitmask (bit indices must fit 32 bits: checked at construction)
+inline uint64_t occ_words(const int n[3]) {
+  return (uint64_t)((n[0] + 7) >> 3) * (uint64_t)((n[1] + 7) >> 3) * (uint64_t)((n[2] + 7) >> 3) * 16u;
+}
+
+__device__ inline bool occ_test(const uint32_t* occ, uint32_t bit) {
+  return (occ[bit >> 5] >> (bit & 31)) & 1u;
 }
 
 // Eigen normalized()
@@ -178,7 +194,7 @@ constexpr int kBrickShiftDefault = 1;    // 2^3-cell bricks (reverse batch: 8.1 
 constexpr int kBrickDistCapDefault = 63;  // brick distance field saturates here (in bricks)
 
 struct DevVol {
-  const uint32_t* occ;     // N-bit occupancy (x-major lin)
+  const uint32_t* occ;     // occupancy bitmask (occ_bit tiles)
   const uint8_t* bdist;    // per brick: L-inf distance in bricks to the nearest occupied brick (0 = occupied), capped
   int bsh;                 // brick edge = 1 << bsh cells
   const uint32_t* brick;   // one bit per brick, x-major over nb[]

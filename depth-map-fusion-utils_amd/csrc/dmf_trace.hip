@@ -69,7 +69,7 @@ __device__ inline bool reverse_march(const Geom& g, const DevVol& vd, const floa
     const int a = bin_axis(g, 0, p[0]), b = bin_axis(g, 1, p[1]), c = bin_axis(g, 2, p[2]);
     if (a == cx && b == cy && c == cz) continue;  // hash == centroid_hash
     if (!valid_coords(g, a, b, c)) return false;
-    if (occ_test(vd.occ, lin_index(g, a, b, c))) return true;
+    if (occ_test(vd.occ, occ_bit(g, a, b, c))) return true;
     if (kSkip) {
       const uint32_t bl = ((uint32_t)(a >> vd.bsh) * (uint32_t)vd.nb[1] + (uint32_t)(b >> vd.bsh)) *
                               (uint32_t)vd.nb[2] + (uint32_t)(c >> vd.bsh);
@@ -237,9 +237,9 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   const int a = bin_axis(g, 0, p[0]), b = bin_axis(g, 1, p[1]), c = bin_axis(g, 2, p[2]);
   if (a == L.cx && b == L.cy && c == L.cz) { ++L.s; return 0; }
   if (!valid_coords(g, a, b, c)) return 2;
-  const uint32_t lin = lin_index(g, a, b, c);
-  if ((lin >> 5) != L.occi) { L.occi = lin >> 5; L.occw = vd.occ[L.occi]; }
-  if ((L.occw >> (lin & 31)) & 1u) return 1;
+  const uint32_t ob = occ_bit(g, a, b, c);
+  if ((ob >> 5) != L.occi) { L.occi = ob >> 5; L.occw = vd.occ[L.occi]; }
+  if ((L.occw >> (ob & 31)) & 1u) return 1;
   const int ba = a >> vd.bsh, bb = b >> vd.bsh, bc = c >> vd.bsh;
   const uint32_t bl = ((uint32_t)ba * (uint32_t)vd.nb[1] + (uint32_t)bb) * (uint32_t)vd.nb[2] + (uint32_t)bc;
   if (bl != L.known_full) {
@@ -664,10 +664,9 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, const uint32_t* __restr
         atomicAdd(hazards, 1ull);
         continue;
       }
-      const uint32_t lin = lin_index(g, a, b, cc);
-      if (occ_test(occ, lin)) {
+      if (occ_test(occ, occ_bit(g, a, b, cc))) {
         kk = k;
-        sl = slot_of[lin];
+        sl = slot_of[lin_index(g, a, b, cc)];
         break;
       }
     }
@@ -909,7 +908,7 @@ __global__ void k_will_collide(Geom g, const uint32_t* __restrict__ occ, const f
     if (!valid_points(g, px, py, pz)) continue;
     const int x = bin_axis(g, 0, px), y = bin_axis(g, 1, py), z = bin_axis(g, 2, pz);
     if (!valid_coords(g, x, y, z)) continue;
-    if (occ_test(occ, lin_index(g, x, y, z))) collided = true;
+    if (occ_test(occ, occ_bit(g, x, y, z))) collided = true;
   }
   out[i] = collided ? 1 : 0;
 }
@@ -955,7 +954,7 @@ __global__ __launch_bounds__(64 * kCostWaves) void k_cost_map(Geom g, const uint
       const float pz = a[2] + div_rn(v[2] * fd, 1000.0f, 1.0f / 1000.0f);
       if (valid_points(g, px, py, pz)) {
         const int x = bin_axis(g, 0, px), y = bin_axis(g, 1, py), z = bin_axis(g, 2, pz);
-        hit = valid_coords(g, x, y, z) && occ_test(occ, lin_index(g, x, y, z));
+        hit = valid_coords(g, x, y, z) && occ_test(occ, occ_bit(g, x, y, z));
       }
     }
     if (__builtin_amdgcn_ballot_w64(hit)) {
