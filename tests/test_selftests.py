@@ -2,7 +2,10 @@
 * tools/brick_selftest.cpp — the brick decomposition of the fusion DDA (dmf_brick.hpp)
   restarts the fine walk on exactly the cells the plain walk visits in each brick;
 * tools/fastdiv_selftest.cpp — div_rn (dmf_internal.hpp) equals IEEE division over the
-  projection and reverse-march domains."""
+  projection and reverse-march domains;
+* ASan + UBSan builds of both self-tests and of the CPU oracle
+  (tools/oracle_sanitize.cpp drives every oracle entry point on a small scene): undefined
+  behaviour or an out-of-bounds access in the checkers fails the CPU suite."""
 import os
 import subprocess
 
@@ -11,10 +14,14 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _build_and_run(src, out, args, extra=()):
+SAN = ["-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"]
+
+
+def _build_and_run(src, out, args, extra=(), opt=("-O2",), more=()):
     exe = os.path.join(out, os.path.basename(src)[:-4])
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", *extra, src, "-o", exe], check=True)
-    return subprocess.run([exe, *args], capture_output=True, text=True, timeout=300)
+    subprocess.run(["g++", *opt, "-std=c++17", "-ffp-contract=off", *extra, src, *more, "-o", exe], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    return subprocess.run([exe, *args], capture_output=True, text=True, timeout=300, env=env)
 
 
 def test_brick_decomposition_selftest(tmp_path):
@@ -29,3 +36,15 @@ def test_fast_division_selftest(tmp_path):
     r = _build_and_run(os.path.join(ROOT, "tools", "fastdiv_selftest.cpp"), str(tmp_path), [])
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 mismatches" in r.stdout
+
+
+@pytest.mark.timeout(300)
+def test_selftests_and_oracle_under_sanitizers(tmp_path):
+    inc = ["-I", os.path.join(ROOT, "depth-map-fusion-utils_amd", "csrc")]
+    r = _build_and_run(os.path.join(ROOT, "tools", "brick_selftest.cpp"), str(tmp_path), ["20000", "11"], inc, SAN)
+    assert r.returncode == 0 and " 0 failures" in r.stdout, r.stdout + r.stderr
+    r = _build_and_run(os.path.join(ROOT, "tools", "fastdiv_selftest.cpp"), str(tmp_path), ["9973"], (), SAN)
+    assert r.returncode == 0 and " 0 mismatches" in r.stdout, r.stdout + r.stderr
+    r = _build_and_run(os.path.join(ROOT, "tools", "oracle_sanitize.cpp"), str(tmp_path), [], ["-fopenmp"], SAN,
+                       [os.path.join(ROOT, "oracle", "oracle.cpp")])
+    assert r.returncode == 0 and "oracle sanitize ok" in r.stdout, r.stdout + r.stderr

@@ -9,8 +9,11 @@
 //      random focal lengths and principal points;
 //   2. float, the reverse march's (v * depth) / 1000.0f (RayTracingEngine.hpp:166-176):
 //      every float n with |n| in [2^-40, 2^40], and +-0.
-// Build: g++ -O2 -ffp-contract=off tools/fastdiv_selftest.cpp ; run: ./a.out
+// Build: g++ -O2 -ffp-contract=off tools/fastdiv_selftest.cpp ; run: ./a.out [stride]
+// (stride > 1 subsamples depths and float bit patterns: the sanitizer build of
+// tests/test_selftests.py; the exhaustive run is stride 1)
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -30,7 +33,8 @@ static float div_rn(float n, float d, float y) {
   return n == 0.0f ? q0 : q;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const int stride = argc > 1 ? std::atoi(argv[1]) : 1;
   long bad = 0, checked = 0;
   // 1. double projection quotients
   std::mt19937_64 rng(7);
@@ -45,7 +49,7 @@ int main() {
   while (nc < 64) { cams[nc][0] = (double)(float)uf(rng); cams[nc][1] = (double)(float)uc(rng); ++nc; }
   for (int k = 0; k < nc; ++k) {
     const double d = cams[k][0], c = cams[k][1], y = 1.0 / d;
-    for (int mm = 0; mm <= 1100; ++mm) {
+    for (int mm = 0; mm <= 1100; mm += stride) {
       const double z = mm * 0.001;
       for (int col = 0; col < 2048; ++col) {
         const double n = z * ((double)col - c);
@@ -61,7 +65,7 @@ int main() {
   // 1b. the whole uint16 depth range, every 7th column
   for (int k = 0; k < nc; ++k) {
     const double d = cams[k][0], c = cams[k][1], y = 1.0 / d;
-    for (int mm = 1101; mm <= 65535; ++mm) {
+    for (int mm = 1101; mm <= 65535; mm += stride) {
       const double z = mm * 0.001;
       for (int col = mm % 7; col < 2048; col += 7) {
         const double n = z * ((double)col - c);
@@ -78,7 +82,7 @@ int main() {
   //    range; outside it they divide: near the subnormal range the identity fails, e.g.
   //    n = 2.17e-41)
   const float d = 1000.0f, y = 1.0f / 1000.0f;
-  for (uint32_t bits = ((127u - 40u) << 23); bits < ((127u + 40u) << 23); ++bits) {
+  for (uint32_t bits = ((127u - 40u) << 23); bits < ((127u + 40u) << 23); bits += (uint32_t)stride) {
     for (int s = 0; s < 2; ++s) {
       float n;
       const uint32_t b = bits | (s ? 0x80000000u : 0u);
