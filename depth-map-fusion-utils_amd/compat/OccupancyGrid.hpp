@@ -1,10 +1,9 @@
 // OccupancyGrid.hpp — drop-in for the reference include/OccupancyGrid.hpp:50-318 class
 // API (setDimensions, setResolution, setK, construct, updateStates, downloadCloud,
-// downloadHQCloud) backed by dmf_ogrid_* on the MI355X.  updateStates returns the
-// deterministic single-threaded result of the reference's OpenMP loops.  The dense
-// per-voxel state is on the device (state() copies it); the reference's public
-// voxels_ / voxels_reorganized_ containers and downloadReorganizedCloud are not
-// mirrored.  (The per-voxel struct is not named Voxel here: the reference's two
+// downloadHQCloud, downloadReorganizedCloud) backed by dmf_ogrid_* on the MI355X.
+// updateStates returns the deterministic single-threaded result of the reference's OpenMP
+// loops.  The dense per-voxel state is on the device (state() copies it); the reference's
+// public voxels_ / voxels_reorganized_ containers are not mirrored.  (The per-voxel struct is not named Voxel here: the reference's two
 // headers cannot be included together, this compat set can.)
 #pragma once
 #include <vector>
@@ -12,26 +11,6 @@
 #include "dmf.h"
 #include "dmf_types.hpp"
 #include "Volume.hpp"  // dmf_check
-
-namespace dmf_compat {
-struct PointNormal {
-  float x = 0, y = 0, z = 0;
-  float normal[3] = {0, 0, 0};
-  float curvature = 0;
-};
-struct PointXYZRGBNormal {
-  float x = 0, y = 0, z = 0;
-  uint8_t r = 0, g = 0, b = 0;
-  float normal[3] = {0, 0, 0};
-  float curvature = 0;
-};
-}  // namespace dmf_compat
-#ifndef DMF_COMPAT_REAL_PCL
-namespace pcl {
-using PointNormal = dmf_compat::PointNormal;
-using PointXYZRGBNormal = dmf_compat::PointXYZRGBNormal;
-}  // namespace pcl
-#endif
 
 class OccupancyGrid {
  public:
@@ -86,6 +65,9 @@ class OccupancyGrid {
   bool downloadCloud(OutPtr cloud) { return download(cloud, 0); }
   template <class OutPtr>
   bool downloadHQCloud(OutPtr cloud) { return download(cloud, 1); }
+  // :200-286 (modes 2 / 3 of dmf_ogrid_download: the merged voxels, x-major)
+  template <class OutPtr>
+  bool downloadReorganizedCloud(OutPtr cloud, bool clean = false) { return download(cloud, clean ? 3 : 2); }
 
   dmf_ogrid* handle() { return h_; }
 

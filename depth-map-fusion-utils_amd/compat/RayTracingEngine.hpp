@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "Camera.hpp"
+#include "CommonUtilities.hpp"
 #include "Volume.hpp"
 #include "dmf.h"
 
@@ -14,9 +15,6 @@ constexpr double k_AngleMin = 0;
 constexpr double k_AngleMax = 90;
 constexpr double k_ZMin = 0.20;
 constexpr double k_ZMax = 1.0;
-
-// CommonUtilities.hpp:17
-constexpr int degree(double radian) { return int((radian * 180) / 3.14159); }
 
 class RayTracingEngine {
  public:

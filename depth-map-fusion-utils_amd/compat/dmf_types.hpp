@@ -10,7 +10,12 @@
 #pragma once
 #include <cmath>
 #include <cstdint>
+#include <cstring>
+#include <initializer_list>
 #include <memory>
+#include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 namespace dmf_compat {
@@ -38,6 +43,10 @@ struct Vector3f {
   Vector3f operator*(double s) const { const float f = (float)s; return {v[0] * f, v[1] * f, v[2] * f}; }
   Vector3f operator/(double s) const { const float f = (float)s; return {v[0] / f, v[1] / f, v[2] / f}; }
   float dot(const Vector3f& o) const { return sum3(v[0] * o.v[0], v[1] * o.v[1], v[2] * o.v[2]); }
+  // Eigen cross(): (a1 b2 - a2 b1, a2 b0 - a0 b2, a0 b1 - a1 b0)
+  Vector3f cross(const Vector3f& o) const {
+    return {v[1] * o.v[2] - v[2] * o.v[1], v[2] * o.v[0] - v[0] * o.v[2], v[0] * o.v[1] - v[1] * o.v[0]};
+  }
   float squaredNorm() const { return dot(*this); }
   float norm() const { return std::sqrt(squaredNorm()); }
   Vector3f normalized() const {
@@ -82,23 +91,118 @@ struct Affine3f {
   }
 };
 
+struct PointXYZ {
+  float x = 0, y = 0, z = 0;
+};
+
 struct PointXYZRGB {
   float x = 0, y = 0, z = 0;
   uint8_t r = 0, g = 0, b = 0;
 };
 
+// PCL's normal[3] aliases normal_x, normal_y, normal_z
+#define DMF_COMPAT_NORMAL_FIELDS                   \
+  union {                                          \
+    float normal[3];                               \
+    struct {                                       \
+      float normal_x, normal_y, normal_z;          \
+    };                                             \
+  };
+
 struct Normal {
-  float normal[3] = {0, 0, 0};
+  DMF_COMPAT_NORMAL_FIELDS
   float curvature = 0;
+  Normal() : normal{0, 0, 0} {}
+};
+
+struct PointNormal {
+  float x = 0, y = 0, z = 0;
+  DMF_COMPAT_NORMAL_FIELDS
+  float curvature = 0;
+  PointNormal() : normal{0, 0, 0} {}
+};
+
+struct PointXYZRGBNormal {
+  float x = 0, y = 0, z = 0;
+  uint8_t r = 0, g = 0, b = 0;
+  DMF_COMPAT_NORMAL_FIELDS
+  float curvature = 0;
+  PointXYZRGBNormal() : normal{0, 0, 0} {}
 };
 
 template <class T>
 struct PointCloud {
   std::vector<T> points;
+  uint32_t width = 0, height = 1;
+  bool is_dense = true;
   using Ptr = std::shared_ptr<PointCloud<T>>;
   size_t size() const { return points.size(); }
-  void push_back(const T& p) { points.push_back(p); }
+  bool empty() const { return points.empty(); }
+  void push_back(const T& p) { points.push_back(p); width = (uint32_t)points.size(); height = 1; }
+  T& operator[](size_t i) { return points[i]; }
+  const T& operator[](size_t i) const { return points[i]; }
+  typename std::vector<T>::iterator begin() { return points.begin(); }
+  typename std::vector<T>::iterator end() { return points.end(); }
 };
+
+// PCD field setters (pcl/io/pcd_io.h): rgb arrives as the packed 0x00RRGGBB integer
+inline void set_xyz(float* p, const std::string& n, double v) {
+  if (n == "x") p[0] = (float)v;
+  else if (n == "y") p[1] = (float)v;
+  else if (n == "z") p[2] = (float)v;
+}
+inline void set_rgb(uint8_t& r, uint8_t& g, uint8_t& b, const std::string& n, double v) {
+  if (n != "rgb" && n != "rgba") return;
+  const uint32_t u = (uint32_t)v;
+  r = (uint8_t)(u >> 16); g = (uint8_t)(u >> 8); b = (uint8_t)u;
+}
+inline void set_nrm(float* nr, float& curv, const std::string& n, double v) {
+  if (n == "normal_x") nr[0] = (float)v;
+  else if (n == "normal_y") nr[1] = (float)v;
+  else if (n == "normal_z") nr[2] = (float)v;
+  else if (n == "curvature") curv = (float)v;
+}
+inline void set_field(PointXYZ& p, const std::string& n, double v) { float t[3] = {p.x, p.y, p.z}; set_xyz(t, n, v); p.x = t[0]; p.y = t[1]; p.z = t[2]; }
+inline void set_field(PointXYZRGB& p, const std::string& n, double v) {
+  float t[3] = {p.x, p.y, p.z}; set_xyz(t, n, v); p.x = t[0]; p.y = t[1]; p.z = t[2];
+  set_rgb(p.r, p.g, p.b, n, v);
+}
+inline void set_field(Normal& p, const std::string& n, double v) { set_nrm(p.normal, p.curvature, n, v); }
+inline void set_field(PointNormal& p, const std::string& n, double v) {
+  float t[3] = {p.x, p.y, p.z}; set_xyz(t, n, v); p.x = t[0]; p.y = t[1]; p.z = t[2];
+  set_nrm(p.normal, p.curvature, n, v);
+}
+inline void set_field(PointXYZRGBNormal& p, const std::string& n, double v) {
+  float t[3] = {p.x, p.y, p.z}; set_xyz(t, n, v); p.x = t[0]; p.y = t[1]; p.z = t[2];
+  set_rgb(p.r, p.g, p.b, n, v);
+  set_nrm(p.normal, p.curvature, n, v);
+}
+
+// Float mean of every field of points idx[s..e) (pcl/filters/voxel_grid.h)
+template <class T>
+inline T mean_point(const std::vector<T>& pts, const std::vector<std::pair<int64_t, size_t>>& idx, size_t s, size_t e) {
+  float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  T out = pts[idx[s].second];
+  for (size_t i = s; i < e; ++i) {
+    const T& p = pts[idx[i].second];
+    acc[0] += p.x; acc[1] += p.y; acc[2] += p.z;
+    if constexpr (std::is_same<T, PointXYZRGB>::value || std::is_same<T, PointXYZRGBNormal>::value) {
+      acc[3] += p.r; acc[4] += p.g; acc[5] += p.b;
+    }
+    if constexpr (std::is_same<T, PointXYZRGBNormal>::value) {
+      acc[6] += p.normal[0]; acc[7] += p.normal[1]; acc[8] += p.normal[2]; acc[9] += p.curvature;
+    }
+  }
+  const float n = (float)(e - s);
+  out.x = acc[0] / n; out.y = acc[1] / n; out.z = acc[2] / n;
+  if constexpr (std::is_same<T, PointXYZRGB>::value || std::is_same<T, PointXYZRGBNormal>::value) {
+    out.r = (uint8_t)(acc[3] / n); out.g = (uint8_t)(acc[4] / n); out.b = (uint8_t)(acc[5] / n);
+  }
+  if constexpr (std::is_same<T, PointXYZRGBNormal>::value) {
+    out.normal[0] = acc[6] / n; out.normal[1] = acc[7] / n; out.normal[2] = acc[8] / n; out.curvature = acc[9] / n;
+  }
+  return out;
+}
 
 // rows 0..2 of any Affine3f-like transform (the lite type or real Eigen) as float[12]
 template <class T>
@@ -118,7 +222,10 @@ using Vector3f = dmf_compat::Vector3f;
 
 #ifndef DMF_COMPAT_REAL_PCL
 namespace pcl {
+using PointXYZ = dmf_compat::PointXYZ;
 using PointXYZRGB = dmf_compat::PointXYZRGB;
+using PointXYZRGBNormal = dmf_compat::PointXYZRGBNormal;
+using PointNormal = dmf_compat::PointNormal;
 using Normal = dmf_compat::Normal;
 template <class T>
 using PointCloud = dmf_compat::PointCloud<T>;

@@ -113,8 +113,8 @@ int main(int argc, char** argv) {
     regions_covered.push_back(good_points);
   }
   // tests/SetCover.cpp:236-239 + include/Algorithms.hpp:38-86
-  auto cameras_selected = setCover(engine, volume, camera_locations, resolution_single_dimension);
-  auto again = Algorithms::greedySetCover(volume, regions_covered);
+  auto cameras_selected = dmf_compat::setCoverBatched(engine, volume, camera_locations, resolution_single_dimension);
+  auto again = Algorithms::greedySetCover(regions_covered);
   cout << "selected";
   for (auto s : cameras_selected) cout << " " << s;
   cout << "\nselected_from_sets";

@@ -1,0 +1,3 @@
+// pcl/visualization/cloud_viewer.h for the drop-in build (headless).
+#pragma once
+#include "pcl_visualizer.h"

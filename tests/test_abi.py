@@ -67,9 +67,11 @@ int main() {
   g.updateStates(c, n);
   auto out = std::make_shared<pcl::PointCloud<pcl::PointXYZRGBNormal>>();
   g.downloadHQCloud(out);
+  g.downloadReorganizedCloud(out, true);
   VoxelVolume v;
   std::vector<std::vector<unsigned long long int>> sets;
   auto sel = Algorithms::greedySetCover(v, sets);
+  sel = Algorithms::greedySetCover(sets);  // the reference signature (Algorithms.hpp:38)
   return (int)(out->points.size() + sel.size());
 }
 ''')
