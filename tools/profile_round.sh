@@ -10,12 +10,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-BENCH="python3 bench.py --steps 3 --warmup 1 --cpu-frames 0 ${BENCHARGS}"
+BENCH="python3 bench.py --steps 3 --warmup 1 --cpu-frames 0 --cpu-reverse-poses 0 --pmc off ${BENCHARGS}"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- $BENCH > "$OUT/bench_kt.json" 2> "$OUT/bench_kt.err" || exit 1
 i=0
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" "SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 400 rocprofv3 --pmc $pmc --output-format csv -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-frames 0 --no-secondary ${BENCHARGS} > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || exit 2
+  timeout -k 10 400 rocprofv3 --pmc $pmc --output-format csv -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-frames 0 --no-secondary --pmc off ${BENCHARGS} > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || exit 2
 done
 python3 tools/pmc_summary.py "$OUT" "profiles/$TAG" || exit 3
 echo "profile $TAG collected"
