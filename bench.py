@@ -389,7 +389,7 @@ def main():
         if kname.startswith("dmf::k_bk_fuse"):
             # brick-owned pipeline: kernel_ms spans all four launches
             pipeline = ["dmf::k_bk_rays", "dmf::k_bk_scan",
-                        "dmf::k_bk_pairs<true>" if kname.startswith("dmf::k_bk_fuse_s") else "dmf::k_bk_pairs<false>",
+                        "dmf::k_bk_pairs<true, false>" if kname.startswith("dmf::k_bk_fuse_s") else "dmf::k_bk_pairs<false, true>",
                         kname]
             diagnostics = {"pairs": int(st[4]) // args.steps, "parts": int(st[5]) // args.steps,
                            "flushed_cells": int(st[6]) // args.steps,

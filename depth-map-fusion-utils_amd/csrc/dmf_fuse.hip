@@ -191,14 +191,13 @@ __device__ inline int pixel_ray(const Geom& g, const CamP& cam, const uint16_t* 
 }
 
 // pixel_ray up to the quantised endpoints (the brick path's ray record).
-__device__ inline bool pixel_quant(const Geom& g, const CamP& cam, const uint16_t* __restrict__ depth,
-                                   const PoseX* __restrict__ poses, int p, int r, int c, int dmin, int dmax,
-                                   int64_t qs[3], int64_t qe[3], bool& inside, bool& valid) {
+// As below with the pixel's depth already loaded (d < 0: outside the frame).
+__device__ inline bool pixel_quant_d(const Geom& g, const CamP& cam, int d, const PoseX* __restrict__ poses, int p,
+                                     int r, int c, int dmin, int dmax, int64_t qs[3], int64_t qe[3], bool& inside,
+                                     bool& valid) {
   valid = false;
   inside = false;
-  if (r >= cam.H || c >= cam.W) return false;
-  const int d = depth[((int64_t)p * cam.H + r) * cam.W + c];
-  if (!(d >= dmin && d < dmax)) return false;
+  if (d < 0 || !(d >= dmin && d < dmax)) return false;
   valid = true;
   const PoseX& T = poses[p];
   float pc[3], E[3];
@@ -208,6 +207,16 @@ __device__ inline bool pixel_quant(const Geom& g, const CamP& cam, const uint16_
   if (inside) inside = valid_coords(g, bin_axis(g, 0, E[0]), bin_axis(g, 1, E[1]), bin_axis(g, 2, E[2]));
   const float O[3] = {T.f[3], T.f[7], T.f[11]};
   return dda_quantize(g, O, E, inside, qs, qe);
+}
+
+__device__ inline int pixel_depth(const CamP& cam, const uint16_t* __restrict__ depth, int p, int r, int c) {
+  return (r >= cam.H || c >= cam.W) ? -1 : (int)depth[((int64_t)p * cam.H + r) * cam.W + c];
+}
+
+__device__ inline bool pixel_quant(const Geom& g, const CamP& cam, const uint16_t* __restrict__ depth,
+                                   const PoseX* __restrict__ poses, int p, int r, int c, int dmin, int dmax,
+                                   int64_t qs[3], int64_t qe[3], bool& inside, bool& valid) {
+  return pixel_quant_d(g, cam, pixel_depth(cam, depth, p, r, c), poses, p, r, c, dmin, dmax, qs, qe, inside, valid);
 }
 
 __device__ inline void wave_stats(unsigned long long* stats, unsigned long long upd, unsigned long long ray,
@@ -807,16 +816,18 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int64_t pk0 = (int64_t)blockIdx.x * span, pk1 = min(npackets, pk0 + span);
   unsigned long long upd = 0, nvalid = 0, nhit = 0;
+  // (loading the next packet's depth one packet ahead measured slower: 0.79 -> 0.84 ms)
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
     const int p = (int)(pk / packets_pose);
     const int q = (int)(pk - (int64_t)p * packets_pose);
     const int r = (q / packets_x) * 8 + (l >> 3), c = (q % packets_x) * 8 + (l & 7);
+    const int d = pixel_depth(cam, depth, p, r, c);
     int64_t qs[3], qe[3];
     bool inside, valid;
     ulonglong2 rec;
     rec.x = 0;
     rec.y = 0;
-    if (pixel_quant(g, cam, depth, poses, p, r, c, dmin, dmax, qs, qe, inside, valid)) {
+    if (pixel_quant_d(g, cam, d, poses, p, r, c, dmin, dmax, qs, qe, inside, valid)) {
       uint64_t A, B;
       bk::pack_ray(qs, qe, inside, A, B);
       rec.x = A;
@@ -904,7 +915,12 @@ __device__ inline uint32_t bk_e30(int32_t e) {
 // SLAB (phase F's major-axis walk, k_bk_fuse_s): the E fields hold the
 // slab state (b1, b2, b12) of dmf_brick.hpp instead of (E01, E02, E12), the |dq| fields are
 // in (major, minor1, minor2) order, and pb.y bits 27-28 name the major axis.
-template <bool SLAB>
+// AGG: slots from wave-aggregated LDS atomics (hist_take_agg: one atomic per distinct brick
+// among the wave's lanes, its return broadcast by readlane at once) or, AGG = false (the
+// slab pipeline's default), one LDS atomic per lane whose return is only consumed by the
+// pair's store at the next brick boundary (its latency hides behind that boundary's
+// count_at; B 1.92 -> 1.88 ms).
+template <bool SLAB, bool AGG = true>
 __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
@@ -919,8 +935,13 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int64_t pk0 = (int64_t)blockIdx.x * span, pk1 = min(npackets, pk0 + span);
   constexpr uint32_t m5 = bk::kB - 1;
+  // the next packet's ray record is loaded one packet ahead: its HBM latency hides behind
+  // this packet's coarse walk (B 2.03 -> 1.92 ms) instead of stalling the wave per packet
+  ulonglong2 rnext = make_ulonglong2(0, 0);
+  if (pk0 + w < pk1) rnext = rays[(pk0 + w) * 64 + l];
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
-    const ulonglong2 rec = rays[pk * 64 + l];
+    const ulonglong2 rec = rnext;
+    if (pk + nw < pk1) rnext = rays[(pk + nw) * 64 + l];
     if (!(rec.y >> 63)) continue;
     bk::QRay R;
     bk::decode_ray(rec.x, rec.y, R);
@@ -1000,7 +1021,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets
         cur = entry(c);
         idx = nidx;
       }
-      slot = hist_take_agg(hist, b);
+      slot = AGG ? hist_take_agg(hist, b) : atomicAdd(&hist[b], 1u);
     });
     put(slot, cur, endc, (uint32_t)(R.nsteps - idx), R.end_inside);
   }
@@ -1618,7 +1639,7 @@ static int fuse_variant() {
   return v;
 }
 constexpr int kVariantBrick = 40;
-constexpr int kVariantSlab = 44;  // 44..49: slab walk (k_bk_pairs<true> + k_bk_fuse_s); 40..43: per-cell walk
+constexpr int kVariantSlab = 44;  // 44..49: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
 static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantSlab + 5; }
 static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantSlab + 5); }
 static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
@@ -1708,7 +1729,9 @@ static int bk_attributes() {
                                 (int)(sizeof(uint32_t) * 32768)));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(sizeof(uint32_t) * 32768)));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(uint32_t) * 32768)));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(sizeof(uint32_t) * 32768)));
     attr_set.store(true);
   }
@@ -1759,8 +1782,12 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                        ctlp);
     DMF_LAUNCH_CHECK();
     const int fv = fuse_variant();
-    if (is_slab_variant(fv))
-      hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk, pl.span, bg,
+    if (fv == 48)  // wave-aggregated slot atomics (the previous default)
+      hipLaunchKernelGGL((k_bk_pairs<true, true>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk,
+                         pl.span, bg, (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra,
+                         (uint2*)prb);
+    else if (is_slab_variant(fv))
+      hipLaunchKernelGGL((k_bk_pairs<true, false>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk, pl.span, bg,
                          (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra, (uint2*)prb);
     else
       hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk, pl.span,
@@ -1783,7 +1810,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       case 45: DMF_BK_FUSE_S(24, 8, 4, 1); break;
       case 46: DMF_BK_FUSE_S(32, 8, 4, 1); break;
       case 47: DMF_BK_FUSE_S(40, 8, 4, 1); break;
-      case 48: DMF_BK_FUSE_S(24, 8, 3, 1); break;
+      case 48: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // with k_bk_pairs<true, true>
       case 49: DMF_BK_FUSE_S(32, 8, 4, 2); break;
       default: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // 0, 44
     }
@@ -1847,7 +1874,7 @@ static const char* variant_name(int v) {
     case 45: return "dmf::k_bk_fuse_s<24, 8, 4, 1>";
     case 46: return "dmf::k_bk_fuse_s<32, 8, 4, 1>";
     case 47: return "dmf::k_bk_fuse_s<40, 8, 4, 1>";
-    case 48: return "dmf::k_bk_fuse_s<24, 8, 3, 1>";
+    case 48: return "dmf::k_bk_fuse_s<16, 8, 4, 1> (pairs: wave-aggregated slots)";
     case 49: return "dmf::k_bk_fuse_s<32, 8, 4, 2>";
     default: return "dmf::k_bk_fuse_s<16, 8, 4, 1>";  // 0, 44; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
