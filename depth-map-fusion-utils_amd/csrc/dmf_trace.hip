@@ -635,11 +635,25 @@ static int reverse_lists(dmf_volume* v, const dmf_camera* cam, const float* pose
 
 // ---------------------------------------------------------------- forward march
 // First occupied sample per lattice pixel (RayTracingEngine.hpp:280-308 loop body).
-__global__ __launch_bounds__(256) void k_forward(Geom g, const uint32_t* __restrict__ occ,
-                                                 const int32_t* __restrict__ slot_of, CamP cam,
-                                                 const PoseX* __restrict__ pose, int zstart, int zdelta, int rdelta,
-                                                 int cdelta, int R, int C, int32_t* __restrict__ k_out,
-                                                 int32_t* __restrict__ slot_out,
+//
+// Empty-space skipping (kSkip), exact.  Sample k is w_k = T * project(r, c, zd_k) in the
+// reference's float/double arithmetic; the same expression in exact arithmetic is the
+// line L(zd) = t + zd * dir (project is linear in zd).  A rounding-error bound
+// eps_a(zd) = 8u (|t_a| + zd * 0.001 (|m_a0 ux| + |m_a1 uy| + |m_a2|)), u = 2^-24, covers
+// |w_k - L(zd_k)| on each axis (5 roundings of float terms on inputs within u of exact;
+// 8u leaves room).  Hence, with every margin delta = 2 eps(zd_j) + 1e-9 m:
+//  * entry: samples whose exact point lies before the line enters the volume box grown by
+//    delta are outside the volume (validPoints false, the reference `continue`s) — jump to
+//    the last of them;
+//  * bricks: if samples s and j both lie inside an empty cube of bricks (L-inf brick
+//    distance field, as the reverse march) shrunk by delta, their exact points lie inside it
+//    shrunk by eps and, the cube being convex, so do the exact points of every sample in
+//    between; those samples are therefore inside the cube: no hit, no hazard — jump to j.
+// j is estimated from the line and then verified by evaluating sample j exactly.
+template <bool kSkip>
+__global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ pose,
+                                                 int zstart, int zdelta, int rdelta, int cdelta, int R, int C,
+                                                 int32_t* __restrict__ k_out, int32_t* __restrict__ slot_out,
                                                  unsigned long long* __restrict__ hazards,
                                                  unsigned long long* __restrict__ stats) {
   stats = stat_slot(stats);
@@ -652,29 +666,146 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, const uint32_t* __restr
   if (idx < (int64_t)R * C) {
     const int r = (int)(idx / C) * rdelta, c = (int)(idx % C) * cdelta;
     int32_t kk = -1, sl = -1;
+    const float* m = pose->f;
+    // the exact line (double estimates) and the error-bound coefficients
+    double dir[3], eA[3], eB[3];
+    float fdir[3], frd[3];  // float copies for the jump estimates (verified exactly)
+    int dmin_jump = 1 << 30;  // smallest brick distance d whose cube holds >= 2 more samples
+    if (kSkip) {
+      const double ux = ((double)c - cam.cx) / cam.fx, uy = ((double)r - cam.cy) / cam.fy;
+      double step = 0.0;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const double m0 = m[4 * a], m1 = m[4 * a + 1], m2 = m[4 * a + 2];
+        dir[a] = 0.001 * (m0 * ux + m1 * uy + m2);
+        eA[a] = 0x1p-21 * fabs((double)m[4 * a + 3]);
+        eB[a] = 0x1p-21 * 0.001 * (fabs(m0 * ux) + fabs(m1 * uy) + fabs(m2));
+        fdir[a] = (float)dir[a];
+        frd[a] = dir[a] != 0.0 ? (float)(1.0 / dir[a]) : 0.0f;
+        step = fmax(step, fabs(dir[a]) * zdelta / g.dl[a]);  // cells per sample along axis a
+      }
+      // the cube reaches (d - 1) bricks of 2^bsh cells beyond the current brick on every side
+      dmin_jump = 1 + (int)ceil(2.0 * step / (double)(1 << vd.bsh)) + 1;
+    }
+    auto margin = [&](int a, double zd) { return 2.0 * (eA[a] + zd * eB[a]) + 1e-9; };
+    const int last_k = (int)((kZMax * 1000 - 1 - zstart) / zdelta);  // samples k = 0..last_k
+    uint32_t known_full = 0xffffffffu;  // last brick found occupied (or not skippable)
+    bool entered = false;
     int k = 0;
     for (int zd = zstart; (double)zd < kZMax * 1000; zd += zdelta, ++k) {
       float pc[3], w[3];
       project(cam, r, c, zd, pc);
-      xform(pose->f, pc[0], pc[1], pc[2], w);
+      xform(m, pc[0], pc[1], pc[2], w);
       ++samples;
-      if (!valid_points(g, w[0], w[1], w[2])) continue;
+      if (!valid_points(g, w[0], w[1], w[2])) {
+        if (kSkip && !entered) {
+          // jump to the last sample before the line enters the volume grown by the margin
+          entered = true;  // (once: after the entry the march proceeds normally)
+          double tin = -1e300, tout = 1e300;
+          const double zmax = kZMax * 1000;
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            const double dm = margin(a, zmax);
+            const double lo = g.mn[a] - dm, hi = g.mx[a] + dm, t0 = (double)m[4 * a + 3];
+            if (dir[a] == 0.0) {
+              if (t0 <= lo || t0 >= hi) tout = -1e300;  // never enters
+            } else {
+              const double ta = (lo - t0) / dir[a], tb = (hi - t0) / dir[a];
+              tin = fmax(tin, fmin(ta, tb));
+              tout = fmin(tout, fmax(ta, tb));
+            }
+          }
+          int kj = tout < tin ? last_k : (int)floor((tin - (double)zstart) / zdelta) - 1;
+          kj = min(kj, last_k);
+          if (kj > k) {
+            const int zj = zstart + kj * zdelta;
+            float qc[3], q[3];
+            project(cam, r, c, zj, qc);
+            xform(m, qc[0], qc[1], qc[2], q);
+            ++samples;
+            if (!valid_points(g, q[0], q[1], q[2])) {  // verified: still outside
+              k = kj;
+              zd = zj;
+            }
+          }
+        }
+        continue;
+      }
+      entered = true;
       const int a = bin_axis(g, 0, w[0]), b = bin_axis(g, 1, w[1]), cc = bin_axis(g, 2, w[2]);
       if (!valid_coords(g, a, b, cc)) {  // reference indexes voxels_ unguarded here (UB)
         atomicAdd(hazards, 1ull);
         continue;
       }
-      if (occ_test(occ, occ_bit(g, a, b, cc))) {
+      if (occ_test(vd.occ, occ_bit(g, a, b, cc))) {
         kk = k;
-        sl = slot_of[lin_index(g, a, b, cc)];
+        sl = vd.slot_of[lin_index(g, a, b, cc)];
         break;
       }
+      if (!kSkip) continue;
+      const int ba = a >> vd.bsh, bb = b >> vd.bsh, bc = cc >> vd.bsh;
+      const uint32_t bl = ((uint32_t)ba * (uint32_t)vd.nb[1] + (uint32_t)bb) * (uint32_t)vd.nb[2] + (uint32_t)bc;
+      if (bl == known_full) continue;
+      const int d = vd.bdist[bl];
+      if (d >= dmin_jump) {  // (smaller cubes cannot hold two more samples: not worth a try)
+        const int Rb = d - 1;  // bricks within Rb of this one are empty
+        const int bx[3] = {ba, bb, bc};
+        double lo[3], hi[3];
+        float zexit = 3.0e38f;
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+          lo[ax] = g.mn[ax] + (double)(max(bx[ax] - Rb, 0) << vd.bsh) * g.dl[ax];
+          hi[ax] = g.mn[ax] + (double)min((bx[ax] + Rb + 1) << vd.bsh, g.n[ax]) * g.dl[ax];
+          if (fdir[ax] != 0.0f)
+            zexit = fminf(zexit, ((float)(fdir[ax] > 0.0f ? hi[ax] : lo[ax]) - m[4 * ax + 3]) * frd[ax]);
+        }
+        int kj = min((int)floorf((zexit - (float)zstart) / (float)zdelta) - 1, last_k);
+        if (kj > k + 1) {
+          const int zj = zstart + kj * zdelta;
+          float qc[3], q[3];
+          project(cam, r, c, zj, qc);
+          xform(m, qc[0], qc[1], qc[2], q);
+          ++samples;
+          bool ok = true;
+#pragma unroll
+          for (int ax = 0; ax < 3; ++ax) {
+            const double dm = margin(ax, (double)zj);
+            ok = ok && (double)w[ax] >= lo[ax] + dm && (double)w[ax] <= hi[ax] - dm && (double)q[ax] >= lo[ax] + dm &&
+                 (double)q[ax] <= hi[ax] - dm;
+          }
+          if (ok) {  // samples k+1 .. kj lie inside the empty cube
+            k = kj;
+            zd = zj;
+            continue;
+          }
+        }
+      }
+      known_full = bl;  // occupied brick, or the jump failed: step through it
     }
     k_out[idx] = kk;
     slot_out[idx] = sl;
   }
   if (stats) wave_add_u64(&stats[0], (unsigned long long)samples);
 }
+
+// DMF_FWD_SKIP=0 disables the forward march's empty-space skipping (A/B, diagnostics)
+static bool fwd_skip() {
+  static const bool on = [] {
+    const char* e = getenv("DMF_FWD_SKIP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+#define DMF_LAUNCH_FORWARD(GRID, ...)                                                                          \
+  do {                                                                                                        \
+    if (fwd_skip()) {                                                                                         \
+      DMF_TRY(ensure_brick_dist(v));                                                                          \
+      hipLaunchKernelGGL(k_forward<true>, GRID, dim3(256), 0, v->stream, __VA_ARGS__);                         \
+    } else {                                                                                                  \
+      hipLaunchKernelGGL(k_forward<false>, GRID, dim3(256), 0, v->stream, __VA_ARGS__);                        \
+    }                                                                                                         \
+  } while (0)
 
 enum FwdMode { kTrace = 0, kClassify = 1, kGoodPoints = 2, kPoints = 3, kMinimum = 4 };
 
@@ -776,8 +907,8 @@ static int run_forward(dmf_volume* v, const dmf_camera* cam, const float* pose, 
   const CamP cp = cam_params(cam);
   const Geom g = v->geom();
   const dim3 grid((unsigned)((RC + 255) / 256));
-  hipLaunchKernelGGL(k_forward, grid, dim3(256), 0, v->stream, g, v->d_occ, v->d_slot_of, cp, tab, zstart, zdelta,
-                     rdelta, cdelta, R, C, (int32_t*)kb, (int32_t*)sb, hz, nullptr);
+  DMF_LAUNCH_FORWARD(grid, g, v->dev(), cp, tab, zstart, zdelta, rdelta, cdelta, R, C, (int32_t*)kb, (int32_t*)sb, hz,
+                     nullptr);
   DMF_LAUNCH_CHECK();
   unsigned long long* minkey = nullptr;
   if ((mode == kPoints || mode == kGoodPoints) && v->V > 0) {
@@ -1097,9 +1228,8 @@ int dmf_forward_first_hits_device(dmf_volume* v, const dmf_camera* cam, const fl
   DMF_HIP(hipMemsetAsync(aux, 0, 64, v->stream));
   unsigned long long* st = nullptr;
   if (d_stats) DMF_TRY(stats_begin(v, &st));
-  hipLaunchKernelGGL(k_forward, dim3((unsigned)((RC + 255) / 256), (unsigned)P), dim3(256), 0, v->stream, v->geom(),
-                     v->d_occ, v->d_slot_of, cam_params(cam), tab, zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot,
-                     (unsigned long long*)aux, st);
+  DMF_LAUNCH_FORWARD(dim3((unsigned)((RC + 255) / 256), (unsigned)P), v->geom(), v->dev(), cam_params(cam), tab,
+                     zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot, (unsigned long long*)aux, st);
   DMF_LAUNCH_CHECK();
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 1));
   return DMF_OK;
@@ -1124,9 +1254,8 @@ int dmf_forward_first_hits(dmf_volume* v, const dmf_camera* cam, const float* po
   DMF_TRY(scratch(v, kScHost2, 64, &aux));
   DMF_HIP(hipMemsetAsync(aux, 0, 64, v->stream));
   const dim3 grid((unsigned)((RC + 255) / 256));
-  hipLaunchKernelGGL(k_forward, grid, dim3(256), 0, v->stream, v->geom(), v->d_occ, v->d_slot_of, cam_params(cam), tab,
-                     zstart, zdelta, rdelta, cdelta, R, C, (int32_t*)kb, (int32_t*)sb, (unsigned long long*)aux,
-                     nullptr);
+  DMF_LAUNCH_FORWARD(grid, v->geom(), v->dev(), cam_params(cam), tab, zstart, zdelta, rdelta, cdelta, R, C,
+                     (int32_t*)kb, (int32_t*)sb, (unsigned long long*)aux, nullptr);
   DMF_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_first_hit_hash, grid, dim3(256), 0, v->stream, (const int32_t*)sb, v->d_hash, RC,
                      (uint64_t*)hb);
