@@ -920,8 +920,13 @@ __device__ inline uint32_t bk_e30(int32_t e) {
 // slab pipeline's default), one LDS atomic per lane whose return is only consumed by the
 // pair's store at the next brick boundary (its latency hides behind that boundary's
 // count_at; B 1.92 -> 1.88 ms).
+#if defined(DMF_BK_PAIRS_WAVES)  // A/B: cap pass B's VGPRs for more waves per SIMD (spills)
+#define DMF_BK_PAIRS_ATTR __attribute__((amdgpu_waves_per_eu(DMF_BK_PAIRS_WAVES)))
+#else
+#define DMF_BK_PAIRS_ATTR
+#endif
 template <bool SLAB, bool AGG = true>
-__global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
+__global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
                                                          const uint32_t* __restrict__ wg_base, uint4* __restrict__ pa,
@@ -1659,11 +1664,11 @@ static bool brick_path_ok(const Geom& g) {
 }
 
 // Default choice (variant 0): the brick pipeline pays a per-ray cost (passes A/B) that
-// the shorter rays of small grids do not amortise.  Measured on MI355X (640x480 frames):
-// 256^3 k_fuse_l 2.58 ms vs brick 2.86 ms (64 frames); 512^3 brick 9.4 vs 10.2 ms (128
-// frames); 1024^3 brick 13.0 vs 17.5 ms (32 frames).
+// the shorter rays of small grids do not amortise.  Measured on MI355X (640x480 frames,
+// slab walk): 256^3 (64 frames) brick 2.43 ms vs k_fuse_l 2.50; 320^3 2.91 vs 3.08; 384^3
+// 3.30 vs 3.62; 512^3 (128 frames) 7.6 vs 10.2; 1024^3 (32 frames) brick ahead by 2x.
 static bool brick_preferred(const Geom& g) {
-  return std::max(g.n[0], std::max(g.n[1], g.n[2])) >= 384;
+  return std::max(g.n[0], std::max(g.n[1], g.n[2])) >= 256;
 }
 
 static std::atomic<const char*> g_last_kernel{nullptr};
@@ -1948,8 +1953,8 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
   unsigned long long* st = nullptr;
   if (d_stats) DMF_TRY(stats_begin(v, &st));
   const int pkx = (cp.W + 7) / 8;
-  // default (variant 0): the brick-owned pipeline where it applies (<= 1024 cells per
-  // axis), the LDS-box kernel k_fuse_l<12, 1280> otherwise
+  // default (variant 0): the brick-owned pipeline where it applies (longest axis 256-1024
+  // cells), the LDS-box kernel k_fuse_l<12, 1280> otherwise
   const int fv = fuse_variant();
   if (brick_path_ok(g) && (is_brick_variant(fv) || (fv == 0 && brick_preferred(g)))) {
     g_last_kernel.store(variant_name(fv));

@@ -132,8 +132,9 @@ def test_config_full_poses(cfg):
         assert np.array_equal(s0[:4], s1[:4])
         assert f.torch.equal(c0, c1)
         del c1
-    if cfg == "config3":  # the default path splits 256 frames into pose batches
-        assert k0.startswith("dmf::k_bk_fuse")
+    # every config's grid (256-1024 cells per axis) takes the slab-walk brick pipeline;
+    # config 3's 256 frames are split into pose batches on it
+    assert k0.startswith("dmf::k_bk_fuse_s")
 
 
 def test_config3_batches_equal_single_batch(monkeypatch):
