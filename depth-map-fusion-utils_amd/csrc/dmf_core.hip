@@ -747,6 +747,9 @@ int dmf_volume_destroy(dmf_volume* v) {
   (void)hipDeviceSynchronize();
   free_state(v);
   if (v->switch_ev) (void)hipEventDestroy(v->switch_ev);
+  for (hipEvent_t e : v->bk_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (v->bk_side) (void)hipStreamDestroy(v->bk_side);
   delete v;
   return DMF_OK;
   DMF_API_END

@@ -731,6 +731,7 @@ constexpr int kBkThreads = 1024;
 // passes A/B: 256-lane workgroups (several per CU) while the LDS brick histogram is small;
 // 1024 lanes when it is large (over 8192 bricks: one workgroup per CU by LDS)
 constexpr int kBkPassThreads = 256, kBkPassThreadsBig = 1024, kBkBigHist = 8192;
+constexpr int kBkPipeDefault = 1;  // pipelined pose batches per call (DMF_BK_PIPE; 1 = off)
 constexpr uint32_t kBkPartMax = 65535;  // pairs per part: 16-bit miss / hit fields never carry
 // LDS box of phase F: cell (x, y, z) of the brick at word x*kSx + y*kSy + z.  The skew
 // (kSy = 33, kSx = 32*33 + 1) puts the cell in bank (x + y + z) mod 32 instead of z alone,
@@ -1696,8 +1697,17 @@ struct BkPlan {
   int pkx = 0, pky = 0;
   int64_t ppose = 0, max_pairs_ray = 0, PB = 0;
   int ab_threads = 0, span = 0;
+  int sets = 1;  // scratch buffer sets: 2 = pose batches pipelined (A/S/B of batch j+1 beside F of j)
   size_t hist_bytes = 0, nwg_max = 0, pair_cap = 0;
 };
+
+// Pose batches a call is cut into so that passes A/S/B of one batch run beside phase F of
+// the previous one (DMF_BK_PIPE; 1 = one batch when it fits the budget, no side stream).
+static int bk_pipe_chunks() {
+  const char* e = getenv("DMF_BK_PIPE");
+  const int n = e ? atoi(e) : kBkPipeDefault;
+  return std::max(1, std::min(n, 64));
+}
 
 static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, BkPlan& pl) {
   pl.bg = brick_geom(g);
@@ -1708,8 +1718,13 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   const int64_t rays_pose = pl.ppose * 64;
   const int64_t ray_cap = (int64_t)UINT32_MAX / pl.max_pairs_ray;  // pair offsets are 32-bit
   const uint64_t per_pose = (uint64_t)rays_pose * (uint64_t)pl.max_pairs_ray * (sizeof(uint4) + sizeof(uint2));
+  const int chunks = bk_pipe_chunks();
+  // two buffer sets share the budget when the batches are pipelined (opt-in: measured
+  // slower, DESIGN.md §5.3 -- A/B beside F slow down 2-5x and F by ~7 %)
+  pl.sets = (P >= 2 && chunks > 1) ? 2 : 1;
   int64_t PB = std::min<int64_t>(P, ray_cap / rays_pose);
-  PB = std::min<int64_t>(PB, (int64_t)(v->bk_budget / per_pose));
+  PB = std::min<int64_t>(PB, (int64_t)(v->bk_budget / pl.sets / per_pose));
+  PB = std::min<int64_t>(PB, ((int64_t)P + chunks - 1) / chunks);
   if (const char* e = getenv("DMF_BK_BATCH_POSES")) {  // test hook: cap the poses per batch
     const int64_t cap = (int64_t)atoll(e);
     if (cap > 0) PB = std::min<int64_t>(PB, cap);
@@ -1743,70 +1758,111 @@ static int bk_attributes() {
   return DMF_OK;
 }
 
-// Every scratch buffer of a plan (allocates only when a slot is too small).
-static int bk_scratch(dmf_volume* v, const BkPlan& pl, void** rays, void** bricks, void** ctl, void** wgb, void** pra,
-                      void** prb) {
-  DMF_TRY(scratch(v, kScBkRays, sizeof(ulonglong2) * (size_t)(pl.PB * pl.ppose * 64), rays));
-  DMF_TRY(scratch(v, kScBkBricks, sizeof(uint32_t) * (3 * (size_t)pl.bg.nbricks + 4), bricks));
-  DMF_TRY(scratch(v, kScBkCtl, sizeof(unsigned long long) * 4, ctl));
+// One scratch set of a plan: ray records, brick counts / offsets / part prefix, queue
+// control words, per-workgroup bases, pair records.
+struct BkBufs {
+  ulonglong2* rays = nullptr;
+  uint32_t *cnt = nullptr, *off = nullptr, *part_pref = nullptr, *wgb = nullptr;
+  unsigned long long* ctl = nullptr;
+  uint4* pra = nullptr;
+  uint2* prb = nullptr;
+};
+
+// Scratch set `set` of a plan (allocates only when a slot is too small).
+static int bk_scratch(dmf_volume* v, const BkPlan& pl, int set, BkBufs& b) {
+  const int o = set * kScBkSetStride;
+  void *rays, *bricks, *ctl, *wgb, *pra, *prb;
+  DMF_TRY(scratch(v, kScBkRays + o, sizeof(ulonglong2) * (size_t)(pl.PB * pl.ppose * 64), &rays));
+  DMF_TRY(scratch(v, kScBkBricks + o, sizeof(uint32_t) * (3 * (size_t)pl.bg.nbricks + 4), &bricks));
+  DMF_TRY(scratch(v, kScBkCtl + o, sizeof(unsigned long long) * 4, &ctl));
   // per-workgroup base inside each brick (pass A -> pass B)
-  DMF_TRY(scratch(v, kScBkWgBase, sizeof(uint32_t) * pl.nwg_max * (size_t)pl.bg.nbricks, wgb));
-  DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * pl.pair_cap, pra));
-  DMF_TRY(scratch(v, kScBkPairsB, sizeof(uint2) * pl.pair_cap, prb));
+  DMF_TRY(scratch(v, kScBkWgBase + o, sizeof(uint32_t) * pl.nwg_max * (size_t)pl.bg.nbricks, &wgb));
+  DMF_TRY(scratch(v, kScBkPairs + o, sizeof(uint4) * pl.pair_cap, &pra));
+  DMF_TRY(scratch(v, kScBkPairsB + o, sizeof(uint2) * pl.pair_cap, &prb));
+  b.rays = (ulonglong2*)rays;
+  b.cnt = (uint32_t*)bricks;
+  b.off = b.cnt + pl.bg.nbricks;
+  b.part_pref = b.off + pl.bg.nbricks;  // nbricks + 1
+  b.wgb = (uint32_t*)wgb;
+  b.ctl = (unsigned long long*)ctl;
+  b.pra = (uint4*)pra;
+  b.prb = (uint2*)prb;
+  return DMF_OK;
+}
+
+// The side stream and events of pipelined batches (created once per volume).
+static int bk_side(dmf_volume* v) {
+  if (!v->bk_side) DMF_HIP(hipStreamCreateWithFlags(&v->bk_side, hipStreamNonBlocking));
+  for (hipEvent_t& e : v->bk_ev)
+    if (!e) DMF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return DMF_OK;
 }
 
 // Brick-owned fusion of P frames (kernels above), in pose batches sized by bk_plan.  Only
 // enqueues work: pass S leaves the pair and part counts on the device, pass B writes the
 // pairs below the planned bound, phase F reads the part count itself (its persistent
-// workgroups exit when the queue is empty).
+// workgroups exit when the queue is empty).  With two scratch sets, batch j's passes A/S/B
+// run on the volume's side stream (after the call's earlier work and after F(j-2) has freed
+// the set) while F(j-1) runs on the caller's stream: F occupies 135 KB of LDS and a quarter
+// of the registers per CU, so an A/B workgroup fits beside it (opt-in, DMF_BK_PIPE: the
+// co-resident kernels slow each other more than they hide).  Every side-stream operation is joined back into the caller's stream (F(j) waits for
+// B(j)), so the call keeps plain stream semantics and stays capturable.
 static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint16_t* d_depth, const PoseX* tab, int P,
                        const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses, unsigned long long* st) {
   BkPlan pl;
   DMF_TRY(bk_plan(v, cp, g, P, pl));
   const BkGeom& bg = pl.bg;
   DMF_TRY(bk_attributes());
-  void *rays, *bricks, *ctl, *wgb, *pra, *prb;
-  DMF_TRY(bk_scratch(v, pl, &rays, &bricks, &ctl, &wgb, &pra, &prb));
-  uint32_t* cnt = (uint32_t*)bricks;
-  uint32_t* off = cnt + bg.nbricks;
-  uint32_t* part_pref = off + bg.nbricks;  // nbricks + 1
-  unsigned long long* ctlp = (unsigned long long*)ctl;
+  BkBufs set[2];
+  for (int k = 0; k < pl.sets; ++k) DMF_TRY(bk_scratch(v, pl, k, set[k]));
+  const bool pipe = pl.sets == 2 && P > pl.PB;
+  hipStream_t sa = v->stream;  // stream of passes A, S, B
+  if (pipe) {
+    DMF_TRY(bk_side(v));
+    sa = v->bk_side;
+    DMF_HIP(hipEventRecord(v->bk_ev[0], v->stream));
+    DMF_HIP(hipStreamWaitEvent(sa, v->bk_ev[0], 0));
+  }
   const unsigned nf = (unsigned)cu_count(v->device);
-  for (int64_t p0 = 0; p0 < P; p0 += pl.PB) {
+  const int fv = fuse_variant();
+  int64_t j = 0;
+  for (int64_t p0 = 0; p0 < P; p0 += pl.PB, ++j) {
+    const BkBufs& b = set[pipe ? j & 1 : 0];
     const int64_t pb = std::min<int64_t>(pl.PB, P - p0);
     const int64_t npk = pb * pl.ppose;
     const unsigned nwg = (unsigned)((npk + pl.span - 1) / pl.span);
-    DMF_HIP(hipMemsetAsync(cnt, 0, pl.hist_bytes, v->stream));
-    DMF_HIP(hipMemsetAsync(ctlp, 0, sizeof(unsigned long long) * 4, v->stream));
-    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, g, cp,
+    if (pipe && j >= 2) DMF_HIP(hipStreamWaitEvent(sa, v->bk_ev[3 + (j & 1)], 0));  // F(j-2) is done with the set
+    DMF_HIP(hipMemsetAsync(b.cnt, 0, pl.hist_bytes, sa));
+    DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sa));
+    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, g, cp,
                        d_depth + (size_t)p0 * cp.H * cp.W, tab + p0, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
-                       npk, pl.span, bg, (ulonglong2*)rays, cnt, (uint32_t*)wgb, st);
+                       npk, pl.span, bg, b.rays, b.cnt, b.wgb, st);
     DMF_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, v->stream, bg.nbricks, (const uint32_t*)cnt, off, part_pref,
-                       ctlp);
+    hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off, b.part_pref,
+                       b.ctl);
     DMF_LAUNCH_CHECK();
-    const int fv = fuse_variant();
     if (fv == 48)  // wave-aggregated slot atomics (the previous default)
-      hipLaunchKernelGGL((k_bk_pairs<true, true>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk,
-                         pl.span, bg, (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra,
-                         (uint2*)prb);
+      hipLaunchKernelGGL((k_bk_pairs<true, true>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
+                         (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
     else if (is_slab_variant(fv))
-      hipLaunchKernelGGL((k_bk_pairs<true, false>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk, pl.span, bg,
-                         (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra, (uint2*)prb);
+      hipLaunchKernelGGL((k_bk_pairs<true, false>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
+                         (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
     else
-      hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, v->stream, npk, pl.span,
-                         bg, (const ulonglong2*)rays, (const uint32_t*)off, (const uint32_t*)wgb, (uint4*)pra,
-                         (uint2*)prb);
+      hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
+                         (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
     DMF_LAUNCH_CHECK();
+    if (pipe) {
+      DMF_HIP(hipEventRecord(v->bk_ev[1 + (j & 1)], sa));
+      DMF_HIP(hipStreamWaitEvent(v->stream, v->bk_ev[1 + (j & 1)], 0));
+    }
 #define DMF_BK_FUSE(R, S, U, N, C, B)                                                                           \
   hipLaunchKernelGGL((k_bk_fuse<R, S, U, N, C, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,            \
-                     (const uint4*)pra, (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt,           \
-                     (const uint32_t*)part_pref, ctlp, d_hits, d_misses, st)
+                     (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
+                     (const uint32_t*)b.part_pref, b.ctl, d_hits, d_misses, st)
 #define DMF_BK_FUSE_S(R, S, U, N)                                                                              \
-  hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg, (const uint4*)pra,     \
-                     (const uint2*)prb, (const uint32_t*)off, (const uint32_t*)cnt, (const uint32_t*)part_pref, ctlp, \
-                     d_hits, d_misses, st)
+  hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,                \
+                     (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
+                     (const uint32_t*)b.part_pref, b.ctl, d_hits, d_misses, st)
     switch (fv) {
       case 40: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
       case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
@@ -1822,6 +1878,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
 #undef DMF_BK_FUSE
 #undef DMF_BK_FUSE_S
     DMF_LAUNCH_CHECK();
+    if (pipe) DMF_HIP(hipEventRecord(v->bk_ev[3 + (j & 1)], v->stream));
   }
   return DMF_OK;
 }
@@ -1911,8 +1968,9 @@ int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t m
     BkPlan pl;
     DMF_TRY(bk_plan(v, cp, g, P, pl));
     DMF_TRY(bk_attributes());
-    void *rays, *bricks, *ctl, *wgb, *pra, *prb;
-    DMF_TRY(bk_scratch(v, pl, &rays, &bricks, &ctl, &wgb, &pra, &prb));
+    BkBufs set;
+    for (int k = 0; k < pl.sets; ++k) DMF_TRY(bk_scratch(v, pl, k, set));
+    if (pl.sets == 2) DMF_TRY(bk_side(v));
   }
   DMF_HIP(hipStreamSynchronize(v->stream));
   return DMF_OK;

@@ -258,6 +258,10 @@ struct dmf_volume {
   int64_t nenum = 0, enum_cap = 0, enum_hazards = 0;
   // brick fusion pair-list budget (dmf_fuse_reserve)
   uint64_t bk_budget = 48ull << 30;
+  // pipelined pose batches: passes A/S/B run on bk_side while phase F of the previous batch
+  // runs on `stream`; events: [0] call start, [1+s] set s written (B done), [3+s] set s free (F done)
+  hipStream_t bk_side = nullptr;
+  hipEvent_t bk_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   // scratch arena
   std::vector<std::pair<void*, size_t>> scratch;
 

@@ -692,10 +692,12 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
     assert int(c0[:nt].astype(np.int64).sum()) == int(s0[2])  # one hit per ray ending inside
 
 
-def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch):
+@pytest.mark.parametrize("pipe", ["1", "3"])
+def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, pipe):
     """The brick pipeline (variants 44 = slab walk, 40 = per-cell walk) split into several pose
     batches (DMF_BK_BATCH_POSES=2 over 5 frames: batches of 2, 2, 1) accumulates the same
-    counters as the oracle."""
+    counters as the oracle -- one after another, and pipelined over two scratch sets with
+    passes A/S/B on the volume's side stream (DMF_BK_PIPE=3)."""
     poses, depth, _ = Hh.frames()
     poses, depth = poses[:5], depth[:5]
     ov = Hh.oracle_volume(oracle, n=80, clouds=[])
@@ -704,6 +706,7 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch):
     from dmf_amd import _lib
     L = _lib.load()
     monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
+    monkeypatch.setenv("DMF_BK_PIPE", pipe)
     for variant, name in ((44, "dmf::k_bk_fuse_s<16, 8, 4, 1>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
         _lib.check(L.dmf_fuse_set_variant(variant))  # the brick pipeline at this small grid
         try:
