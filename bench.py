@@ -8,7 +8,8 @@ One step = clear the int32 hit/miss counters, fuse the rank's 128 depth frames
 (back-projection + exact integer 3D-DDA, libdmf.so brick pipeline k_bk_*), merge the
 ranks' counters (N>1: RCCL reduce-scatter, slab finalize, all-gather of the int16 slabs,
 libdmf dmf_fuse_merge_finalize_device) or finalize (N=1) to the clamped int16 log-odds
-grid.  The merge of step i overlaps the fusion of step i+1 (dmf_amd.schedule).  Inputs
+grid.  The merge of step i and the clear of its buffer overlap the fusion of step i+1
+(dmf_amd.schedule).  Inputs
 are resident in HBM before timing starts.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 through
@@ -281,8 +282,9 @@ def main():
     _lib.check(L.dmf_fuse_reserve(vol._h, pcam, P, 0))
 
     # The step schedule (dmf_amd.schedule.run_steps, tested on CPU under random stream
-    # orders): clear + fuse on the compute stream; the merge of step i on the comm stream,
-    # overlapping the fusion of step i+1 (two counter buffers).  Merge = libdmf's
+    # orders): fuse on the compute stream; the merge of step i, then the zeroing of its
+    # buffer for step i+2, on the comm stream, overlapping the fusion of step i+1 (two
+    # counter buffers).  Merge = libdmf's
     # reduce-scatter / slab finalize / all-gather over torch's RCCL communicator (N > 1),
     # or the plain finalize (N = 1: no collective).
     merge_mode = os.environ.get("DMF_BENCH_MERGE", "rs")
@@ -339,13 +341,13 @@ def main():
     def seg(a, b):
         v = [r[a].elapsed_time(r[b]) for r in ev if a in r and b in r]
         return float(np.mean(v)) if v else 0.0
-    clear_ms, fuse_ms, merge_ms = seg("c0", "c1"), seg("c1", "c2"), seg("a0", "a1")
+    clear_ms, fuse_ms, merge_ms = seg("z0", "z1"), seg("c1", "c2"), seg("a0", "a1")
     breakdown = {"clear": clear_ms, "fuse": fuse_ms, "merge": merge_ms,
                  "merge_kind": {"rs": "RCCL reduce-scatter(hits, misses) + slab finalize + all-gather(int16) "
                                       "(dmf_fuse_merge_finalize_device)",
                                 "torch": "torch RCCL all-reduce(sum) + finalize"}[merge_mode] if world > 1
                  else "finalize (no collective at N=1)",
-                 "schedule": "merge of step i on the comm stream overlaps fuse of step i+1 (2 counter buffers)"}
+                 "schedule": "merge of step i, then the zeroing of its buffer for step i+2, on the comm stream overlap fuse of step i+1 (2 counter buffers)"}
     # grid-wide streaming passes, priced separately: clear writes the
     # 2 tiled int32 counter arrays; finalize reads them and writes int16 log-odds
     clear_bytes = 2 * 4 * nct

@@ -1329,7 +1329,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
 // dependency chains: at 4 waves per SIMD a single chain leaves the SIMD idle between
 // its dependent instructions).  A wave refills when >= REFILL of its 64 * NSLOT slots
 // are idle, from per-slot records prefetched one refill ahead.
-template <int REFILL, int S_ORDER, int UNROLL, int NSLOT>
+template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, bool BL = false>
 __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, const uint4* __restrict__ pa,
                                                           const uint2* __restrict__ pb,
                                                           const uint32_t* __restrict__ off,
@@ -1505,6 +1505,29 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
         for (int q = 0; q < NSLOT; ++q) {
+          if constexpr (BL) {
+            // branch-free slab: sign masks instead of compares, and the adds a lane does not
+            // own go to its private dummy word (no exec-mask regions, so the slots' chains
+            // interleave)
+            const uint32_t n1 = (uint32_t)((int32_t)b1[q] >> 31), n2 = (uint32_t)((int32_t)b2[q] >> 31);  // ~c1, ~c2
+            const uint32_t mo = (uint32_t)((int32_t)~b12[q] >> 31);                                        // o
+            const int nc = 3 + (int32_t)n1 + (int32_t)n2;
+            const int v = min(nc, r[q]);
+            const uint32_t x1 = d1[q] & ~n1, x2 = d2[q] & ~n2;
+            const uint32_t sel = ~n2 & (n1 | mo);  // c2 && (!c1 || o): the first extra cell is on m2
+            const uint32_t p1 = cur[q] + ((sel & d2[q]) | (~sel & x1)), p2 = cur[q] + x1 + x2;
+            const uint32_t dw = (uint32_t)(kBkBoxWords + 4 + l) * 4u;
+            const uint32_t a0 = v >= 1 ? cur[q] : dw, a1 = v >= 2 ? p1 : dw, a2 = v >= 3 ? p2 : dw;
+            atomicAdd((uint32_t*)(lds + a0), 1u);
+            atomicAdd((uint32_t*)(lds + a1), 1u);
+            atomicAdd((uint32_t*)(lds + a2), 1u);
+            cur[q] = p2 + dM[q];
+            b1[q] += (n1 & K1[q]) | (~n1 & K1mM[q]);
+            b2[q] += (n2 & K2[q]) | (~n2 & K2mM[q]);
+            b12[q] += (K2[q] & ~n1) + (nK1[q] & ~n2);
+            r[q] -= nc;
+            continue;
+          }
           const bool c1 = (int32_t)b1[q] >= 0, c2 = (int32_t)b2[q] >= 0, o = (int32_t)b12[q] >= 0;
           // cells in this slab (1 + c1 + c2) and how many of them the pair still owns
           const int nc = 3 + ((int32_t)b1[q] >> 31) + ((int32_t)b2[q] >> 31);
@@ -1645,9 +1668,10 @@ static int fuse_variant() {
   return v;
 }
 constexpr int kVariantBrick = 40;
-constexpr int kVariantSlab = 44;  // 44..49: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
-static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantSlab + 5; }
-static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantSlab + 5); }
+constexpr int kVariantSlab = 44;  // 44..51: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
+constexpr int kVariantLast = 51;  // 50, 51: branch-free slab body (measured slower)
+static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantLast; }
+static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantLast); }
 static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
 
 static BkGeom brick_geom(const Geom& g) {
@@ -1863,6 +1887,10 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,                \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
                      (const uint32_t*)b.part_pref, b.ctl, d_hits, d_misses, st)
+#define DMF_BK_FUSE_SB(R, S, U, N)                                                                             \
+  hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,          \
+                     (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
+                     (const uint32_t*)b.part_pref, b.ctl, d_hits, d_misses, st)
     switch (fv) {
       case 40: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
       case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
@@ -1873,10 +1901,13 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       case 47: DMF_BK_FUSE_S(40, 8, 4, 1); break;
       case 48: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // with k_bk_pairs<true, true>
       case 49: DMF_BK_FUSE_S(32, 8, 4, 2); break;
+      case 50: DMF_BK_FUSE_SB(16, 8, 4, 1); break;
+      case 51: DMF_BK_FUSE_SB(32, 8, 4, 2); break;
       default: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // 0, 44
     }
 #undef DMF_BK_FUSE
 #undef DMF_BK_FUSE_S
+#undef DMF_BK_FUSE_SB
     DMF_LAUNCH_CHECK();
     if (pipe) DMF_HIP(hipEventRecord(v->bk_ev[3 + (j & 1)], v->stream));
   }
@@ -1938,6 +1969,8 @@ static const char* variant_name(int v) {
     case 47: return "dmf::k_bk_fuse_s<40, 8, 4, 1>";
     case 48: return "dmf::k_bk_fuse_s<16, 8, 4, 1> (pairs: wave-aggregated slots)";
     case 49: return "dmf::k_bk_fuse_s<32, 8, 4, 2>";
+    case 50: return "dmf::k_bk_fuse_s<16, 8, 4, 1, true>";
+    case 51: return "dmf::k_bk_fuse_s<32, 8, 4, 2, true>";
     default: return "dmf::k_bk_fuse_s<16, 8, 4, 1>";  // 0, 44; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
 }

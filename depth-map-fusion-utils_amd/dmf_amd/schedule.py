@@ -4,11 +4,13 @@ events) and a CPU simulator that executes the enqueued work in random stream-con
 orders (gloo collectives inside).
 
 One step on one rank:
-  compute lane:  [wait until buffer b's previous merge is done] clear(b) -> fuse(b, i)
-  comm lane:     [wait fuse(b, i)] merge(b, i)   (reduce-scatter + slab finalize +
-                                                  all-gather, or all-reduce + finalize)
-Counters are multi-buffered, so the merge of step i overlaps the fusion of step i+1; the
-last merge is waited for before the schedule returns (it is inside the timed region).
+  compute lane:  [wait until buffer b's previous merge + clear are done] fuse(b, i)
+  comm lane:     [wait fuse(b, i)] merge(b, i) (reduce-scatter + slab finalize +
+                 all-gather, or all-reduce + finalize) -> clear(b) for step i + nbuf
+Counters are multi-buffered, so the merge of step i and the zeroing of its buffer overlap
+the fusion of step i+1.  A buffer's first use in a run is cleared on the compute lane, so
+K steps do exactly K clears, K fusions and K merges; the last merge is waited for before
+the schedule returns (it is inside the timed region).
 """
 from __future__ import annotations
 
@@ -92,29 +94,36 @@ def run_steps(rt, nsteps, nbuf, clear, fuse, merge, marks=None, reuse_wait=True)
 
     clear(b), fuse(b, i), merge(b, i) enqueue (or, on the simulator, perform) the work of
     step i on counter buffer b = i % nbuf.  marks(i, name, lane), if given, is called at
-    the step's phase boundaries (c0, c1, c2 on compute; a0, a1 on comm) for timing.
-    reuse_wait=False drops the buffer-reuse dependency (tests show it is needed)."""
+    the step's phase boundaries (z0, z1 around the clear that prepares step i's buffer, on
+    whichever lane runs it; c1, c2 around the fusion on compute; a0, a1 around the merge
+    on comm) for timing.  reuse_wait=False drops the buffer-reuse dependency (tests show it
+    is needed)."""
+    def mark(i, name, lane):
+        if marks:
+            marks(i, name, lane)
+
     merged = [None] * nbuf
     last = None
     for i in range(nsteps):
         b = i % nbuf
         if reuse_wait and merged[b] is not None:
             rt.wait("compute", merged[b])
-        if marks:
-            marks(i, "c0", "compute")
-        rt.enqueue("compute", lambda b=b: clear(b))
-        if marks:
-            marks(i, "c1", "compute")
+        if i < nbuf:  # the buffer's first use in this run
+            mark(i, "z0", "compute")
+            rt.enqueue("compute", lambda b=b: clear(b))
+            mark(i, "z1", "compute")
+        mark(i, "c1", "compute")
         rt.enqueue("compute", lambda b=b, i=i: fuse(b, i))
-        if marks:
-            marks(i, "c2", "compute")
+        mark(i, "c2", "compute")
         fused = rt.record("compute")
         rt.wait("comm", fused)
-        if marks:
-            marks(i, "a0", "comm")
+        mark(i, "a0", "comm")
         rt.enqueue("comm", lambda b=b, i=i: merge(b, i))
-        if marks:
-            marks(i, "a1", "comm")
+        mark(i, "a1", "comm")
+        if i + nbuf < nsteps:  # zero the buffer for step i + nbuf behind its merge
+            mark(i + nbuf, "z0", "comm")
+            rt.enqueue("comm", lambda b=b: clear(b))
+            mark(i + nbuf, "z1", "comm")
         merged[b] = last = rt.record("comm")
     if last is not None:
         rt.wait("compute", last)

@@ -580,11 +580,12 @@ def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
             L.dmf_device_free(h, p_)
 
 
-@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49])
+@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51])
 def brick_variant(dmf, request):
     """Select a brick-owned fusion variant for one test: DMF_FUSE_VARIANT 40-43 = the
-    per-cell walk (k_bk_fuse: refill threshold, pair order, interleaving), 44-49 = the
-    slab walk (k_bk_fuse_s, the default: refill threshold, unroll, two pairs per lane)."""
+    per-cell walk (k_bk_fuse: refill threshold, pair order, interleaving), 44-51 = the
+    slab walk (k_bk_fuse_s, the default: refill threshold, unroll, two pairs per lane,
+    branch-free body)."""
     from dmf_amd import _lib
     L = _lib.load()
     _lib.check(L.dmf_fuse_set_variant(request.param))
