@@ -276,7 +276,7 @@ def main():
     nlo = C.c_int64()
     _lib.check(L.dmf_fuse_logodds_cells_padded(vol._h, world, C.addressof(nlo)))
     logodds = torch.empty(nlo.value, dtype=torch.int16, device=dev)
-    stats = torch.zeros(16, dtype=torch.int64, device=dev)  # 8 used; diagnostic builds add 7..15
+    stats = torch.zeros(20, dtype=torch.int64, device=dev)  # 8 used; diagnostic builds add 7..19
     pcam, pprm = C.addressof(cam), C.addressof(prm)
     # all fusion scratch allocated up front: the timed calls neither allocate nor sync
     _lib.check(L.dmf_fuse_reserve(vol._h, pcam, P, 0))
@@ -403,6 +403,8 @@ def main():
                                     "f_wave_cycles": {"refill": int(st[10]) // args.steps, "walk": int(st[11]) // args.steps,
                                                       "flush": int(st[12]) // args.steps,
                                                       "part_barrier": int(st[15]) // args.steps,
+                                                      "refill_decode": int(st[16]) // args.steps,
+                                                      "refill_prefetch": int(st[17]) // args.steps,
                                                       "lifetime_sum": int(st[14]) // args.steps,
                                                       "lifetime_max_wave": int(st[13])}})
         else:

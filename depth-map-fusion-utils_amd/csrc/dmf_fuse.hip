@@ -1350,6 +1350,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
   // diagnostic build: wave blocks, slots active at block start, refills, and s_memtime
   // cycles per phase (refill, walk, flush incl. its barriers, wait at the part-start barrier)
   unsigned long long nblocks = 0, nlanes = 0, nrefill = 0, t_refill = 0, t_walk = 0, t_flush = 0, t_bar = 0;
+  unsigned long long t_dec = 0, t_pf = 0;  // refill split: decode (incl. the record wait), index allocation + prefetch
   const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
   char* const lds = (char*)box;
@@ -1474,6 +1475,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
 #if defined(DMF_EXP_STATS)
           if (l == 0) ++nrefill;
 #endif
+          DMF_T(td0);
 #pragma unroll
           for (int q = 0; q < NSLOT; ++q) {
             if (r[q] <= 0 && fok[q]) {
@@ -1481,7 +1483,13 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
               fok[q] = false;
             }
           }
+#if defined(DMF_EXP_STATS)
+          __builtin_amdgcn_s_waitcnt(0);  // close the decode interval on its loads and LDS adds
+#endif
+          DMF_TACC(t_dec, td0);
+          DMF_T(tp0);
           if (more) prefetch(take);
+          DMF_TACC(t_pf, tp0);
           any_act = false;
 #pragma unroll
           for (int q = 0; q < NSLOT; ++q) any_act |= __builtin_amdgcn_ballot_w64(r[q] > 0) != 0;
@@ -1592,6 +1600,8 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       atomicAdd(&stats[11], t_walk);
       atomicAdd(&stats[12], t_flush);
       atomicAdd(&stats[15], t_bar);
+      atomicAdd(&stats[16], t_dec);
+      atomicAdd(&stats[17], t_pf);
       const unsigned long long t_end = __builtin_amdgcn_s_memtime();
       atomicMax(&stats[13], t_end - t_start);
       atomicAdd(&stats[14], t_end - t_start);

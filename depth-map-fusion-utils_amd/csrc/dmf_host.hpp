@@ -62,7 +62,7 @@ static_assert(kScBkCtl2 - kScBkCtl == kScBkSetStride, "brick scratch sets must b
 // of kStatSlots x kStatWidth counters (one hot address per counter serialises at the
 // memory side); stats_end() sums the slots into the caller's counters.
 #if defined(DMF_EXP_STATS)
-constexpr int kStatSlots = 256, kStatWidth = 16;  // diagnostic builds: extra counters 7..15
+constexpr int kStatSlots = 256, kStatWidth = 20;  // diagnostic builds: extra counters 7..19
 #else
 constexpr int kStatSlots = 256, kStatWidth = 8;
 #endif
