@@ -2021,14 +2021,14 @@ static const char* variant_name(int v) {
     case 41: return "dmf::k_bk_fuse<16, 8, 8, 1, 0, false>";
     case 42: return "dmf::k_bk_fuse<32, 8, 8, 2, 0, false>";
     case 43: return "dmf::k_bk_fuse<16, 8, 8, 1, 256, true>";
-    case 45: return "dmf::k_bk_fuse_s<24, 8, 4, 1>";
-    case 46: return "dmf::k_bk_fuse_s<32, 8, 4, 1>";
-    case 47: return "dmf::k_bk_fuse_s<40, 8, 4, 1>";
-    case 48: return "dmf::k_bk_fuse_s<16, 8, 4, 1> (pairs: wave-aggregated slots)";
-    case 49: return "dmf::k_bk_fuse_s<32, 8, 4, 2>";
+    case 45: return "dmf::k_bk_fuse_s<24, 8, 4, 1, false>";
+    case 46: return "dmf::k_bk_fuse_s<32, 8, 4, 1, false>";
+    case 47: return "dmf::k_bk_fuse_s<40, 8, 4, 1, false>";
+    case 48: return "dmf::k_bk_fuse_s<16, 8, 4, 1, false> (pairs: wave-aggregated slots)";
+    case 49: return "dmf::k_bk_fuse_s<32, 8, 4, 2, false>";
     case 50: return "dmf::k_bk_fuse_s<16, 8, 4, 1, true>";
     case 51: return "dmf::k_bk_fuse_s<32, 8, 4, 2, true>";
-    default: return "dmf::k_bk_fuse_s<16, 8, 4, 1>";  // 0, 44; grids over 1024 cells per axis: k_fuse_l<12, 1280>
+    default: return "dmf::k_bk_fuse_s<16, 8, 4, 1, false>";  // 0, 44; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
 }
 

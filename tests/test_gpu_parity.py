@@ -708,7 +708,7 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, pipe):
     L = _lib.load()
     monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
     monkeypatch.setenv("DMF_BK_PIPE", pipe)
-    for variant, name in ((44, "dmf::k_bk_fuse_s<16, 8, 4, 1>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
+    for variant, name in ((44, "dmf::k_bk_fuse_s<16, 8, 4, 1, false>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
         _lib.check(L.dmf_fuse_set_variant(variant))  # the brick pipeline at this small grid
         try:
             hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))

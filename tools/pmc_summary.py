@@ -38,8 +38,10 @@ bench = json.load(open(os.path.join(src, "bench_kt.json")))
 PIPE = ("dmf::k_bk_", "dmf::k_fuse")
 kernels = sorted({k for (k, c) in tot if k.startswith(PIPE)})
 if kernels:
-    # per fusion call (a call of a multi-batch config launches each kernel once per batch)
-    calls = int(bench["steps"]) + int(bench["warmup"])
+    # per fusion call (a call of a multi-batch config launches each kernel once per batch);
+    # the PMC passes run their own (shorter) bench command: count its calls, not the trace's
+    pmc_bench = json.load(open(sorted(glob.glob(os.path.join(src, "pmc*.json")))[0]))
+    calls = int(pmc_bench["steps"]) + int(pmc_bench["warmup"])
 
     def per(k, c):
         return tot.get((k, c), 0.0) / max(calls, 1)
@@ -56,15 +58,20 @@ if kernels:
             "note": "traffic = sum over the pipeline's kernels of (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch; "
                     "FETCH doubled per MI355X_MICROARCH.md"}
     json.dump(summ, open(os.path.join(dst, "pmc_fuse_summary.json"), "w"), indent=1)
-    # the bench's lookup table: one entry per (grid, poses, image, kernel)
-    tpath = os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json")
-    try:
-        table = json.load(open(tpath))
-    except (OSError, ValueError):
-        table = []
-    key = lambda e: (e.get("grid"), e.get("poses"), e.get("image"), e.get("kernel"))  # noqa: E731
-    table = [e for e in table if key(e) != key(summ)] + [
-        {k: summ[k] for k in ("grid", "poses", "image", "kernel", "hbm_bytes_per_launch", "profile")}]
-    json.dump(table, open(tpath, "w"), indent=1)
     print(json.dumps(summ, indent=1))
 shutil.copy(os.path.join(src, "bench_kt.json"), os.path.join(dst, "bench_under_rocprof.json"))
+# per-kernel average over the timed steps only (rocprofv3 --stats also averages the cold
+# warmup dispatches): the last `steps` fusion calls of the traced bench command
+trace = sorted(csv.DictReader(open(os.path.join(src, "kt", "run_kernel_trace.csv"))), key=lambda r: int(r["Start_Timestamp"]))
+durs = collections.defaultdict(list)
+for r in trace:
+    durs[r["Kernel_Name"].split("(")[0].replace("void ", "")].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+steps, warm = int(bench["steps"]), int(bench["warmup"])
+with open(os.path.join(dst, "kernel_timed_avg.csv"), "w") as f:
+    f.write("kernel,dispatches_total,dispatches_timed,avg_ms_timed\n")
+    for k, v in sorted(durs.items()):
+        if not k.startswith("dmf::"):
+            continue
+        per_call = len(v) // max(steps + warm, 1) if len(v) >= steps + warm else 0
+        timed = v[-steps * per_call:] if per_call else v
+        f.write(f"{k},{len(v)},{len(timed)},{sum(timed) / len(timed):.4f}\n")

@@ -10,7 +10,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-BENCH="python3 bench.py --steps 3 --warmup 1 --cpu-frames 0 --cpu-reverse-poses 0 --pmc off ${BENCHARGS}"
+BENCH="python3 bench.py --steps 20 --warmup 2 --cpu-frames 0 --cpu-reverse-poses 0 --pmc off ${BENCHARGS}"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- $BENCH > "$OUT/bench_kt.json" 2> "$OUT/bench_kt.err" || exit 1
 i=0
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" "SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
