@@ -83,10 +83,17 @@ __device__ inline void dda_select(int32_t& E01, int32_t& E02, int32_t& E12, int3
   E12 += s1 ? K2 : (s2 ? -K1 : 0);
 }
 
-// Grid coordinates of the ray origin (oracle.cpp dda_ray: (O - min) / delta in double).
+// (x - min) / delta in double (oracle.cpp dda_ray); a power-of-two delta divides exactly
+// as a multiplication by its (exact) reciprocal, as in bin_axis
+__device__ inline double grid_coord(const Geom& g, int a, float x) {
+  const double t = (double)x - g.mn[a];
+  return g.pow2 ? t * g.inv[a] : t / g.dl[a];
+}
+
+// Grid coordinates of the ray origin.
 __device__ inline void grid_origin(const Geom& g, const float O[3], double go[3]) {
 #pragma unroll
-  for (int a = 0; a < 3; ++a) go[a] = ((double)O[a] - g.mn[a]) / g.dl[a];
+  for (int a = 0; a < 3; ++a) go[a] = grid_coord(g, a, O[a]);
 }
 
 // Clip O->E to the grid and quantise the clipped endpoints to 1/256 cell (clamped
@@ -103,7 +110,7 @@ __device__ inline bool dda_quantize_go(const Geom& g, const double go[3], const 
   double ge[3], D[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    ge[a] = ((double)E[a] - g.mn[a]) / g.dl[a];
+    ge[a] = grid_coord(g, a, E[a]);
     D[a] = ge[a] - go[a];
   }
   double t0 = 0.0, t1 = 1.0;
