@@ -906,14 +906,20 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
 
 // Scan of the brick counts (one workgroup): list offsets, write cursors, and the part
 // table part_pref[b] = parts of bricks < b (a brick of n pairs has ceil(n / 65535)
-// parts).  ctl[0] = pairs, ctl[1] = parts.
+// parts).  ctl[0] = pairs, ctl[1] = parts.  order[] = the parts largest first (counting
+// sort into 64 size classes of 1024 pairs): phase F's queue hands out the big parts
+// first, so the parts left when the queue runs dry are the small ones (the CUs finish
+// together; counter sums do not depend on the order).
 __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* __restrict__ cnt,
                                                   uint32_t* __restrict__ off,
                                                   uint32_t* __restrict__ part_pref,
-                                                  unsigned long long* __restrict__ ctl) {
+                                                  unsigned long long* __restrict__ ctl,
+                                                  uint32_t* __restrict__ order) {
   __shared__ unsigned long long s_pairs[1024];
   __shared__ uint32_t s_parts[1024];
+  __shared__ uint32_t s_cls[64];
   const int t = threadIdx.x;
+  if (t < 64) s_cls[t] = 0;
   const int per = (nbricks + 1023) / 1024;
   const int i0 = min(nbricks, t * per), i1 = min(nbricks, i0 + per);
   unsigned long long sp = 0;
@@ -934,12 +940,35 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
     __syncthreads();
   }
   unsigned long long base = t ? s_pairs[t - 1] : 0ull;
-  uint32_t pbase = t ? s_parts[t - 1] : 0u;
+  const uint32_t pbase0 = t ? s_parts[t - 1] : 0u;
+  uint32_t pbase = pbase0;
+  auto size_class = [](uint32_t n, uint32_t np) { return min(63u, ((n + np - 1) / np) >> 10); };
   for (int i = i0; i < i1; ++i) {
     off[i] = (uint32_t)base;
     part_pref[i] = pbase;
     base += cnt[i];
-    pbase += (cnt[i] + kBkPartMax - 1) / kBkPartMax;
+    const uint32_t np = (cnt[i] + kBkPartMax - 1) / kBkPartMax;
+    pbase += np;
+    if (np) atomicAdd(&s_cls[size_class(cnt[i], np)], np);
+  }
+  __syncthreads();
+  if (t == 0) {  // class starts, largest class first
+    uint32_t acc = 0;
+    for (int c = 63; c >= 0; --c) {
+      const uint32_t v = s_cls[c];
+      s_cls[c] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  pbase = pbase0;
+  for (int i = i0; i < i1; ++i) {
+    const uint32_t np = (cnt[i] + kBkPartMax - 1) / kBkPartMax;
+    if (np) {
+      const uint32_t pos = atomicAdd(&s_cls[size_class(cnt[i], np)], np);
+      for (uint32_t k = 0; k < np; ++k) order[pos + k] = pbase + k;
+    }
+    pbase += np;
   }
   if (t == 1023) {
     part_pref[nbricks] = s_parts[1023];
@@ -1389,6 +1418,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
                                                           const uint32_t* __restrict__ off,
                                                           const uint32_t* __restrict__ cnt,
                                                           const uint32_t* __restrict__ part_pref,
+                                                          const uint32_t* __restrict__ order,
                                                           unsigned long long* __restrict__ ctl,
                                                           int32_t* __restrict__ hits, int32_t* __restrict__ misses,
                                                           unsigned long long* __restrict__ stats) {
@@ -1416,8 +1446,8 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     DMF_T(tb0);
     __syncthreads();
     DMF_TACC(t_bar, tb0);
-    const uint32_t t = sh[0];
-    if (t >= nparts) break;
+    if (sh[0] >= nparts) break;
+    const uint32_t t = order ? order[sh[0]] : sh[0];  // largest parts first (k_bk_scan)
     int lo = 0, hi = bg.nbricks - 1;  // last brick b with part_pref[b] <= t
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -1850,7 +1880,7 @@ static int bk_attributes() {
 // control words, per-workgroup bases, pair records.
 struct BkBufs {
   ulonglong2* rays = nullptr;
-  uint32_t *cnt = nullptr, *off = nullptr, *part_pref = nullptr, *wgb = nullptr;
+  uint32_t *cnt = nullptr, *off = nullptr, *part_pref = nullptr, *order = nullptr, *wgb = nullptr;
   unsigned long long* ctl = nullptr;
   uint4* pra = nullptr;
   uint2* prb = nullptr;
@@ -1861,7 +1891,9 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, int set, BkBufs& b) {
   const int o = set * kScBkSetStride;
   void *rays, *bricks, *ctl, *wgb, *pra, *prb;
   DMF_TRY(scratch(v, kScBkRays + o, sizeof(ulonglong2) * (size_t)(pl.PB * pl.ppose * 64), &rays));
-  DMF_TRY(scratch(v, kScBkBricks + o, sizeof(uint32_t) * (3 * (size_t)pl.bg.nbricks + 4), &bricks));
+  // cnt | off | part_pref (nbricks + 1) | order (every part: <= nbricks + pairs / 65535)
+  const size_t max_parts = (size_t)pl.bg.nbricks + pl.pair_cap / kBkPartMax + 1;
+  DMF_TRY(scratch(v, kScBkBricks + o, sizeof(uint32_t) * (3 * (size_t)pl.bg.nbricks + 4 + max_parts), &bricks));
   DMF_TRY(scratch(v, kScBkCtl + o, sizeof(unsigned long long) * 4, &ctl));
   // per-workgroup base inside each brick (pass A -> pass B)
   DMF_TRY(scratch(v, kScBkWgBase + o, sizeof(uint32_t) * pl.nwg_max * (size_t)pl.bg.nbricks, &wgb));
@@ -1871,6 +1903,7 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, int set, BkBufs& b) {
   b.cnt = (uint32_t*)bricks;
   b.off = b.cnt + pl.bg.nbricks;
   b.part_pref = b.off + pl.bg.nbricks;  // nbricks + 1
+  b.order = b.part_pref + pl.bg.nbricks + 4;
   b.wgb = (uint32_t*)wgb;
   b.ctl = (unsigned long long*)ctl;
   b.pra = (uint4*)pra;
@@ -1913,9 +1946,14 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   }
   const unsigned nf = (unsigned)cu_count(v->device);
   const int fv = fuse_variant();
+  const bool lpt_on = [] {  // A/B: DMF_BK_LPT=0 hands the parts out in brick order
+    const char* e = getenv("DMF_BK_LPT");
+    return !(e && atoi(e) == 0);
+  }();
   int64_t j = 0;
   for (int64_t p0 = 0; p0 < P; p0 += pl.PB, ++j) {
     const BkBufs& b = set[pipe ? j & 1 : 0];
+    const uint32_t* lpt = lpt_on ? b.order : nullptr;
     const int64_t pb = std::min<int64_t>(pl.PB, P - p0);
     const int64_t npk = pb * pl.ppose;
     const unsigned nwg = (unsigned)((npk + pl.span - 1) / pl.span);
@@ -1927,7 +1965,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                        npk, pl.span, bg, b.rays, b.cnt, b.wgb, st);
     DMF_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off, b.part_pref,
-                       b.ctl);
+                       b.ctl, b.order);
     DMF_LAUNCH_CHECK();
     if (fv == 48)  // wave-aggregated slot atomics (the previous default)
       hipLaunchKernelGGL((k_bk_pairs<true, true>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
@@ -1950,11 +1988,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
 #define DMF_BK_FUSE_S(R, S, U, N)                                                                              \
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,                \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
-                     (const uint32_t*)b.part_pref, b.ctl, d_hits, d_misses, st)
+                     (const uint32_t*)b.part_pref, (const uint32_t*)lpt, b.ctl, d_hits, d_misses, st)
 #define DMF_BK_FUSE_SB(R, S, U, N)                                                                             \
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,          \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
-                     (const uint32_t*)b.part_pref, b.ctl, d_hits, d_misses, st)
+                     (const uint32_t*)b.part_pref, (const uint32_t*)lpt, b.ctl, d_hits, d_misses, st)
     switch (fv) {
       case 40: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
       case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
