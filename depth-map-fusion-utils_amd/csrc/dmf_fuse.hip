@@ -906,15 +906,16 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
 
 // Scan of the brick counts (one workgroup): list offsets, write cursors, and the part
 // table part_pref[b] = parts of bricks < b (a brick of n pairs has ceil(n / 65535)
-// parts).  ctl[0] = pairs, ctl[1] = parts.  order[] = the parts largest first (counting
-// sort into 64 size classes of 1024 pairs): phase F's queue hands out the big parts
-// first, so the parts left when the queue runs dry are the small ones (the CUs finish
-// together; counter sums do not depend on the order).
+// parts).  ctl[0] = pairs, ctl[1] = parts.  order[] = the parts as (brick, index in the
+// brick), largest first (counting sort into 64 size classes of 1024 pairs): phase F's
+// queue hands out the big parts first, so the parts left when the queue runs dry are the
+// small ones (the CUs finish together; counter sums do not depend on the order), and F
+// needs no search of part_pref for the brick of a part.
 __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* __restrict__ cnt,
                                                   uint32_t* __restrict__ off,
                                                   uint32_t* __restrict__ part_pref,
                                                   unsigned long long* __restrict__ ctl,
-                                                  uint32_t* __restrict__ order) {
+                                                  uint2* __restrict__ order) {
   __shared__ unsigned long long s_pairs[1024];
   __shared__ uint32_t s_parts[1024];
   __shared__ uint32_t s_cls[64];
@@ -966,7 +967,7 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
     const uint32_t np = (cnt[i] + kBkPartMax - 1) / kBkPartMax;
     if (np) {
       const uint32_t pos = atomicAdd(&s_cls[size_class(cnt[i], np)], np);
-      for (uint32_t k = 0; k < np; ++k) order[pos + k] = pbase + k;
+      for (uint32_t k = 0; k < np; ++k) order[pos + k] = make_uint2((uint32_t)i, k);  // (brick, part of it)
     }
     pbase += np;
   }
@@ -1418,7 +1419,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
                                                           const uint32_t* __restrict__ off,
                                                           const uint32_t* __restrict__ cnt,
                                                           const uint32_t* __restrict__ part_pref,
-                                                          const uint32_t* __restrict__ order,
+                                                          const uint2* __restrict__ order,
                                                           unsigned long long* __restrict__ ctl,
                                                           int32_t* __restrict__ hits, int32_t* __restrict__ misses,
                                                           unsigned long long* __restrict__ stats) {
@@ -1447,15 +1448,24 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     __syncthreads();
     DMF_TACC(t_bar, tb0);
     if (sh[0] >= nparts) break;
-    const uint32_t t = order ? order[sh[0]] : sh[0];  // largest parts first (k_bk_scan)
-    int lo = 0, hi = bg.nbricks - 1;  // last brick b with part_pref[b] <= t
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (part_pref[mid] <= t) lo = mid;
-      else hi = mid - 1;
+    int b;
+    uint32_t j;
+    if (order) {  // largest parts first, (brick, index) from k_bk_scan
+      const uint2 o = order[sh[0]];
+      b = (int)o.x;
+      j = o.y;
+    } else {  // brick order: the last brick b with part_pref[b] <= t
+      const uint32_t t = sh[0];
+      int lo = 0, hi = bg.nbricks - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (part_pref[mid] <= t) lo = mid;
+        else hi = mid - 1;
+      }
+      b = lo;
+      j = t - part_pref[b];
     }
-    const int b = lo;
-    const uint32_t np = part_pref[b + 1] - part_pref[b], j = t - part_pref[b], nb_pairs = cnt[b];
+    const uint32_t nb_pairs = cnt[b], np = (nb_pairs + kBkPartMax - 1) / kBkPartMax;
     const uint32_t p0 = off[b] + (uint32_t)(((uint64_t)nb_pairs * j) / np);
     const uint32_t n = (uint32_t)(((uint64_t)nb_pairs * (j + 1)) / np) - (uint32_t)(((uint64_t)nb_pairs * j) / np);
     const int bz = b % bg.nb[2], by = (b / bg.nb[2]) % bg.nb[1], bx = b / (bg.nb[2] * bg.nb[1]);
@@ -1880,7 +1890,8 @@ static int bk_attributes() {
 // control words, per-workgroup bases, pair records.
 struct BkBufs {
   ulonglong2* rays = nullptr;
-  uint32_t *cnt = nullptr, *off = nullptr, *part_pref = nullptr, *order = nullptr, *wgb = nullptr;
+  uint32_t *cnt = nullptr, *off = nullptr, *part_pref = nullptr, *wgb = nullptr;
+  uint2* order = nullptr;
   unsigned long long* ctl = nullptr;
   uint4* pra = nullptr;
   uint2* prb = nullptr;
@@ -1891,9 +1902,9 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, int set, BkBufs& b) {
   const int o = set * kScBkSetStride;
   void *rays, *bricks, *ctl, *wgb, *pra, *prb;
   DMF_TRY(scratch(v, kScBkRays + o, sizeof(ulonglong2) * (size_t)(pl.PB * pl.ppose * 64), &rays));
-  // cnt | off | part_pref (nbricks + 1) | order (every part: <= nbricks + pairs / 65535)
+  // cnt | off | part_pref (nbricks + 1) | order (uint2 per part: <= nbricks + pairs / 65535)
   const size_t max_parts = (size_t)pl.bg.nbricks + pl.pair_cap / kBkPartMax + 1;
-  DMF_TRY(scratch(v, kScBkBricks + o, sizeof(uint32_t) * (3 * (size_t)pl.bg.nbricks + 4 + max_parts), &bricks));
+  DMF_TRY(scratch(v, kScBkBricks + o, sizeof(uint32_t) * (3 * (size_t)pl.bg.nbricks + 6 + 2 * max_parts), &bricks));
   DMF_TRY(scratch(v, kScBkCtl + o, sizeof(unsigned long long) * 4, &ctl));
   // per-workgroup base inside each brick (pass A -> pass B)
   DMF_TRY(scratch(v, kScBkWgBase + o, sizeof(uint32_t) * pl.nwg_max * (size_t)pl.bg.nbricks, &wgb));
@@ -1903,7 +1914,7 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, int set, BkBufs& b) {
   b.cnt = (uint32_t*)bricks;
   b.off = b.cnt + pl.bg.nbricks;
   b.part_pref = b.off + pl.bg.nbricks;  // nbricks + 1
-  b.order = b.part_pref + pl.bg.nbricks + 4;
+  b.order = (uint2*)(b.part_pref + pl.bg.nbricks + 4 + (pl.bg.nbricks & 1));  // 8-B aligned
   b.wgb = (uint32_t*)wgb;
   b.ctl = (unsigned long long*)ctl;
   b.pra = (uint4*)pra;
@@ -1953,7 +1964,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   int64_t j = 0;
   for (int64_t p0 = 0; p0 < P; p0 += pl.PB, ++j) {
     const BkBufs& b = set[pipe ? j & 1 : 0];
-    const uint32_t* lpt = lpt_on ? b.order : nullptr;
+    const uint2* lpt = lpt_on ? b.order : nullptr;
     const int64_t pb = std::min<int64_t>(pl.PB, P - p0);
     const int64_t npk = pb * pl.ppose;
     const unsigned nwg = (unsigned)((npk + pl.span - 1) / pl.span);
@@ -1988,11 +1999,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
 #define DMF_BK_FUSE_S(R, S, U, N)                                                                              \
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,                \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
-                     (const uint32_t*)b.part_pref, (const uint32_t*)lpt, b.ctl, d_hits, d_misses, st)
+                     (const uint32_t*)b.part_pref, lpt, b.ctl, d_hits, d_misses, st)
 #define DMF_BK_FUSE_SB(R, S, U, N)                                                                             \
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,          \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
-                     (const uint32_t*)b.part_pref, (const uint32_t*)lpt, b.ctl, d_hits, d_misses, st)
+                     (const uint32_t*)b.part_pref, lpt, b.ctl, d_hits, d_misses, st)
     switch (fv) {
       case 40: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
       case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
