@@ -1816,9 +1816,10 @@ static int cu_count(int device) {
 // known only on the device (pass A), so the host sizes the pair lists by the geometric
 // bound rays x (1 + brick boundaries a grid-crossing ray can pass), and the fusion call
 // never reads anything back: no host synchronisation, no allocation once reserved
-// (dmf_fuse_reserve).  The bound is ~4-5x the pairs of typical scenes, so the per-volume
-// budget caps the poses per batch instead (default 48 GiB of MI355X's 288 GB; a 512^3 /
-// 640x480 128-frame call fits one batch).
+// (dmf_fuse_reserve).  The bound is ~4-8x the pairs of typical scenes, so the per-volume
+// budget caps the poses per batch instead (default a third of the device's HBM, ~96 GB of
+// MI355X's 288 GB: a 512^3 / 640x480 128-frame call and a 1024^3 / 1280x720 32-frame call
+// each fit one batch).
 
 struct BkPlan {
   BkGeom bg;

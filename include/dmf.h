@@ -239,7 +239,8 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
  * volume, so that dmf_fuse_depth_device then neither allocates nor synchronises (e.g. for
  * hipGraph capture).  The brick pipeline sizes its (ray, brick) pair lists by a geometric
  * bound and splits larger calls into pose batches that fit max_scratch_bytes (0 = keep the
- * current budget; default 48 GiB).  Synchronises the stream once. */
+ * current budget; default a third of the device's memory, ~96 GB on MI355X).  Synchronises
+ * the stream once. */
 int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t max_scratch_bytes);
 /* Elements of one tiled counter array (>= xdim*ydim*zdim: dims padded to 2, 2, 4). */
 int dmf_fuse_counter_cells(const dmf_volume* v, int64_t* n);
