@@ -716,3 +716,61 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, pipe):
         finally:
             _lib.check(L.dmf_fuse_set_variant(0))
         assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
+
+
+def _edge_fusion_cases():
+    """Fusion inputs at the edges of the path: a ragged frame (61x37: packets hang over the
+    right and bottom edges), exactly axis-aligned cameras (integer principal point: one ray
+    per frame runs along a grid axis, its row and column are planar, and a constant depth
+    puts every end on one plane), depths at the [dmin, dmax) bounds, frames with no valid
+    pixel, and a camera whose rays all miss the grid."""
+    from dmf_amd import scene
+    cases = []
+    Kr = np.array([60.0, 0.0, 30.3, 0.0, 60.0, 18.7, 0.0, 0.0, 1.0], np.float32)
+    pr = scene.fibonacci_poses(3, seed=11)
+    dr = np.stack([scene.render(Kr, 61, 37, T)[0] for T in pr])
+    cases.append(("ragged", Kr, 37, 61, pr, dr))
+    Ka = np.array([50.0, 0.0, 32.0, 0.0, 50.0, 24.0, 0.0, 0.0, 1.0], np.float32)
+
+    def pose(R, t):
+        return np.concatenate([np.asarray(R, np.float32), np.asarray(t, np.float32)[:, None]], 1).reshape(12)
+    axis = np.stack([pose(np.eye(3), [0.0, 0.0, -0.9]),                       # looks along +z
+                     pose([[0, 0, 1], [1, 0, 0], [0, 1, 0]], [-0.9, 0.0, 0.0]),   # along +x
+                     pose([[1, 0, 0], [0, 0, -1], [0, 1, 0]], [0.0, 0.9, 0.0])])  # along -y
+    plane = np.full((3, 48, 64), 600, np.uint16)
+    ramp = np.tile(np.linspace(150, 1100, 64).astype(np.uint16), (48, 1))[None].repeat(3, 0)
+    near = axis.copy()
+    near[:, [3, 7, 11]] *= np.float32(0.6 / 0.9)  # 0.1 m from the grid face
+    bounds = np.full((3, 48, 64), 200, np.uint16)
+    bounds[:, ::2, :] = 1000  # dmin is valid, dmax is not
+    cases += [("axis_plane", Ka, 48, 64, axis, plane), ("axis_ramp", Ka, 48, 64, axis, ramp),
+              ("depth_bounds", Ka, 48, 64, near, bounds),
+              ("ends_before_grid", Ka, 48, 64, axis, bounds),
+              ("no_valid_pixel", Ka, 48, 64, axis, np.zeros((3, 48, 64), np.uint16)),
+              ("misses_grid", Ka, 48, 64, pose(np.eye(3), [0.0, 0.0, 0.9])[None], plane[:1])]
+    return cases
+
+
+@pytest.mark.parametrize("variant", [44, 40, 31])
+def test_fuse_edge_cases(oracle, dmf, variant):
+    """Every edge case of _edge_fusion_cases through the slab-walk brick pipeline (44), the
+    per-cell brick walk (40) and k_fuse_l (31): counters and statistics equal the oracle's
+    (zero where nothing is valid or nothing reaches the grid)."""
+    from dmf_amd import _lib
+    L = _lib.load()
+    _lib.check(L.dmf_fuse_set_variant(variant))
+    try:
+        for name, Kc, Hc, Wc, P, D in _edge_fusion_cases():
+            ov = Hh.oracle_volume(oracle, n=96, clouds=[])
+            gv = Hh.gpu_volume(n=96, clouds=[])
+            ho, mo, so = oracle.fuse_depth(ov, Kc, D, P, dmin=200, dmax=1000)
+            eng = dmf.RayTracingEngine(dmf.Camera(Kc, Hc, Wc))
+            hg, mg, sg = eng.fuse_depth(gv, D, P, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
+            assert np.array_equal(so, sg), (name, so, sg)
+            assert np.array_equal(ho, hg) and np.array_equal(mo, mg), name
+            if name in ("no_valid_pixel", "misses_grid", "ends_before_grid"):
+                assert so[0] == 0 and not hg.any() and not mg.any(), name
+            else:
+                assert so[0] > 0, name
+    finally:
+        _lib.check(L.dmf_fuse_set_variant(0))
