@@ -1778,8 +1778,8 @@ static int fuse_variant() {
   return v;
 }
 constexpr int kVariantBrick = 40;
-constexpr int kVariantSlab = 44;  // 44..51: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
-constexpr int kVariantLast = 51;  // 50, 51: branch-free slab body (measured slower)
+constexpr int kVariantSlab = 44;  // 44..53: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
+constexpr int kVariantLast = 53;  // 50, 51: branch-free slab body (measured slower); 53 = the default kernel
 static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantLast; }
 static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantLast); }
 static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
@@ -2023,7 +2023,9 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       case 49: DMF_BK_FUSE_S(32, 8, 4, 2); break;
       case 50: DMF_BK_FUSE_SB(16, 8, 4, 1); break;
       case 51: DMF_BK_FUSE_SB(32, 8, 4, 2); break;
-      default: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // 0, 44
+      case 44: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // the previous default
+      case 52: DMF_BK_FUSE_S(24, 32, 4, 1); break;
+      default: DMF_BK_FUSE_S(24, 16, 4, 1); break;  // 0, 53
     }
 #undef DMF_BK_FUSE
 #undef DMF_BK_FUSE_S
@@ -2091,7 +2093,9 @@ static const char* variant_name(int v) {
     case 49: return "dmf::k_bk_fuse_s<32, 8, 4, 2, false>";
     case 50: return "dmf::k_bk_fuse_s<16, 8, 4, 1, true>";
     case 51: return "dmf::k_bk_fuse_s<32, 8, 4, 2, true>";
-    default: return "dmf::k_bk_fuse_s<16, 8, 4, 1, false>";  // 0, 44; grids over 1024 cells per axis: k_fuse_l<12, 1280>
+    case 44: return "dmf::k_bk_fuse_s<16, 8, 4, 1, false>";
+    case 52: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false>";
+    default: return "dmf::k_bk_fuse_s<24, 16, 4, 1, false>";  // 0, 53; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
 }
 

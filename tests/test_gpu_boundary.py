@@ -11,7 +11,6 @@
 """
 import ctypes as C
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -47,7 +46,7 @@ def _oracle_counts(oracle, depth, poses, n):
     return oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
 
 
-@pytest.mark.parametrize("n,variant", [(96, 44), (96, 40), (96, 31)])
+@pytest.mark.parametrize("n,variant", [(96, 53), (96, 40), (96, 31)])
 def test_fuse_device_never_blocks_the_host(oracle, n, variant):
     """dmf_fuse_depth_device only enqueues (include/dmf.h; brick pipeline and the LDS-box
     kernel): with its stream held busy by a ~1 s spin kernel, the call returns while the
@@ -155,23 +154,16 @@ def test_merge_entry_points_dmf_comm_world1(n):
         _lib.check(L.dmf_comm_destroy(comm))
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def test_merge_over_torch_process_group_world1():
+def test_merge_over_torch_process_group_world1(tmp_path):
     """The bench's path: torch's ProcessGroupNCCL communicator pointer handed to libdmf
-    (one librccl instance in the process), merge-finalize == plain finalize."""
+    (one librccl instance in the process), merge-finalize == plain finalize.  (A file
+    store: a free-port probe can race RCCL's own bootstrap sockets.)"""
     torch, L, _lib, vol, dev, d_depth, d_poses, cam, prm, poses, depth = _setup(80)
     import torch.distributed as dist
     from dmf_amd import dist as D
     import bench
     P = poses.shape[0]
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+    dist.init_process_group("nccl", init_method=f"file://{tmp_path / 'pg_store'}", rank=0, world_size=1,
                             device_id=dev)
     try:
         dist.barrier()

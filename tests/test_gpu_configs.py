@@ -126,7 +126,7 @@ def test_config_full_poses(cfg):
     _invariants(f, c0, s0)
     # the other exact kernels: k_fuse_l (or the slab-walk brick pipeline when the default is
     # k_fuse_l) and the per-cell-walk brick pipeline (variant 40)
-    for other in (31 if k0.startswith("dmf::k_bk_fuse") else 44, 40):
+    for other in (31 if k0.startswith("dmf::k_bk_fuse") else 53, 40):
         c1, s1, k1 = f.run(other)
         assert k0 != k1
         assert np.array_equal(s0[:4], s1[:4])
@@ -141,9 +141,9 @@ def test_config3_batches_equal_single_batch(monkeypatch):
     """Config 3's frames through the brick pipeline in batches of 7 poses == the budget's
     default batching (pose batches accumulate into the same counters)."""
     f = Fusion(512, 1280, 720, 48, seed=99)
-    c0, s0, _ = f.run(44)
+    c0, s0, _ = f.run(53)
     monkeypatch.setenv("DMF_BK_BATCH_POSES", "7")
-    c1, s1, _ = f.run(44)
+    c1, s1, _ = f.run(53)
     assert np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
 
 
@@ -177,7 +177,7 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
     d_poses = torch.from_numpy(poses).to(dev)
     out = {}
     try:
-        for variant in (44, 40, 31):
+        for variant in (53, 40, 31):
             _lib.check(L.dmf_fuse_set_variant(variant))
             c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
             st = torch.zeros(8, dtype=torch.int64, device=dev)
@@ -187,7 +187,7 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
             out[variant] = (c, st.cpu().numpy(), L.dmf_fuse_kernel().decode())
     finally:
         _lib.check(L.dmf_fuse_set_variant(0))
-    (c0, s0, k0), (c1, s1, k1), (c2, s2, k2) = out[44], out[31], out[40]
+    (c0, s0, k0), (c1, s1, k1), (c2, s2, k2) = out[53], out[31], out[40]
     assert k0.startswith("dmf::k_bk_fuse_s") and k1.startswith("dmf::k_fuse_l") and k2.startswith("dmf::k_bk_fuse<")
     assert s0[0] > 10 ** 8 and np.array_equal(s0[:4], s1[:4]) and torch.equal(c0, c1)
     assert np.array_equal(s0[:4], s2[:4]) and torch.equal(c0, c2)
@@ -198,7 +198,7 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
     ov.constructVolume()
     ho, mo, _ = oracle.fuse_depth(ov, K, depth[2:3], poses[2:3], dmin=scene.DEPTH_MIN_MM, dmax=scene.DEPTH_MAX_MM,
                                   threads=16)
-    _lib.check(L.dmf_fuse_set_variant(44))
+    _lib.check(L.dmf_fuse_set_variant(53))
     try:
         c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
         _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth[2].data_ptr(), d_poses[2].data_ptr(), 1,

@@ -580,12 +580,12 @@ def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
             L.dmf_device_free(h, p_)
 
 
-@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51])
+@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53])
 def brick_variant(dmf, request):
     """Select a brick-owned fusion variant for one test: DMF_FUSE_VARIANT 40-43 = the
     per-cell walk (k_bk_fuse: refill threshold, pair order, interleaving), 44-51 = the
     slab walk (k_bk_fuse_s, the default: refill threshold, unroll, two pairs per lane,
-    branch-free body)."""
+    branch-free body, refill threshold 24 with pair order spread 16 / 32: 53 = the default)."""
     from dmf_amd import _lib
     L = _lib.load()
     _lib.check(L.dmf_fuse_set_variant(request.param))
@@ -695,7 +695,7 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
 
 @pytest.mark.parametrize("pipe", ["1", "3"])
 def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, pipe):
-    """The brick pipeline (variants 44 = slab walk, 40 = per-cell walk) split into several pose
+    """The brick pipeline (variants 53 = the default slab walk, 40 = per-cell walk) split into several pose
     batches (DMF_BK_BATCH_POSES=2 over 5 frames: batches of 2, 2, 1) accumulates the same
     counters as the oracle -- one after another, and pipelined over two scratch sets with
     passes A/S/B on the volume's side stream (DMF_BK_PIPE=3)."""
@@ -708,7 +708,7 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, pipe):
     L = _lib.load()
     monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
     monkeypatch.setenv("DMF_BK_PIPE", pipe)
-    for variant, name in ((44, "dmf::k_bk_fuse_s<16, 8, 4, 1, false>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
+    for variant, name in ((53, "dmf::k_bk_fuse_s<24, 16, 4, 1, false>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
         _lib.check(L.dmf_fuse_set_variant(variant))  # the brick pipeline at this small grid
         try:
             hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
@@ -751,9 +751,10 @@ def _edge_fusion_cases():
     return cases
 
 
-@pytest.mark.parametrize("variant", [44, 40, 31])
+@pytest.mark.parametrize("variant", [53, 44, 40, 31])
 def test_fuse_edge_cases(oracle, dmf, variant):
-    """Every edge case of _edge_fusion_cases through the slab-walk brick pipeline (44), the
+    """Every edge case of _edge_fusion_cases through the slab-walk brick pipeline (53 = the
+    default kernel, 44 = its previous parameters), the
     per-cell brick walk (40) and k_fuse_l (31): counters and statistics equal the oracle's
     (zero where nothing is valid or nothing reaches the grid)."""
     from dmf_amd import _lib
