@@ -916,7 +916,7 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
                                                   uint32_t* __restrict__ off,
                                                   uint32_t* __restrict__ part_pref,
                                                   unsigned long long* __restrict__ ctl,
-                                                  uint2* __restrict__ order) {
+                                                  uint2* __restrict__ order, uint32_t part_max) {
   __shared__ unsigned long long s_pairs[1024];
   __shared__ uint32_t s_parts[1024];
   __shared__ uint32_t s_cls[64];
@@ -933,7 +933,7 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
   uint32_t spt = 0;
   for (int i = i0; i < i1; ++i) {
     sp += s_cnt[i];
-    spt += (s_cnt[i] + kBkPartMax - 1) / kBkPartMax;
+    spt += (s_cnt[i] + part_max - 1) / part_max;
   }
   s_pairs[t] = sp;
   s_parts[t] = spt;
@@ -954,7 +954,7 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
     off[i] = (uint32_t)base;
     part_pref[i] = pbase;
     base += s_cnt[i];
-    const uint32_t np = (s_cnt[i] + kBkPartMax - 1) / kBkPartMax;
+    const uint32_t np = (s_cnt[i] + part_max - 1) / part_max;
     pbase += np;
     if (np) atomicAdd(&s_cls[size_class(s_cnt[i], np)], np);
   }
@@ -970,7 +970,7 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
   __syncthreads();
   pbase = pbase0;
   for (int i = i0; i < i1; ++i) {
-    const uint32_t np = (s_cnt[i] + kBkPartMax - 1) / kBkPartMax;
+    const uint32_t np = (s_cnt[i] + part_max - 1) / part_max;
     if (np) {
       const uint32_t pos = atomicAdd(&s_cls[size_class(s_cnt[i], np)], np);
       for (uint32_t k = 0; k < np; ++k) order[pos + k] = make_uint2((uint32_t)i, k);  // (brick, part of it)
@@ -1425,7 +1425,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
                                                           const uint32_t* __restrict__ off,
                                                           const uint32_t* __restrict__ cnt,
                                                           const uint32_t* __restrict__ part_pref,
-                                                          const uint2* __restrict__ order,
+                                                          const uint2* __restrict__ order, uint32_t part_max,
                                                           unsigned long long* __restrict__ ctl,
                                                           int32_t* __restrict__ hits, int32_t* __restrict__ misses,
                                                           unsigned long long* __restrict__ stats) {
@@ -1471,7 +1471,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       b = lo;
       j = t - part_pref[b];
     }
-    const uint32_t nb_pairs = cnt[b], np = (nb_pairs + kBkPartMax - 1) / kBkPartMax;
+    const uint32_t nb_pairs = cnt[b], np = (nb_pairs + part_max - 1) / part_max;
     const uint32_t p0 = off[b] + (uint32_t)(((uint64_t)nb_pairs * j) / np);
     const uint32_t n = (uint32_t)(((uint64_t)nb_pairs * (j + 1)) / np) - (uint32_t)(((uint64_t)nb_pairs * j) / np);
     const int bz = b % bg.nb[2], by = (b / bg.nb[2]) % bg.nb[1], bx = b / (bg.nb[2] * bg.nb[1]);
@@ -1833,6 +1833,7 @@ struct BkPlan {
   int64_t ppose = 0, max_pairs_ray = 0, PB = 0;
   int ab_threads = 0, span = 0;
   int sets = 1;  // scratch buffer sets: 2 = pose batches pipelined (A/S/B of batch j+1 beside F of j)
+  uint32_t part_max = kBkPartMax;  // pairs per part of phase F (DMF_BK_PART_MAX: A/B)
   size_t hist_bytes = 0, nwg_max = 0, pair_cap = 0;
 };
 
@@ -1870,6 +1871,9 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   // packets per workgroup of passes A/B (>= 16 per wave; the histogram's zero + flush
   // amortised over >= 64 packets per 1k bricks)
   pl.span = std::max(16 * (pl.ab_threads / 64), (pl.bg.nbricks + 63) / 64);
+  if (const char* e = getenv("DMF_BK_SPAN")) pl.span = std::max(4, std::min(atoi(e), 4096));  // A/B
+  if (const char* e = getenv("DMF_BK_PART_MAX"))
+    pl.part_max = (uint32_t)std::max(1024, std::min(atoi(e), (int)kBkPartMax));
   pl.hist_bytes = sizeof(uint32_t) * (size_t)pl.bg.nbricks;
   pl.nwg_max = (size_t)((PB * pl.ppose + pl.span - 1) / pl.span);
   pl.pair_cap = (size_t)(PB * rays_pose * pl.max_pairs_ray);
@@ -1910,7 +1914,7 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, int set, BkBufs& b) {
   void *rays, *bricks, *ctl, *wgb, *pra, *prb;
   DMF_TRY(scratch(v, kScBkRays + o, sizeof(ulonglong2) * (size_t)(pl.PB * pl.ppose * 64), &rays));
   // cnt | off | part_pref (nbricks + 1) | order (uint2 per part: <= nbricks + pairs / 65535)
-  const size_t max_parts = (size_t)pl.bg.nbricks + pl.pair_cap / kBkPartMax + 1;
+  const size_t max_parts = (size_t)pl.bg.nbricks + pl.pair_cap / pl.part_max + 1;
   DMF_TRY(scratch(v, kScBkBricks + o, sizeof(uint32_t) * (3 * (size_t)pl.bg.nbricks + 6 + 2 * max_parts), &bricks));
   DMF_TRY(scratch(v, kScBkCtl + o, sizeof(unsigned long long) * 4, &ctl));
   // per-workgroup base inside each brick (pass A -> pass B)
@@ -1983,7 +1987,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                        npk, pl.span, bg, b.rays, b.cnt, b.wgb, st);
     DMF_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off, b.part_pref,
-                       b.ctl, b.order);
+                       b.ctl, b.order, pl.part_max);
     DMF_LAUNCH_CHECK();
     if (fv == 48)  // wave-aggregated slot atomics (the previous default)
       hipLaunchKernelGGL((k_bk_pairs<true, true>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
@@ -2006,11 +2010,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
 #define DMF_BK_FUSE_S(R, S, U, N)                                                                              \
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,                \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
-                     (const uint32_t*)b.part_pref, lpt, b.ctl, d_hits, d_misses, st)
+                     (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st)
 #define DMF_BK_FUSE_SB(R, S, U, N)                                                                             \
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,          \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
-                     (const uint32_t*)b.part_pref, lpt, b.ctl, d_hits, d_misses, st)
+                     (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st)
     switch (fv) {
       case 40: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
       case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
