@@ -1431,6 +1431,16 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
                                                           unsigned long long* __restrict__ stats) {
   __shared__ uint32_t box[kBkBoxWords + 4 + 64];  // counters (skewed), control words, diagnostic words
   uint32_t* sh = box + kBkBoxWords;
+  // (dM, d1, d2) LDS byte strides of a pair, looked up by its record bits 22-28 (step signs,
+  // a step-count bit, hit, major axis): one ds_read instead of ~17 selects per refill
+  // (F -1.3 %); written before the first part's barrier
+  __shared__ uint4 slut[128];
+  if (threadIdx.x < 128) {
+    const uint32_t c = threadIdx.x;
+    const uint32_t sx = c & 1u ? 0u - 4u * kBkSx : 4u * kBkSx, sy = c & 2u ? 0u - 4u * kBkSy : 4u * kBkSy,
+                   sz = c & 4u ? 0u - 4u : 4u, M = (c >> 5) & 3u;
+    slut[c] = make_uint4(M == 0 ? sx : (M == 1 ? sy : sz), M == 0 ? sy : sx, M == 2 ? sy : sz, 0u);
+  }
   stats = stat_slot(stats);
   const int tid = threadIdx.x, l = tid & 63;
   for (int i = tid; i < kBkBoxWords; i += blockDim.x) box[i] = 0;
@@ -1512,13 +1522,10 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       nK1[q] = 0u - K1[q];
       cur[q] = (ra.w & 0xffffu) * 4u;
       r[q] = (int)((ra.x >> 30) | ((ra.y >> 30) << 2) | ((ra.z >> 30) << 4) | (((rb.y >> 25) & 1u) << 6));
-      const uint32_t sx = (rb.y >> 22) & 1u ? 0u - 4u * kBkSx : 4u * kBkSx;
-      const uint32_t sy = (rb.y >> 23) & 1u ? 0u - 4u * kBkSy : 4u * kBkSy;
-      const uint32_t sz = (rb.y >> 24) & 1u ? 0u - 4u : 4u;
-      const uint32_t M = (rb.y >> 27) & 3u;
-      dM[q] = M == 0 ? sx : (M == 1 ? sy : sz);
-      d1[q] = M == 0 ? sy : sx;
-      d2[q] = M == 2 ? sy : sz;
+      const uint4 st3 = slut[(rb.y >> 22) & 127u];
+      dM[q] = st3.x;
+      d1[q] = st3.y;
+      d2[q] = st3.z;
       // the pair's last cell: a hit when the ray ends there inside the grid, else a miss
       atomicAdd(&box[ra.w >> 16], (rb.y >> 26) & 1u ? 0x10000u : 1u);
     };
