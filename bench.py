@@ -220,7 +220,7 @@ def main():
     os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--grid", type=int, default=GRID)
     ap.add_argument("--poses-per-gpu", type=int, default=POSES_PER_GPU)
