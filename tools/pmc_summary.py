@@ -27,11 +27,12 @@ for f in sorted(glob.glob(os.path.join(src, "pmc*", "run_counter_collection.csv"
             continue
         tot[(k, r["Counter_Name"])] += float(r["Counter_Value"])
         ndisp[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
-with open(os.path.join(dst, "pmc_per_kernel.csv"), "w") as f:
-    f.write("kernel,counter,total,dispatches,per_dispatch\n")
+with open(os.path.join(dst, "pmc_per_kernel.csv"), "w", newline="") as f:
+    w = csv.writer(f)  # quoted: template arguments hold commas
+    w.writerow(["kernel", "counter", "total", "dispatches", "per_dispatch"])
     for (k, c), v in sorted(tot.items()):
         n = len(ndisp[(k, c)])
-        f.write(f"{k},{c},{v:.0f},{n},{v / n:.1f}\n")
+        w.writerow([k, c, f"{v:.0f}", n, f"{v / n:.1f}"])
 bench = json.load(open(os.path.join(src, "bench_kt.json")))
 # the fusion launch = every kernel of the fusion pipeline (brick path: k_bk_rays, k_bk_scan,
 # k_bk_pairs, k_bk_fuse; LDS-box path: k_fuse_l alone), priced per bench step
@@ -68,10 +69,11 @@ for r in trace:
     durs[r["Kernel_Name"].split("(")[0].replace("void ", "")].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
 steps, warm = int(bench["steps"]), int(bench["warmup"])
 with open(os.path.join(dst, "kernel_timed_avg.csv"), "w") as f:
-    f.write("kernel,dispatches_total,dispatches_timed,avg_ms_timed\n")
+    w = csv.writer(f)
+    w.writerow(["kernel", "dispatches_total", "dispatches_timed", "avg_ms_timed"])
     for k, v in sorted(durs.items()):
         if not k.startswith("dmf::"):
             continue
         per_call = len(v) // max(steps + warm, 1) if len(v) >= steps + warm else 0
         timed = v[-steps * per_call:] if per_call else v
-        f.write(f"{k},{len(v)},{len(timed)},{sum(timed) / len(timed):.4f}\n")
+        w.writerow([k, len(v), len(timed), f"{sum(timed) / len(timed):.4f}"])
