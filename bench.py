@@ -243,9 +243,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # DMF_BENCH_BACKEND=gloo rehearses the N > 1 path with ranks sharing GPUs (no RCCL: the
+    # merge falls back to torch's all-reduce + finalize); the driver's runs use nccl (= RCCL)
+    backend = os.environ.get("DMF_BENCH_BACKEND", "nccl")
+    local_rank = local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     grid = args.grid
     P = args.poses_per_gpu
@@ -291,7 +298,7 @@ def main():
     comm_ptr = None
     if world > 1:
         dist.barrier()  # connects the RCCL communicator
-        if merge_mode == "rs" and one_rccl_mapped():
+        if backend == "nccl" and merge_mode == "rs" and one_rccl_mapped():
             comm_ptr = D.torch_comm_ptr(device=dev)
         else:
             merge_mode = "torch"
@@ -313,7 +320,7 @@ def main():
             # N = 1: no communicator, the finalize alone (on the comm stream, behind fuse(i+1))
             D.merge_finalize_device(vol, c, pprm, logodds, comm_ptr, rt.lanes["comm"].cuda_stream)
         else:
-            dist.all_reduce(c, op=dist.ReduceOp.SUM)  # fallback: torch's RCCL all-reduce
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)  # fallback: torch's all-reduce (RCCL, or gloo)
             _lib.check(L.dmf_fuse_finalize_device(vol._h, c.data_ptr(), c.data_ptr() + 4 * npad, pprm,
                                                   logodds.data_ptr()))
 
@@ -345,7 +352,7 @@ def main():
     breakdown = {"clear": clear_ms, "fuse": fuse_ms, "merge": merge_ms,
                  "merge_kind": {"rs": "RCCL reduce-scatter(hits, misses) + slab finalize + all-gather(int16) "
                                       "(dmf_fuse_merge_finalize_device)",
-                                "torch": "torch RCCL all-reduce(sum) + finalize"}[merge_mode] if world > 1
+                                "torch": f"torch {'RCCL' if backend == 'nccl' else backend} all-reduce(sum) + finalize"}[merge_mode] if world > 1
                  else "finalize (no collective at N=1)",
                  "schedule": "merge of step i, then the zeroing of its buffer for step i+2, on the comm stream overlap fuse of step i+1 (2 counter buffers)"}
     # grid-wide streaming passes, priced separately: clear writes the
@@ -431,7 +438,8 @@ def main():
                        "grid": grid, "image": f"{WIDTH}x{HEIGHT}", "poses_per_gpu": P, "global_poses": P * world,
                        "parallelism": f"pose-sharded dp{world}" + (
                            " + RCCL reduce-scatter / all-gather merge (libdmf)" if merge_mode == "rs" and world > 1
-                           else " + RCCL all-reduce(sum) merge" if world > 1 else "")},
+                           else f" + {'RCCL' if backend == 'nccl' else backend} all-reduce(sum) merge" if world > 1
+                           else "")},
             "mrays_per_s": rays / elapsed / 1e6,
             "fuse_diagnostics": diagnostics,
             "updates_per_ray": updates / max(rays, 1.0),
