@@ -282,5 +282,60 @@ __host__ __device__ inline void slab_walk(int M, int32_t b1, int32_t b2, int32_t
   }
 }
 
+// Slab ownership code of a pair (phase F's walk bound, the record's 7-bit count field):
+// R = 3 S + s, where S = slabs walked before the one holding the pair's last cell L and
+// s = cells of L's slab before L.  Cell j (0, 1, 2) of slab k is then owned by the walk
+// (before L) iff R - 3k > j, so F tests three constant thresholds per slab instead of
+// counting cells.  cin = crossing counts at the pair's first cell, cL = at L (counts
+// since the ray's start); sb1, sb2 = slab state (b1, b2) at the ray's start (counts 0).
+// Minor m crossed inside L's slab iff its latest crossing (number cL_m) comes after the
+// major axis's crossing number cL_M that opened the slab, i.e. iff at counts
+// (cL_M - 1, cL_m - 1), where both are the next crossings, b_m < 0 (the slab state's
+// "m crosses before M" test with its tie order).  Evaluated in 64 bits: that state need
+// not be one the walk passes through (m's latest crossing may lie far back), so its b can
+// leave the int32 range.  S = 0: R = the pair's cells - 1 (all in its first slab).
+__host__ __device__ inline uint32_t slab_rcode(int M, int32_t sb1, int32_t sb2, uint32_t KM, uint32_t K1, uint32_t K2,
+                                               const int32_t cin[3], const int32_t cL[3]) {
+  const int m1 = M == 0 ? 1 : 0, m2 = M == 2 ? 1 : 2;
+  const int32_t LM = pick3(cL[0], cL[1], cL[2], M), L1 = pick3(cL[0], cL[1], cL[2], m1),
+                L2 = pick3(cL[0], cL[1], cL[2], m2);
+  const int32_t S = LM - pick3(cin[0], cin[1], cin[2], M);
+  const uint32_t steps = (uint32_t)((cL[0] - cin[0]) + (cL[1] - cin[1]) + (cL[2] - cin[2]));
+  const int64_t e1 = (int64_t)sb1 + (int64_t)(LM - 1) * (int64_t)K1 - (int64_t)(L1 - 1) * (int64_t)KM;
+  const int64_t e2 = (int64_t)sb2 + (int64_t)(LM - 1) * (int64_t)K2 - (int64_t)(L2 - 1) * (int64_t)KM;
+  const uint32_t s = (L1 >= 1 && e1 < 0 ? 1u : 0u) + (L2 >= 1 && e2 < 0 ? 1u : 0u);
+  return S == 0 ? steps : 3u * (uint32_t)S + s;
+}
+
+// Phase F's walk bounded by a slab ownership code R (CPU self-test): slab by slab, cell j
+// of slab k is emitted iff R - 3k > j; stops when R - 3k <= 0.
+template <class F>
+__host__ __device__ inline void slab_walk_owned(int M, int32_t b1, int32_t b2, int32_t b12, uint32_t KM, uint32_t K1,
+                                                uint32_t K2, const int32_t st[3], const int32_t p0[3], int R,
+                                                F&& emit) {
+  const int m1 = M == 0 ? 1 : 0, m2 = M == 2 ? 1 : 2;
+  int32_t p[3] = {p0[0], p0[1], p0[2]};
+  for (int t = R; t > 0; t -= 3) {
+    const bool c1 = b1 >= 0, c2 = b2 >= 0, o = b12 >= 0;
+    emit(p[0], p[1], p[2]);
+    // the first minor step is on m2 iff o, also when only one minor crosses: m2 alone
+    // crossing means m2 < next M < m1 in crossing order (and a non-moving m1 / m2 keeps
+    // b12 at +- kNever), so F picks it with one select on o
+    if (c1 || c2) {
+      const int f = o ? m2 : m1, s = o ? m1 : m2;
+      p[f] += st[f];
+      if (t > 1) emit(p[0], p[1], p[2]);
+      if (c1 && c2) {
+        p[s] += st[s];
+        if (t > 2) emit(p[0], p[1], p[2]);
+      }
+    }
+    p[M] += st[M];
+    b1 = (int32_t)((uint32_t)b1 + K1 - (c1 ? KM : 0u));
+    b2 = (int32_t)((uint32_t)b2 + K2 - (c2 ? KM : 0u));
+    b12 = (int32_t)((uint32_t)b12 + (c1 ? K2 : 0u) - (c2 ? K1 : 0u));
+  }
+}
+
 }  // namespace brick
 }  // namespace dmf

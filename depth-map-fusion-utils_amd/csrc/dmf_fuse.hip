@@ -1103,7 +1103,15 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
     };
     const int32_t c00[3] = {0, 0, 0};
     uint4 cur = entry(c00);
-    int32_t idx = 0;  // crossings before the current pair's first cell
+    int32_t idx = 0;                      // crossings before the current pair's first cell
+    int32_t ci0 = 0, ci1 = 0, ci2 = 0;    // SLAB: their counts per axis
+    // count field: SLAB = the slab ownership code of dmf_brick.hpp slab_rcode (F's walk
+    // bound), else the pair's cells - 1; cL = crossing counts at the pair's last cell
+    auto count_field = [&](int32_t L0, int32_t L1, int32_t L2) -> uint32_t {
+      if (!SLAB) return (uint32_t)(L0 + L1 + L2 - idx);
+      const int32_t cin[3] = {ci0, ci1, ci2}, cL[3] = {L0, L1, L2};
+      return bk::slab_rcode(M, sb1, sb2, KM, Km1, Km2, cin, cL);
+    };
     uint32_t slot = 0;
     bk_coarse(bg, R, [&](int b, int a, int bx, int by, int bz) {
       if (a >= 0) {
@@ -1112,14 +1120,16 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
         if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
         else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
         else bk::counts_at(R, 2, boundary_k(2, bz), c);
-        const int32_t nidx = c[0] + c[1] + c[2];
-        put(slot, cur, last_before(c, a), (uint32_t)(nidx - idx - 1), false);
+        put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
         cur = entry(c);
-        idx = nidx;
+        idx = c[0] + c[1] + c[2];
+        ci0 = c[0];
+        ci1 = c[1];
+        ci2 = c[2];
       }
       slot = AGG ? hist_take_agg(hist, b) : atomicAdd(&hist[b], 1u);
     });
-    put(slot, cur, endc, (uint32_t)(R.nsteps - idx), R.end_inside);
+    put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }
 }
 
@@ -1616,8 +1626,12 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
 #pragma unroll
       for (int q = 0; q < NSLOT; ++q) nlanes += (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(r[q] > 0));
 #endif
+      // r is the pair's slab ownership code (dmf_brick.hpp slab_rcode): cell j of the
+      // k-th slab from here is owned iff r - 3k > j.  Inside the block the thresholds move
+      // (3u + j) and r drops by 3 UNROLL once at its end: no per-slab count arithmetic.
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
+        const int t = 3 * u;
 #pragma unroll
         for (int q = 0; q < NSLOT; ++q) {
           if constexpr (BL) {
@@ -1626,13 +1640,13 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
             // interleave)
             const uint32_t n1 = (uint32_t)((int32_t)b1[q] >> 31), n2 = (uint32_t)((int32_t)b2[q] >> 31);  // ~c1, ~c2
             const uint32_t mo = (uint32_t)((int32_t)~b12[q] >> 31);                                        // o
-            const int nc = 3 + (int32_t)n1 + (int32_t)n2;
-            const int v = min(nc, r[q]);
             const uint32_t x1 = d1[q] & ~n1, x2 = d2[q] & ~n2;
-            const uint32_t sel = ~n2 & (n1 | mo);  // c2 && (!c1 || o): the first extra cell is on m2
-            const uint32_t p1 = cur[q] + ((sel & d2[q]) | (~sel & x1)), p2 = cur[q] + x1 + x2;
+            // the first extra cell is on m2 iff o (also when only one minor crosses:
+            // dmf_brick.hpp slab_walk_owned)
+            const uint32_t p1 = cur[q] + ((mo & x2) | (~mo & x1)), p2 = cur[q] + x1 + x2;
             const uint32_t dw = (uint32_t)(kBkBoxWords + 4 + l) * 4u;
-            const uint32_t a0 = v >= 1 ? cur[q] : dw, a1 = v >= 2 ? p1 : dw, a2 = v >= 3 ? p2 : dw;
+            const uint32_t a0 = r[q] > t ? cur[q] : dw, a1 = (r[q] > t + 1 && (n1 & n2) == 0u) ? p1 : dw,
+                           a2 = (r[q] > t + 2 && (n1 | n2) == 0u) ? p2 : dw;
             atomicAdd((uint32_t*)(lds + a0), 1u);
             atomicAdd((uint32_t*)(lds + a1), 1u);
             atomicAdd((uint32_t*)(lds + a2), 1u);
@@ -1640,37 +1654,37 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
             b1[q] += (n1 & K1[q]) | (~n1 & K1mM[q]);
             b2[q] += (n2 & K2[q]) | (~n2 & K2mM[q]);
             b12[q] += (K2[q] & ~n1) + (nK1[q] & ~n2);
-            r[q] -= nc;
             continue;
           }
           const bool c1 = (int32_t)b1[q] >= 0, c2 = (int32_t)b2[q] >= 0, o = (int32_t)b12[q] >= 0;
-          // cells in this slab (1 + c1 + c2) and how many of them the pair still owns
-          const int nc = 3 + ((int32_t)b1[q] >> 31) + ((int32_t)b2[q] >> 31);
-          const int v = min(nc, r[q]);
           const uint32_t x1 = c1 ? d1[q] : 0u, x2 = c2 ? d2[q] : 0u;
-          const uint32_t p1 = cur[q] + ((c2 && (!c1 || o)) ? d2[q] : x1), p2 = cur[q] + x1 + x2;
+          // the slab's cells: cur, then p1 if a minor crosses (on m2 iff o, also when only
+          // one does: dmf_brick.hpp slab_walk_owned), then p2 if both do
+          const uint32_t p1 = cur[q] + (o ? x2 : x1), p2 = cur[q] + x1 + x2;
+          const bool w0 = r[q] > t, w1 = (c1 || c2) && r[q] > t + 1, w2 = c1 && c2 && r[q] > t + 2;
 #if defined(DMF_EXP_NOLDS)  // timing diagnostics only (wrong counts): no walk adds
-          asm volatile("" ::"v"(v), "v"(p1), "v"(p2));
+          asm volatile("" ::"v"(p1), "v"(p2), "v"((int)w0 + (int)w1 + (int)w2));
 #elif defined(DMF_EXP_LDSLANE)  // timing diagnostics only: conflict-free per-lane words
           {
             const uint32_t dw = (uint32_t)(kBkBoxWords + 4 + l) * 4u;
             asm volatile("" ::"v"(p1), "v"(p2));
-            if (v >= 1) atomicAdd((uint32_t*)(lds + dw), 1u);
-            if (v >= 2) atomicAdd((uint32_t*)(lds + dw), 1u);
-            if (v >= 3) atomicAdd((uint32_t*)(lds + dw), 1u);
+            if (w0) atomicAdd((uint32_t*)(lds + dw), 1u);
+            if (w1) atomicAdd((uint32_t*)(lds + dw), 1u);
+            if (w2) atomicAdd((uint32_t*)(lds + dw), 1u);
           }
 #else
-          if (v >= 1) atomicAdd((uint32_t*)(lds + cur[q]), 1u);
-          if (v >= 2) atomicAdd((uint32_t*)(lds + p1), 1u);
-          if (v >= 3) atomicAdd((uint32_t*)(lds + p2), 1u);
+          if (w0) atomicAdd((uint32_t*)(lds + cur[q]), 1u);
+          if (w1) atomicAdd((uint32_t*)(lds + p1), 1u);
+          if (w2) atomicAdd((uint32_t*)(lds + p2), 1u);
 #endif
           cur[q] = p2 + dM[q];
           b1[q] += c1 ? K1mM[q] : K1[q];
           b2[q] += c2 ? K2mM[q] : K2[q];
           b12[q] += (c1 ? K2[q] : 0u) + (c2 ? nK1[q] : 0u);
-          r[q] -= nc;
         }
       }
+#pragma unroll
+      for (int q = 0; q < NSLOT; ++q) r[q] -= 3 * UNROLL;
       DMF_TACC(t_walk, tw0);
     }
     DMF_T(tf0);
