@@ -1800,7 +1800,7 @@ static int fuse_variant() {
 }
 constexpr int kVariantBrick = 40;
 constexpr int kVariantSlab = 44;  // 44..53: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
-constexpr int kVariantLast = 53;  // 50, 51: branch-free slab body (measured slower); 53 = the default kernel
+constexpr int kVariantLast = 56;  // 50, 51: branch-free slab body (measured slower); 53 = the default kernel
 static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantLast; }
 static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantLast); }
 static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
@@ -2049,8 +2049,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       case 50: DMF_BK_FUSE_SB(16, 8, 4, 1); break;
       case 51: DMF_BK_FUSE_SB(32, 8, 4, 2); break;
       case 44: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // the previous default
-      case 52: DMF_BK_FUSE_S(24, 32, 4, 1); break;
-      default: DMF_BK_FUSE_S(24, 16, 4, 1); break;  // 0, 53
+      case 52: DMF_BK_FUSE_S(24, 16, 4, 1); break;  // the default until the ownership-code walk
+      case 54: DMF_BK_FUSE_S(24, 64, 4, 1); break;
+      case 55: DMF_BK_FUSE_S(20, 32, 4, 1); break;
+      case 56: DMF_BK_FUSE_S(28, 32, 4, 1); break;
+      default: DMF_BK_FUSE_S(24, 32, 4, 1); break;  // 0, 53
     }
 #undef DMF_BK_FUSE
 #undef DMF_BK_FUSE_S
@@ -2119,8 +2122,11 @@ static const char* variant_name(int v) {
     case 50: return "dmf::k_bk_fuse_s<16, 8, 4, 1, true>";
     case 51: return "dmf::k_bk_fuse_s<32, 8, 4, 2, true>";
     case 44: return "dmf::k_bk_fuse_s<16, 8, 4, 1, false>";
-    case 52: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false>";
-    default: return "dmf::k_bk_fuse_s<24, 16, 4, 1, false>";  // 0, 53; grids over 1024 cells per axis: k_fuse_l<12, 1280>
+    case 52: return "dmf::k_bk_fuse_s<24, 16, 4, 1, false>";
+    case 54: return "dmf::k_bk_fuse_s<24, 64, 4, 1, false>";
+    case 55: return "dmf::k_bk_fuse_s<20, 32, 4, 1, false>";
+    case 56: return "dmf::k_bk_fuse_s<28, 32, 4, 1, false>";
+    default: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false>";  // 0, 53; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
 }
 

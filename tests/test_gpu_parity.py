@@ -580,12 +580,13 @@ def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
             L.dmf_device_free(h, p_)
 
 
-@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53])
+@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56])
 def brick_variant(dmf, request):
     """Select a brick-owned fusion variant for one test: DMF_FUSE_VARIANT 40-43 = the
     per-cell walk (k_bk_fuse: refill threshold, pair order, interleaving), 44-51 = the
     slab walk (k_bk_fuse_s, the default: refill threshold, unroll, two pairs per lane,
-    branch-free body, refill threshold 24 with pair order spread 16 / 32: 53 = the default)."""
+    branch-free body), 52-56 = refill threshold 20 / 24 / 28 with pair order spread
+    16 / 32 / 64 (53 = <24, 32>, the default)."""
     from dmf_amd import _lib
     L = _lib.load()
     _lib.check(L.dmf_fuse_set_variant(request.param))
@@ -708,7 +709,7 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, pipe):
     L = _lib.load()
     monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
     monkeypatch.setenv("DMF_BK_PIPE", pipe)
-    for variant, name in ((53, "dmf::k_bk_fuse_s<24, 16, 4, 1, false>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
+    for variant, name in ((53, "dmf::k_bk_fuse_s<24, 32, 4, 1, false>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
         _lib.check(L.dmf_fuse_set_variant(variant))  # the brick pipeline at this small grid
         try:
             hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
