@@ -320,9 +320,13 @@ def main():
             # N = 1: no communicator, the finalize alone (on the comm stream, behind fuse(i+1))
             D.merge_finalize_device(vol, c, pprm, logodds, comm_ptr, rt.lanes["comm"].cuda_stream)
         else:
-            dist.all_reduce(c, op=dist.ReduceOp.SUM)  # fallback: torch's all-reduce (RCCL, or gloo)
-            _lib.check(L.dmf_fuse_finalize_device(vol._h, c.data_ptr(), c.data_ptr() + 4 * npad, pprm,
-                                                  logodds.data_ptr()))
+            # fallback: torch's all-reduce (RCCL, or gloo), issued on the comm lane (the current
+            # stream here); the finalize of every slab of the world-padded counters follows it on
+            # the same lane, so it reads the reduced counters and precedes the buffer's clear,
+            # which run_steps also enqueues on the comm lane
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)
+            _lib.check(L.dmf_fuse_finalize_slab_device(vol._h, c.data_ptr(), pprm, logodds.data_ptr(), world, -1,
+                                                       rt.lanes["comm"].cuda_stream))
 
     def marks(i, name, lane):
         e = torch.cuda.Event(enable_timing=True)

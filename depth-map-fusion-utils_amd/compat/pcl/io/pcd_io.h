@@ -69,6 +69,14 @@ int loadPCDFile(const std::string& file, PointCloud<PointT>& cloud) {
     }
   }
   if (fields.empty() || (data != "ascii" && data != "binary")) return -1;
+  // untrusted header: TYPE F is 4 or 8 bytes, U / I 1, 2, 4 or 8; COUNT >= 1 (and bounded,
+  // so the record stride cannot overflow)
+  for (const auto& f : fields) {
+    const bool ok_size = f.type == 'F' ? (f.size == 4 || f.size == 8)
+                                       : ((f.type == 'U' || f.type == 'I') &&
+                                          (f.size == 1 || f.size == 2 || f.size == 4 || f.size == 8));
+    if (!ok_size || f.count < 1 || f.count > (1 << 20)) return -1;
+  }
   cloud.points.assign(points, PointT());
   cloud.is_dense = true;
   size_t stride = 0;

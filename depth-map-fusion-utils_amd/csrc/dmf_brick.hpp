@@ -337,5 +337,60 @@ __host__ __device__ inline void slab_walk_owned(int M, int32_t b1, int32_t b2, i
   }
 }
 
+// ---- 20-byte pair record: the slab walk on scaled state ----
+//
+// Every K is 2Q|dq| = 512 |dq|, and every update of the slab state (b1, b2, b12) adds a
+// sum of K's, so b mod 512 never changes along a walk, and b >= 0 <=> floor(b / 512) >= 0.
+// Hence the walk runs EXACTLY on beta = b >> 9 (arithmetic shift = floor division) with
+// increments |dq| instead of K: the low 9 bits of b never influence a decision.  Range:
+// |b| < (2Q + 1) max|dq| gives |beta| < 2^18 + 2^9 for grids <= 1024 cells per axis
+// (|dq| < 2^18), a 20-bit two's-complement field; the +-never constant of a non-moving
+// axis (only its sign is ever used) is stored as +-(2^19 - 1).
+//   w0 = beta1 | aM[0:12) << 20          w1 = beta2 | aM[12:18) << 20 | R[0:6) << 26
+//   w2 = beta12 | a1[0:12) << 20         w3 = entry word | last word << 16
+//   w4 = a2 | a1[12:18) << 18 | R[6] << 24 | step signs (x, y, z) << 25 | M << 28 | ends << 30
+// (a = |dq| of the major / minor axes, R = the ownership code of slab_rcode, entry / last =
+// word offsets of the pair's first / last cell in phase F's LDS box).  w[4] >> 24 is the
+// 7-bit stride-table index of phase F.
+__host__ __device__ inline uint32_t beta20(int32_t b) {
+  const int32_t lim = (1 << 19) - 1;
+  const int32_t s = b >> 9;  // arithmetic shift: floor(b / 512)
+  return (uint32_t)(s > lim ? lim : (s < -lim ? -lim : s)) & 0xfffffu;
+}
+
+__host__ __device__ inline void pack20(int32_t b1, int32_t b2, int32_t b12, uint32_t aM, uint32_t a1, uint32_t a2,
+                                       uint32_t entry, uint32_t last, uint32_t R, uint32_t signs, uint32_t M,
+                                       bool ends, uint32_t w[5]) {
+  w[0] = beta20(b1) | (aM & 0xfffu) << 20;
+  w[1] = beta20(b2) | ((aM >> 12) & 0x3fu) << 20 | (R & 0x3fu) << 26;
+  w[2] = beta20(b12) | (a1 & 0xfffu) << 20;
+  w[3] = entry | last << 16;
+  w[4] = a2 | ((a1 >> 12) & 0x3fu) << 18 | ((R >> 6) & 1u) << 24 | signs << 25 | M << 28 | (ends ? 1u << 30 : 0u);
+}
+
+struct Slab20 {
+  int32_t b1, b2, b12;  // beta state
+  uint32_t aM, a1, a2;  // |dq| of the major / minor axes (the beta walk's K)
+  uint32_t entry, last, R, signs, M;
+  bool ends;
+};
+
+__host__ __device__ inline int32_t sext20(uint32_t w) { return (int32_t)(w << 12) >> 12; }
+
+__host__ __device__ inline void unpack20(const uint32_t w[5], Slab20& s) {
+  s.b1 = sext20(w[0]);
+  s.b2 = sext20(w[1]);
+  s.b12 = sext20(w[2]);
+  s.aM = (w[0] >> 20) | ((w[1] >> 20) & 0x3fu) << 12;
+  s.a1 = (w[2] >> 20) | ((w[4] >> 18) & 0x3fu) << 12;
+  s.a2 = w[4] & 0x3ffffu;
+  s.entry = w[3] & 0xffffu;
+  s.last = w[3] >> 16;
+  s.R = (w[1] >> 26) | ((w[4] >> 24) & 1u) << 6;
+  s.signs = (w[4] >> 25) & 7u;
+  s.M = (w[4] >> 28) & 3u;
+  s.ends = ((w[4] >> 30) & 1u) != 0;
+}
+
 }  // namespace brick
 }  // namespace dmf

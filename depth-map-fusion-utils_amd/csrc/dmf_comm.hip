@@ -34,11 +34,64 @@ static int comm_shape(void* comm, int* nranks, int* rank) {
   return DMF_OK;
 }
 
-// Tile rows per rank of the padded counter layout (whole rows, equal counts per rank).
-static int64_t rows_per_rank(const dmf_volume* v, int nranks) {
-  int64_t ntx, tpr;
-  tile_rows(v, &ntx, &tpr);
-  return (ntx + nranks - 1) / nranks;
+// The merge's slab arithmetic for `rank` of `nranks` (rank = -1: the whole grid, as one
+// rank that holds every slab) on a grid of dims (x, y, z), shared by the collective merge
+// and the exported plans.  Tile rows (2 x-rows of 2x2x4-cell tiles) per rank:
+// whole rows, equal counts per rank, the counter arrays padded to nranks * rows rows.
+static dmf_merge_plan merge_plan_dims(int64_t xd, int64_t yd, int64_t zd, int nranks, int rank) {
+  const int64_t ntx = (xd + 1) >> 1, tpr = ((yd + 1) >> 1) * ((zd + 3) >> 2);
+  const int64_t rows = (ntx + nranks - 1) / nranks;
+  dmf_merge_plan p{};
+  p.n_padded = rows * nranks * tpr * 16;
+  p.chunk = rows * tpr * 16;
+  p.logodds_padded = rows * nranks * 2 * yd * zd;
+  p.slab_bytes = rows * 2 * yd * zd * (int64_t)sizeof(int16_t);
+  if (rank < 0) {
+    p.chunk_offset = 0;
+    p.tile_begin = 0;
+    p.tile_end = ntx * tpr;
+    p.slab_offset = 0;
+  } else {
+    p.chunk_offset = rank * p.chunk;
+    // the rank's slab: tile rows [rank*rows, (rank+1)*rows) clipped to the grid (the last
+    // ranks of a grid with fewer tile rows than ranks * rows hold padding only)
+    p.tile_begin = std::min<int64_t>(ntx, rank * rows) * tpr;
+    p.tile_end = std::min<int64_t>(ntx, (rank + 1) * rows) * tpr;
+    p.slab_offset = rank * p.slab_bytes;
+  }
+  return p;
+}
+
+static dmf_merge_plan merge_plan(const dmf_volume* v, int nranks, int rank) {
+  return merge_plan_dims(v->xdim, v->ydim, v->zdim, nranks, rank);
+}
+
+// ncclGroupStart / ncclGroupEnd as a scope: an early error return between them still
+// closes the group (a group left open would absorb the caller's later collectives).
+struct NcclGroup {
+  bool open = false;
+  ncclResult_t start() {
+    const ncclResult_t r = ncclGroupStart();
+    open = r == ncclSuccess;
+    return r;
+  }
+  ncclResult_t end() {
+    open = false;
+    return ncclGroupEnd();
+  }
+  ~NcclGroup() {
+    if (open) ncclGroupEnd();
+  }
+};
+
+// Voxel::view merge: the smallest non-zero id over the ranks (0 = never viewed).
+__global__ void k_view_zero_to_max(int32_t* view, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && view[i] == 0) view[i] = INT32_MAX;
+}
+__global__ void k_view_max_to_zero(int32_t* view, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && view[i] == INT32_MAX) view[i] = 0;
 }
 
 }  // namespace dmf
@@ -91,9 +144,7 @@ int dmf_fuse_counter_cells_padded(const dmf_volume* v, int32_t nranks, int64_t* 
   DMF_API_BEGIN
   if (!n || nranks < 1) return fail(DMF_ERR_INVALID, "bad argument");
   DMF_TRY(require_constructed(v));
-  int64_t ntx, tpr;
-  tile_rows(v, &ntx, &tpr);
-  *n = rows_per_rank(v, nranks) * nranks * tpr * 16;
+  *n = merge_plan(v, nranks, 0).n_padded;
   return DMF_OK;
   DMF_API_END
 }
@@ -102,8 +153,39 @@ int dmf_fuse_logodds_cells_padded(const dmf_volume* v, int32_t nranks, int64_t* 
   DMF_API_BEGIN
   if (!n || nranks < 1) return fail(DMF_ERR_INVALID, "bad argument");
   DMF_TRY(require_constructed(v));
-  *n = rows_per_rank(v, nranks) * nranks * 2 * (int64_t)v->ydim * v->zdim;
+  *n = merge_plan(v, nranks, 0).logodds_padded;
   return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_fuse_merge_plan(const dmf_volume* v, int32_t nranks, int32_t rank, dmf_merge_plan* out) {
+  DMF_API_BEGIN
+  if (!out || nranks < 1 || rank < -1 || rank >= nranks) return fail(DMF_ERR_INVALID, "bad argument");
+  DMF_TRY(require_constructed(v));
+  *out = merge_plan(v, nranks, rank);
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_fuse_merge_plan_dims(int32_t xdim, int32_t ydim, int32_t zdim, int32_t nranks, int32_t rank,
+                             dmf_merge_plan* out) {
+  DMF_API_BEGIN
+  if (!out || nranks < 1 || rank < -1 || rank >= nranks || xdim < 1 || ydim < 1 || zdim < 1)
+    return fail(DMF_ERR_INVALID, "bad argument");
+  *out = merge_plan_dims(xdim, ydim, zdim, nranks, rank);
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_fuse_finalize_slab_device(dmf_volume* v, const int32_t* d_counters, const dmf_fuse_params* prm,
+                                  int16_t* d_logodds, int32_t nranks, int32_t rank, void* stream) {
+  DMF_API_BEGIN
+  DMF_TRY(require_constructed(v));
+  if (!d_counters || !prm || !d_logodds) return fail(DMF_ERR_INVALID, "null argument");
+  if (nranks < 1 || rank < -1 || rank >= nranks) return fail(DMF_ERR_INVALID, "bad rank %d of %d", rank, nranks);
+  const hipStream_t st = stream ? (hipStream_t)stream : v->stream;
+  const dmf_merge_plan p = merge_plan(v, nranks, rank);
+  return finalize_tiles(v, d_counters, d_counters + p.n_padded, prm, d_logodds, p.tile_begin, p.tile_end, st);
   DMF_API_END
 }
 
@@ -128,25 +210,23 @@ int dmf_fuse_merge_finalize_device(dmf_volume* v, int32_t* d_counters, const dmf
   if (!d_counters || !prm || !d_logodds) return fail(DMF_ERR_INVALID, "null argument");
   int nr = 1, rk = 0;
   if (comm) DMF_TRY(comm_shape(comm, &nr, &rk));  // NULL: one rank, no collective
-  int64_t ntx, tpr;
-  tile_rows(v, &ntx, &tpr);
-  const int64_t rows = rows_per_rank(v, nr);
-  const int64_t n_pad = rows * nr * tpr * 16;      // elements per counter array
-  const size_t chunk = (size_t)(rows * tpr * 16);  // this rank's reduced slab of each
+  const dmf_merge_plan p = merge_plan(v, nr, rk);
   int32_t* d_hits = d_counters;
-  int32_t* d_miss = d_counters + n_pad;
-  if (comm) {
-    DMF_NCCL(ncclGroupStart());
-    DMF_NCCL(ncclReduceScatter(d_hits, d_hits + rk * chunk, chunk, ncclInt32, ncclSum, (ncclComm_t)comm, st));
-    DMF_NCCL(ncclReduceScatter(d_miss, d_miss + rk * chunk, chunk, ncclInt32, ncclSum, (ncclComm_t)comm, st));
-    DMF_NCCL(ncclGroupEnd());
+  int32_t* d_miss = d_counters + p.n_padded;
+  if (comm) {  // in place: this rank's reduced slab lands at its own offset of each array
+    NcclGroup grp;
+    DMF_NCCL(grp.start());
+    DMF_NCCL(ncclReduceScatter(d_hits, d_hits + p.chunk_offset, (size_t)p.chunk, ncclInt32, ncclSum,
+                               (ncclComm_t)comm, st));
+    DMF_NCCL(ncclReduceScatter(d_miss, d_miss + p.chunk_offset, (size_t)p.chunk, ncclInt32, ncclSum,
+                               (ncclComm_t)comm, st));
+    DMF_NCCL(grp.end());
   }
-  // the rank's slab: tile rows [rk*rows, (rk+1)*rows) clipped to the grid
-  const int64_t r0 = std::min<int64_t>(ntx, rk * rows), r1 = std::min<int64_t>(ntx, (rk + 1) * rows);
-  DMF_TRY(finalize_tiles(v, d_hits, d_miss, prm, d_logodds, r0 * tpr, r1 * tpr, st));
+  DMF_TRY(finalize_tiles(v, d_hits, d_miss, prm, d_logodds, p.tile_begin, p.tile_end, st));
   // int16 slabs of 2*rows x-rows each, gathered in rank order (bytes: RCCL has no int16)
-  const size_t slab = (size_t)(rows * 2 * (int64_t)v->ydim * v->zdim) * sizeof(int16_t);
-  if (comm) DMF_NCCL(ncclAllGather((const char*)d_logodds + rk * slab, d_logodds, slab, ncclUint8, (ncclComm_t)comm, st));
+  if (comm)
+    DMF_NCCL(ncclAllGather((const char*)d_logodds + p.slab_offset, d_logodds, (size_t)p.slab_bytes, ncclUint8,
+                           (ncclComm_t)comm, st));
   return DMF_OK;
   DMF_API_END
 }
@@ -158,10 +238,20 @@ int dmf_flags_allreduce(dmf_volume* v, void* comm, void* stream) {
   int nr, rk;
   DMF_TRY(comm_shape(comm, &nr, &rk));
   if (v->V == 0) return DMF_OK;
-  DMF_NCCL(ncclGroupStart());
-  DMF_NCCL(ncclAllReduce(v->d_view, v->d_view, (size_t)v->V, ncclInt32, ncclMax, (ncclComm_t)comm, st));
-  DMF_NCCL(ncclAllReduce(v->d_good, v->d_good, (size_t)v->V, ncclUint8, ncclMax, (ncclComm_t)comm, st));
-  DMF_NCCL(ncclGroupEnd());
+  const int64_t n = (int64_t)v->V;
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  // view: the smallest non-zero id (0 -> INT32_MAX, min, back); good: max (a flag)
+  hipLaunchKernelGGL(k_view_zero_to_max, dim3(nb), dim3(256), 0, st, v->d_view, n);
+  DMF_LAUNCH_CHECK();
+  {
+    NcclGroup grp;
+    DMF_NCCL(grp.start());
+    DMF_NCCL(ncclAllReduce(v->d_view, v->d_view, (size_t)n, ncclInt32, ncclMin, (ncclComm_t)comm, st));
+    DMF_NCCL(ncclAllReduce(v->d_good, v->d_good, (size_t)n, ncclUint8, ncclMax, (ncclComm_t)comm, st));
+    DMF_NCCL(grp.end());
+  }
+  hipLaunchKernelGGL(k_view_max_to_zero, dim3(nb), dim3(256), 0, st, v->d_view, n);
+  DMF_LAUNCH_CHECK();
   return DMF_OK;
   DMF_API_END
 }

@@ -1016,12 +1016,17 @@ __device__ inline uint32_t bk_e30(int32_t e) {
 #else
 #define DMF_BK_PAIRS_ATTR
 #endif
-template <bool SLAB, bool AGG = true>
+// R20 (SLAB only; the default): the 20-byte record of dmf_brick.hpp pack20 (beta state,
+// pa = words 0-3, pb = word 4 as uint32) instead of the 24-byte one.
+template <bool SLAB, bool AGG = true, bool R20 = false>
 __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
                                                          const uint32_t* __restrict__ wg_base, uint4* __restrict__ pa,
-                                                         uint2* __restrict__ pb) {
+                                                         void* __restrict__ pbv) {
+  static_assert(SLAB || !R20, "the 20-byte record carries the slab state");
+  uint2* const pb = (uint2*)pbv;
+  uint32_t* const pw = (uint32_t*)pbv;
   extern __shared__ uint32_t hist[];
   // this workgroup's range in brick i starts at off[i] + wg_base[wg][i] (pass A); entries
   // of bricks pass A did not count for this workgroup are never used
@@ -1059,18 +1064,19 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
                            : make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
                                         (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18) | signs);
     // entry state of the pair being built (E fields without the step bits)
+    // (the exact int32 state; put() formats it)
     auto entry = [&](const int32_t c[3]) {
       uint4 e;
       if (SLAB) {  // b = b(0) + c_M K_m - c_m K_M;  b12 = b12(0) + c_1 K_2 - c_2 K_1
         const uint32_t cM = (uint32_t)bk::pick3(c[0], c[1], c[2], M), c1 = (uint32_t)bk::pick3(c[0], c[1], c[2], m1),
                        c2 = (uint32_t)bk::pick3(c[0], c[1], c[2], m2);
-        e.x = bk_e30((int32_t)((uint32_t)sb1 + cM * Km1 - c1 * KM));
-        e.y = bk_e30((int32_t)((uint32_t)sb2 + cM * Km2 - c2 * KM));
-        e.z = bk_e30((int32_t)((uint32_t)sb12 + c1 * Km2 - c2 * Km1));
+        e.x = (uint32_t)sb1 + cM * Km1 - c1 * KM;
+        e.y = (uint32_t)sb2 + cM * Km2 - c2 * KM;
+        e.z = (uint32_t)sb12 + c1 * Km2 - c2 * Km1;
       } else {
-        e.x = bk_e30((int32_t)(e01 + (uint32_t)c[0] * K1 - (uint32_t)c[1] * K0));
-        e.y = bk_e30((int32_t)(e02 + (uint32_t)c[0] * K2 - (uint32_t)c[2] * K0));
-        e.z = bk_e30((int32_t)(e12 + (uint32_t)c[1] * K2 - (uint32_t)c[2] * K1));
+        e.x = e01 + (uint32_t)c[0] * K1 - (uint32_t)c[1] * K0;
+        e.y = e02 + (uint32_t)c[0] * K2 - (uint32_t)c[2] * K0;
+        e.z = e12 + (uint32_t)c[1] * K2 - (uint32_t)c[2] * K1;
       }
       const uint32_t x = (uint32_t)(R.cs[0] + R.st[0] * c[0]) & m5, y = (uint32_t)(R.cs[1] + R.st[1] * c[1]) & m5,
                      z = (uint32_t)(R.cs[2] + R.st[2] * c[2]) & m5;
@@ -1085,12 +1091,20 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
       return bk_lds_word(x, y, z);
     };
     auto put = [&](uint32_t slot, uint4 e, uint32_t last, uint32_t steps, bool ends) {
-      e.x |= (steps & 3u) << 30;
-      e.y |= ((steps >> 2) & 3u) << 30;
-      e.z |= ((steps >> 4) & 3u) << 30;
-      e.w |= last << 16;
-      pa[slot] = e;
-      pb[slot] = make_uint2(wb0.x, wb0.y | ((steps >> 6) << 25) | (ends ? 1u << 26 : 0u));
+      if constexpr (R20) {
+        uint32_t w[5];
+        bk::pack20((int32_t)e.x, (int32_t)e.y, (int32_t)e.z, aM, a1, a2, e.w, last, steps, signs >> 22, (uint32_t)M,
+                   ends, w);
+        pa[slot] = make_uint4(w[0], w[1], w[2], w[3]);
+        pw[slot] = w[4];
+      } else {
+        e.x = bk_e30((int32_t)e.x) | (steps & 3u) << 30;
+        e.y = bk_e30((int32_t)e.y) | ((steps >> 2) & 3u) << 30;
+        e.z = bk_e30((int32_t)e.z) | ((steps >> 4) & 3u) << 30;
+        e.w |= last << 16;
+        pa[slot] = e;
+        pb[slot] = make_uint2(wb0.x, wb0.y | ((steps >> 6) << 25) | (ends ? 1u << 26 : 0u));
+      }
     };
     // the end cell (brick-local): the last cell of the ray's last pair
     const uint32_t endc = bk_lds_word((uint32_t)R.ce[0] & m5, (uint32_t)R.ce[1] & m5, (uint32_t)R.ce[2] & m5);
@@ -1429,9 +1443,11 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
 // dependency chains: at 4 waves per SIMD a single chain leaves the SIMD idle between
 // its dependent instructions).  A wave refills when >= REFILL of its 64 * NSLOT slots
 // are idle, from per-slot records prefetched one refill ahead.
-template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, bool BL = false>
+// R20: 20-byte records (dmf_brick.hpp pack20): the walk runs on the beta state with
+// increments |dq| (exactly the same decisions as b with K = 512 |dq|).
+template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, bool BL = false, bool R20 = false>
 __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, const uint4* __restrict__ pa,
-                                                          const uint2* __restrict__ pb,
+                                                          const void* __restrict__ pbv,
                                                           const uint32_t* __restrict__ off,
                                                           const uint32_t* __restrict__ cnt,
                                                           const uint32_t* __restrict__ part_pref,
@@ -1445,10 +1461,14 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
   // a step-count bit, hit, major axis): one ds_read instead of ~17 selects per refill
   // (F -1.3 %); written before the first part's barrier
   __shared__ uint4 slut[128];
+  const uint2* const pb = (const uint2*)pbv;
+  const uint32_t* const pw = (const uint32_t*)pbv;
   if (threadIdx.x < 128) {
-    const uint32_t c = threadIdx.x;
-    const uint32_t sx = c & 1u ? 0u - 4u * kBkSx : 4u * kBkSx, sy = c & 2u ? 0u - 4u * kBkSy : 4u * kBkSy,
-                   sz = c & 4u ? 0u - 4u : 4u, M = (c >> 5) & 3u;
+    // 24-B record: index bits 0-2 = step signs, 5-6 = M; 20-B record (w4 >> 24): 1-3 = step
+    // signs, 4-5 = M
+    const uint32_t c = threadIdx.x, sg = R20 ? c >> 1 : c, M = R20 ? (c >> 4) & 3u : (c >> 5) & 3u;
+    const uint32_t sx = sg & 1u ? 0u - 4u * kBkSx : 4u * kBkSx, sy = sg & 2u ? 0u - 4u * kBkSy : 4u * kBkSy,
+                   sz = sg & 4u ? 0u - 4u : 4u;
     slut[c] = make_uint4(M == 0 ? sx : (M == 1 ? sy : sz), M == 0 ? sy : sx, M == 2 ? sy : sz, 0u);
   }
   stats = stat_slot(stats);
@@ -1520,6 +1540,27 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     auto decode = [&](int q) {
       const uint4 ra = ca[q];
       const uint2 rb = cb[q];
+      if constexpr (R20) {
+        const uint32_t w[5] = {ra.x, ra.y, ra.z, ra.w, rb.x};
+        bk::Slab20 sd;
+        bk::unpack20(w, sd);
+        b1[q] = (uint32_t)sd.b1;
+        b2[q] = (uint32_t)sd.b2;
+        b12[q] = (uint32_t)sd.b12;
+        K1[q] = sd.a1;
+        K2[q] = sd.a2;
+        K1mM[q] = sd.a1 - sd.aM;
+        K2mM[q] = sd.a2 - sd.aM;
+        nK1[q] = 0u - sd.a1;
+        cur[q] = sd.entry * 4u;
+        r[q] = (int)sd.R;
+        const uint4 st3 = slut[rb.x >> 24 & 127u];
+        dM[q] = st3.x;
+        d1[q] = st3.y;
+        d2[q] = st3.z;
+        atomicAdd(&box[sd.last], sd.ends ? 0x10000u : 1u);
+        return;
+      }
       b1[q] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ra.x, 0, 30);
       b2[q] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ra.y, 0, 30);
       b12[q] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ra.z, 0, 30);
@@ -1558,7 +1599,8 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
           if (fok[q]) {
             const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
             ca[q] = pa[i];
-            cb[q] = pb[i];
+            if constexpr (R20) cb[q] = make_uint2(pw[i], 0u);
+            else cb[q] = pb[i];
           }
         }
         base += (uint32_t)__builtin_popcountll(need[q]);
@@ -1800,7 +1842,9 @@ static int fuse_variant() {
 }
 constexpr int kVariantBrick = 40;
 constexpr int kVariantSlab = 44;  // 44..53: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
-constexpr int kVariantLast = 56;  // 50, 51: branch-free slab body (measured slower); 53 = the default kernel
+constexpr int kVariantLast = 57;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
+constexpr int kVariantRec20 = 57;  // the default: 20-B pair records (beta state, dmf_brick.hpp pack20)
+static bool is_rec20_variant(int v) { return v == 0 || v == kVariantRec20; }
 static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantLast; }
 static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantLast); }
 static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
@@ -1855,6 +1899,7 @@ struct BkPlan {
   int ab_threads = 0, span = 0;
   int sets = 1;  // scratch buffer sets: 2 = pose batches pipelined (A/S/B of batch j+1 beside F of j)
   uint32_t part_max = kBkPartMax;  // pairs per part of phase F (DMF_BK_PART_MAX: A/B)
+  size_t rec_bytes = 24;           // bytes per pair record: 16 (pa) + 8 (pb) or, 20-B records, 16 + 4
   size_t hist_bytes = 0, nwg_max = 0, pair_cap = 0;
 };
 
@@ -1874,7 +1919,8 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   pl.max_pairs_ray = 1 + (pl.bg.nb[0] - 1) + (pl.bg.nb[1] - 1) + (pl.bg.nb[2] - 1);
   const int64_t rays_pose = pl.ppose * 64;
   const int64_t ray_cap = (int64_t)UINT32_MAX / pl.max_pairs_ray;  // pair offsets are 32-bit
-  const uint64_t per_pose = (uint64_t)rays_pose * (uint64_t)pl.max_pairs_ray * (sizeof(uint4) + sizeof(uint2));
+  pl.rec_bytes = is_rec20_variant(fuse_variant()) ? 20 : 24;
+  const uint64_t per_pose = (uint64_t)rays_pose * (uint64_t)pl.max_pairs_ray * pl.rec_bytes;
   const int chunks = bk_pipe_chunks();
   // two buffer sets share the budget when the batches are pipelined (opt-in: measured
   // slower, DESIGN.md §5.3 -- A/B beside F slow down 2-5x and F by ~7 %)
@@ -1915,6 +1961,8 @@ static int bk_attributes() {
                                 (int)(sizeof(uint32_t) * 32768)));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(sizeof(uint32_t) * 32768)));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(uint32_t) * 32768)));
     attr_set.store(true);
   }
   return DMF_OK;
@@ -1928,7 +1976,7 @@ struct BkBufs {
   uint2* order = nullptr;
   unsigned long long* ctl = nullptr;
   uint4* pra = nullptr;
-  uint2* prb = nullptr;
+  void* prb = nullptr;  // uint2 per pair (24-B records) or uint32 (20-B records)
 };
 
 // Scratch set `set` of a plan (allocates only when a slot is too small).
@@ -1943,7 +1991,7 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, int set, BkBufs& b) {
   // per-workgroup base inside each brick (pass A -> pass B)
   DMF_TRY(scratch(v, kScBkWgBase + o, sizeof(uint32_t) * pl.nwg_max * (size_t)pl.bg.nbricks, &wgb));
   DMF_TRY(scratch(v, kScBkPairs + o, sizeof(uint4) * pl.pair_cap, &pra));
-  DMF_TRY(scratch(v, kScBkPairsB + o, sizeof(uint2) * pl.pair_cap, &prb));
+  DMF_TRY(scratch(v, kScBkPairsB + o, (pl.rec_bytes - sizeof(uint4)) * pl.pair_cap, &prb));
   b.rays = (ulonglong2*)rays;
   b.cnt = (uint32_t*)bricks;
   b.off = b.cnt + pl.bg.nbricks;
@@ -1952,7 +2000,7 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, int set, BkBufs& b) {
   b.wgb = (uint32_t*)wgb;
   b.ctl = (unsigned long long*)ctl;
   b.pra = (uint4*)pra;
-  b.prb = (uint2*)prb;
+  b.prb = prb;
   return DMF_OK;
 }
 
@@ -2015,6 +2063,9 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     if (fv == 48)  // wave-aggregated slot atomics (the previous default)
       hipLaunchKernelGGL((k_bk_pairs<true, true>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
                          (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
+    else if (is_rec20_variant(fv))
+      hipLaunchKernelGGL((k_bk_pairs<true, false, true>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span,
+                         bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
     else if (is_slab_variant(fv))
       hipLaunchKernelGGL((k_bk_pairs<true, false>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
                          (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
@@ -2033,6 +2084,10 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
 #define DMF_BK_FUSE_S(R, S, U, N)                                                                              \
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,                \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
+                     (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st)
+#define DMF_BK_FUSE_S20(R, S, U, N)                                                                            \
+  hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N, false, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,   \
+                     (const uint4*)b.pra, (const void*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,    \
                      (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st)
 #define DMF_BK_FUSE_SB(R, S, U, N)                                                                             \
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,          \
@@ -2055,11 +2110,13 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       case 54: DMF_BK_FUSE_S(24, 64, 4, 1); break;
       case 55: DMF_BK_FUSE_S(20, 32, 4, 1); break;
       case 56: DMF_BK_FUSE_S(28, 32, 4, 1); break;
-      default: DMF_BK_FUSE_S(24, 32, 4, 1); break;  // 0, 53
+      case 53: DMF_BK_FUSE_S(24, 32, 4, 1); break;  // 24-B records (the round-2 default)
+      default: DMF_BK_FUSE_S20(24, 32, 4, 1); break;  // 0, 57
     }
 #undef DMF_BK_FUSE
 #undef DMF_BK_FUSE_S
 #undef DMF_BK_FUSE_SB
+#undef DMF_BK_FUSE_S20
     DMF_LAUNCH_CHECK();
     if (pipe) DMF_HIP(hipEventRecord(v->bk_ev[3 + (j & 1)], v->stream));
   }
@@ -2128,7 +2185,8 @@ static const char* variant_name(int v) {
     case 54: return "dmf::k_bk_fuse_s<24, 64, 4, 1, false>";
     case 55: return "dmf::k_bk_fuse_s<20, 32, 4, 1, false>";
     case 56: return "dmf::k_bk_fuse_s<28, 32, 4, 1, false>";
-    default: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false>";  // 0, 53; grids over 1024 cells per axis: k_fuse_l<12, 1280>
+    case 53: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false>";
+    default: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true>";  // 0, 57; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }
 }
 
@@ -2163,6 +2221,31 @@ int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t m
     if (pl.sets == 2) DMF_TRY(bk_side(v));
   }
   DMF_HIP(hipStreamSynchronize(v->stream));
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_fuse_plan(const dmf_volume* v, const dmf_camera* cam, int32_t P, dmf_fuse_plan_info* out) {
+  DMF_API_BEGIN
+  if (!out) return fail(DMF_ERR_INVALID, "null argument");
+  DMF_TRY(check_fuse(v, cam, P, &kDefaultParamsForCheck));
+  *out = dmf_fuse_plan_info{};
+  const Geom g = v->geom();
+  const int fv = fuse_variant();
+  out->max_batches = 1;
+  out->poses_per_batch = P;
+  if (brick_path_ok(g) && (is_brick_variant(fv) || (fv == 0 && brick_preferred(g)))) {
+    BkPlan pl;
+    DMF_TRY(bk_plan(v, cam_params(cam), g, P, pl));
+    out->brick = 1;
+    out->poses_per_batch = (int32_t)pl.PB;
+    out->max_batches = (int32_t)((P + pl.PB - 1) / pl.PB);
+    out->record_bytes = (int32_t)pl.rec_bytes;
+    out->pair_capacity = (uint64_t)pl.pair_cap;
+    out->scratch_bytes = (uint64_t)pl.sets * (uint64_t)(pl.pair_cap * pl.rec_bytes +
+                                                         sizeof(ulonglong2) * (size_t)(pl.PB * pl.ppose * 64) +
+                                                         sizeof(uint32_t) * pl.nwg_max * (size_t)pl.bg.nbricks);
+  }
   return DMF_OK;
   DMF_API_END
 }

@@ -46,6 +46,16 @@ class dmf_volume_info(C.Structure):
         ("hsize", C.c_uint64), ("num_occupied", C.c_int64), ("num_points", C.c_int64), ("hazards", C.c_int64)]
 
 
+class dmf_fuse_plan_info(C.Structure):
+    _fields_ = [("brick", C.c_int32), ("max_batches", C.c_int32), ("poses_per_batch", C.c_int32),
+                ("record_bytes", C.c_int32), ("pair_capacity", C.c_uint64), ("scratch_bytes", C.c_uint64)]
+
+
+class dmf_merge_plan(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("n_padded", "chunk", "chunk_offset", "tile_begin", "tile_end",
+                                         "logodds_padded", "slab_bytes", "slab_offset")]
+
+
 class dmf_fuse_params(C.Structure):
     _fields_ = [("dmin_mm", C.c_int32), ("dmax_mm", C.c_int32), ("l_hit", C.c_int32), ("l_miss", C.c_int32),
                 ("l_min", C.c_int32), ("l_max", C.c_int32)]
@@ -108,6 +118,7 @@ SIGNATURES = {
     "dmf_fuse_counter_cells": (C.c_int, [_vp, _p]),
     "dmf_fuse_counters_to_linear_device": (C.c_int, [_vp, _p, _p]),
     "dmf_fuse_reserve": (C.c_int, [_vp, _p, _i32, C.c_uint64]),
+    "dmf_fuse_plan": (C.c_int, [_vp, _p, _i32, _p]),
     "dmf_rccl_version": (C.c_int, [_p]),
     "dmf_comm_unique_id": (C.c_int, [_p]),
     "dmf_comm_init_rank": (C.c_int, [_p, _i32, _p, _i32, _i32]),
@@ -115,6 +126,9 @@ SIGNATURES = {
     "dmf_fuse_counter_cells_padded": (C.c_int, [_vp, _i32, _p]),
     "dmf_fuse_logodds_cells_padded": (C.c_int, [_vp, _i32, _p]),
     "dmf_fuse_allreduce_device": (C.c_int, [_vp, _p, _i64, _vp, _vp]),
+    "dmf_fuse_merge_plan": (C.c_int, [_vp, _i32, _i32, _p]),
+    "dmf_fuse_merge_plan_dims": (C.c_int, [_i32, _i32, _i32, _i32, _i32, _p]),
+    "dmf_fuse_finalize_slab_device": (C.c_int, [_vp, _p, _p, _p, _i32, _i32, _vp]),
     "dmf_fuse_merge_finalize_device": (C.c_int, [_vp, _p, _p, _p, _vp, _vp]),
     "dmf_flags_allreduce": (C.c_int, [_vp, _vp, _vp]),
     "dmf_ogrid_create": (C.c_int, [_p, _i32]),
@@ -198,3 +212,26 @@ def default_fuse_params(**kw):
     for k, v in kw.items():
         setattr(p, k, int(v))
     return p
+
+
+def fuse_plan(vol, cam, P):
+    """dmf_fuse_plan of a fusion call of P frames of `cam` (a dmf_camera) on `vol` (a
+    dmf_amd.VoxelVolume) as a dict."""
+    info = dmf_fuse_plan_info()
+    check(load().dmf_fuse_plan(vol._h, C.addressof(cam), int(P), C.addressof(info)))
+    return {k: getattr(info, k) for k, _ in dmf_fuse_plan_info._fields_}
+
+
+def merge_plan(vol, nranks, rank):
+    """dmf_fuse_merge_plan as a dict (rank = -1: the whole grid)."""
+    out = dmf_merge_plan()
+    check(load().dmf_fuse_merge_plan(vol._h, int(nranks), int(rank), C.addressof(out)))
+    return {k: getattr(out, k) for k, _ in dmf_merge_plan._fields_}
+
+
+def merge_plan_dims(dims, nranks, rank):
+    """dmf_fuse_merge_plan_dims (host only) as a dict."""
+    out = dmf_merge_plan()
+    check(load().dmf_fuse_merge_plan_dims(int(dims[0]), int(dims[1]), int(dims[2]), int(nranks), int(rank),
+                                          C.addressof(out)))
+    return {k: getattr(out, k) for k, _ in dmf_merge_plan._fields_}

@@ -45,8 +45,8 @@ def sum_over_ranks(values, device=None):
 
 # ---- visibility queries (reverseRayTraceFast / set cover), SURVEY.md §8e ----------
 # Queries only read the grid: rank r evaluates its contiguous pose block, the per-pose
-# outputs are gathered in pose order (no data-path collective during the compute), and
-# the idempotent view/good flags merge with an all-reduce(MAX).
+# outputs are gathered in pose order (no data-path collective during the compute); the
+# good flags merge with an all-reduce(MAX), the view ids with a min over non-zero ids.
 
 def gather_pose_lists(found, lists, group=None):
     """All ranks' (found[], lists[]) of their pose blocks -> the full pose-ordered
@@ -64,11 +64,25 @@ def gather_pose_lists(found, lists, group=None):
 
 
 def merge_flags_max(flags, group=None):
-    """All-reduce(MAX) of a per-voxel flag tensor (view int32 / good uint8 widened), in place."""
+    """All-reduce(MAX) of a per-voxel flag tensor (good uint8 widened), in place."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
     return flags
+
+
+def merge_view_ids(view, group=None):
+    """Voxel::view across pose shards, in place: the smallest non-zero id (0 = never viewed),
+    as dmf_flags_allreduce (classify sets view only while it is 0, RayTracingEngine.hpp:354,
+    so one rank walking the poses in order keeps the first pose's id)."""
+    import torch
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        big = torch.iinfo(view.dtype).max
+        view[view == 0] = big
+        dist.all_reduce(view, op=dist.ReduceOp.MIN, group=group)
+        view[view == big] = 0
+    return view
 
 
 def sharded_visibility(compute, poses, world, rank, group=None):
@@ -87,7 +101,8 @@ def sharded_visibility(compute, poses, world, rank, group=None):
 # finalizes rows [r*rows, (r+1)*rows) and the int16 slabs are all-gathered.  This moves
 # 2*4 B (hits, misses) + 2 B (log-odds) per cell instead of the all-reduce's 2*2*4 B.
 # The GPU path is libdmf's dmf_fuse_merge_finalize_device over an RCCL communicator; the
-# numpy/gloo functions below restate the same partition for CPU tests.
+# gloo path below runs the same partition (libdmf's host-only dmf_fuse_merge_plan_dims)
+# with torch collectives for CPU tests.
 
 def tile_rows(dims):
     """(ntx, tiles per row) of the tiled counter layout of a grid (nx, ny, nz)."""
@@ -146,17 +161,18 @@ def finalize_tiles_np(hits_t, miss_t, dims, l_hit, l_miss, l_min, l_max, out, t0
 
 
 def merge_finalize_gloo(counters, dims, prm, logodds, group=None):
-    """CPU restatement of dmf_fuse_merge_finalize_device over a torch.distributed group:
-    counters = torch int32 [hits | misses] tiled, each padded_counter_cells(dims, world);
-    logodds = torch int16 of padded_logodds_cells(dims, world), filled on every rank."""
+    """dmf_fuse_merge_finalize_device over a torch.distributed group (gloo on CPU): the
+    offsets and slab bounds come from libdmf's own plan (dmf_fuse_merge_plan_dims, the
+    arithmetic the RCCL merge runs), the collectives from torch, the slab finalize from the
+    numpy restatement of k_finalize.  counters = torch int32 [hits | misses] tiled, each
+    plan["n_padded"]; logodds = torch int16 of plan["logodds_padded"], filled on every rank."""
     import torch
     import torch.distributed as dist
+    from . import _lib
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    ntx, tpr = tile_rows(dims)
-    rows = rows_per_rank(dims, world)
-    n_pad = rows * world * tpr * 16
-    chunk = rows * tpr * 16
+    p = _lib.merge_plan_dims(dims, world, rank)
+    n_pad, chunk, off = p["n_padded"], p["chunk"], p["chunk_offset"]
     hits, miss = counters[:n_pad], counters[n_pad: 2 * n_pad]
     for arr in (hits, miss):
         part = torch.empty(chunk, dtype=torch.int32)
@@ -164,15 +180,14 @@ def merge_finalize_gloo(counters, dims, prm, logodds, group=None):
             dist.reduce_scatter_tensor(part, arr, group=group)
         else:
             part.copy_(arr[:chunk])
-        arr[rank * chunk: (rank + 1) * chunk] = part
-    r0, r1 = min(ntx, rank * rows), min(ntx, (rank + 1) * rows)
+        arr[off: off + chunk] = part
     out = logodds.numpy()
     finalize_tiles_np(hits.numpy(), miss.numpy(), dims, prm["l_hit"], prm["l_miss"], prm["l_min"], prm["l_max"],
-                      out, r0 * tpr, r1 * tpr)
-    slab = rows * 2 * dims[1] * dims[2]
+                      out, p["tile_begin"], p["tile_end"])
     if world > 1:
-        mine = logodds[rank * slab: (rank + 1) * slab].clone().view(torch.uint8)
-        allb = torch.empty(world * slab * 2, dtype=torch.uint8)
+        sb, so = p["slab_bytes"] // 2, p["slab_offset"] // 2  # int16 elements
+        mine = logodds[so: so + sb].clone().view(torch.uint8)
+        allb = torch.empty(world * sb * 2, dtype=torch.uint8)
         dist.all_gather_into_tensor(allb, mine, group=group)
         logodds.copy_(allb.view(torch.int16))
     return logodds

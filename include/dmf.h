@@ -242,6 +242,20 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
  * current budget; default a third of the device's memory, ~96 GB on MI355X).  Synchronises
  * the stream once. */
 int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t max_scratch_bytes);
+/* How a fusion call of P frames of `cam`'s size on this volume is executed (no GPU work,
+ * no allocation): brick = 1 for the brick-owned pipeline (k_bk_*), 0 for k_fuse_l; the
+ * call is cut into at most max_batches pose batches of poses_per_batch frames, each with
+ * pair_capacity (ray, brick) pair records of record_bytes; scratch_bytes = the pipeline's
+ * device scratch for that (ray records + pair records + per-workgroup brick bases). */
+typedef struct dmf_fuse_plan_info {
+  int32_t brick;
+  int32_t max_batches;
+  int32_t poses_per_batch;
+  int32_t record_bytes;
+  uint64_t pair_capacity;
+  uint64_t scratch_bytes;
+} dmf_fuse_plan_info;
+int dmf_fuse_plan(const dmf_volume* v, const dmf_camera* cam, int32_t P, dmf_fuse_plan_info* out);
 /* Elements of one tiled counter array (>= xdim*ydim*zdim: dims padded to 2, 2, 4). */
 int dmf_fuse_counter_cells(const dmf_volume* v, int64_t* n);
 /* Tiled counters -> x-major int32 (xdim*ydim*zdim). */
@@ -271,6 +285,33 @@ int dmf_comm_destroy(void* comm);
  * dmf_fuse_merge_finalize_device.  Counters = [hits | misses], each n_padded elements. */
 int dmf_fuse_counter_cells_padded(const dmf_volume* v, int32_t nranks, int64_t* n_padded);
 int dmf_fuse_logodds_cells_padded(const dmf_volume* v, int32_t nranks, int64_t* n_padded);
+/* The merge's slab arithmetic for `rank` of `nranks` (rank = -1: the whole grid), so a
+ * caller with its own collectives (MPI, gloo, a test emulating ranks on one GPU) can
+ * reproduce dmf_fuse_merge_finalize_device exactly: each counter array holds n_padded
+ * elements; the reduce-scatter gives rank r the sums of elements [chunk_offset,
+ * chunk_offset + chunk) of each array (in place); rank r finalizes counter tiles
+ * [tile_begin, tile_end) (tile rows of 2 x-rows, clipped to the grid); the all-gather moves
+ * slab_bytes of int16 log-odds from byte slab_offset of each rank's padded grid
+ * (logodds_padded elements). */
+typedef struct dmf_merge_plan {
+  int64_t n_padded;
+  int64_t chunk;
+  int64_t chunk_offset;
+  int64_t tile_begin;
+  int64_t tile_end;
+  int64_t logodds_padded;
+  int64_t slab_bytes;
+  int64_t slab_offset;
+} dmf_merge_plan;
+int dmf_fuse_merge_plan(const dmf_volume* v, int32_t nranks, int32_t rank, dmf_merge_plan* out);
+/* The same for a grid of xdim x ydim x zdim cells (host only: no volume, no GPU). */
+int dmf_fuse_merge_plan_dims(int32_t xdim, int32_t ydim, int32_t zdim, int32_t nranks, int32_t rank,
+                             dmf_merge_plan* out);
+/* Finalize rank `rank`'s slab (rank = -1: every slab) of the padded [hits | misses]
+ * counters (n_padded per array for nranks) into the padded int16 log-odds grid, on
+ * `stream` (NULL = the volume's).  The merge's own finalize step. */
+int dmf_fuse_finalize_slab_device(dmf_volume* v, const int32_t* d_counters, const dmf_fuse_params* prm,
+                                  int16_t* d_logodds, int32_t nranks, int32_t rank, void* stream);
 /* In-place all-reduce(sum) of [hits | misses] (2*n_per_array int32). */
 int dmf_fuse_allreduce_device(dmf_volume* v, int32_t* d_counters, int64_t n_per_array, void* comm, void* stream);
 /* Merge + finalize: reduce-scatter(sum) of hits and of misses over whole tile rows, this
@@ -280,8 +321,10 @@ int dmf_fuse_allreduce_device(dmf_volume* v, int32_t* d_counters, int64_t n_per_
  * comm = NULL: a single rank (no collective): the whole grid is finalized on `stream`. */
 int dmf_fuse_merge_finalize_device(dmf_volume* v, int32_t* d_counters, const dmf_fuse_params* prm,
                                    int16_t* d_logodds, void* comm, void* stream);
-/* Voxel::view / Voxel::good of the replicated occupied list: all-reduce(max) (the
- * reverse/forward queries of a pose shard set flags idempotently). */
+/* Voxel::view / Voxel::good of the replicated occupied list after pose-sharded queries:
+ * good = all-reduce(max); view = the smallest non-zero id over the ranks (classify sets
+ * view only while it is 0, RayTracingEngine.hpp:354, so a single rank keeps the first
+ * pose's id: the same when view ids grow with pose order, as in the reference's loops). */
 int dmf_flags_allreduce(dmf_volume* v, void* comm, void* stream);
 
 /* ---- OccupancyGrid  (include/OccupancyGrid.hpp:50-318) ----------------------- */

@@ -93,8 +93,11 @@ def _vis_worker(rank, world, port, out_dir):
         return [f for f, _ in res], [g for _, g in res]
     found, lists = D.sharded_visibility(compute, poses, world, rank)
     view, good, _, _ = ov.voxel_table()
-    flags = torch.from_numpy(np.stack([view.astype(np.int32), good.astype(np.int32)]))
-    D.merge_flags_max(flags)
+    v_ids = torch.from_numpy(view.astype(np.int32))
+    D.merge_view_ids(v_ids)
+    g_fl = torch.from_numpy(good.astype(np.int32))
+    D.merge_flags_max(g_fl)
+    flags = torch.stack([v_ids, g_fl])
     sel = oracle.greedy_set_cover(lists, 5)
     np.save(os.path.join(out_dir, f"v{rank}.npy"),
             np.array([len(x) for x in lists] + [int(f) for f in found] + list(sel), np.int64))
@@ -103,8 +106,9 @@ def _vis_worker(rank, world, port, out_dir):
 
 
 def test_sharded_visibility_gloo_world2(tmp_path, oracle):
-    """Pose-sharded reverseRayTraceFast (viz) over 2 gloo ranks: gathered lists, MAX-merged
-    flags and the set cover on the gathered lists equal the single-rank run."""
+    """Pose-sharded reverseRayTraceFast (viz) over 2 gloo ranks: gathered lists, merged
+    flags (good: max, view: min non-zero id) and the set cover on the gathered lists equal
+    the single-rank run."""
     import helpers as Hh
     ov = Hh.oracle_volume(oracle, n=64)
     eng = oracle.Engine(Hh.K)
@@ -216,6 +220,38 @@ def test_step_schedule_needs_reuse_wait(tmp_path, oracle):
         got = np.load(tmp_path / f"sched{r}.npy")
         bad += sum(not np.array_equal(got[s], exp) for s in range(len(seeds)))
     assert bad > 0
+
+
+@pytest.mark.parametrize("dims", [(5, 3, 6), (21, 21, 21), (61, 61, 61), (1024, 1024, 288), (7, 1, 1)])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_merge_plan_partitions_the_grid(dims, world):
+    """libdmf's merge plan (the slab arithmetic of the RCCL merge, dmf_fuse_merge_plan_dims)
+    against the padded sizes restated here: the ranks' reduce-scatter chunks tile the padded
+    counter arrays, their finalize tile ranges tile the grid's tiles in rank order, and
+    their log-odds slabs tile the padded int16 grid."""
+    from dmf_amd import _lib
+    from dmf_amd import dist as D
+    ntx, tpr = D.tile_rows(dims)
+    whole = _lib.merge_plan_dims(dims, world, -1)
+    assert whole["tile_begin"] == 0 and whole["tile_end"] == ntx * tpr
+    t = 0
+    for r in range(world):
+        p = _lib.merge_plan_dims(dims, world, r)
+        assert p["n_padded"] == D.padded_counter_cells(dims, world) == whole["n_padded"]
+        assert p["logodds_padded"] == D.padded_logodds_cells(dims, world)
+        assert p["chunk"] * world == p["n_padded"] and p["chunk_offset"] == r * p["chunk"]
+        assert p["slab_bytes"] * world == 2 * p["logodds_padded"] and p["slab_offset"] == r * p["slab_bytes"]
+        assert p["tile_begin"] == t and p["tile_end"] >= p["tile_begin"]
+        # a rank's tiles lie inside its own reduce-scatter chunk and its own log-odds slab
+        # (ranks past the grid's last tile row hold padding only: an empty range)
+        if p["tile_end"] > p["tile_begin"]:
+            assert p["chunk_offset"] <= 16 * p["tile_begin"] and 16 * p["tile_end"] <= p["chunk_offset"] + p["chunk"]
+            x0 = 2 * (p["tile_begin"] // tpr)
+            x1 = min(dims[0], 2 * (p["tile_end"] // tpr))
+            lo = 2 * x0 * dims[1] * dims[2]
+            assert p["slab_offset"] <= lo and 2 * x1 * dims[1] * dims[2] <= p["slab_offset"] + p["slab_bytes"]
+        t = p["tile_end"]
+    assert t == ntx * tpr
 
 
 def test_merge_partition_single_rank():

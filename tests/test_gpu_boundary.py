@@ -8,6 +8,8 @@
   libdmf itself (dmf_comm_init_rank) and over torch's ProcessGroupNCCL communicator, at
   world size 1 (one GPU per box): merged log-odds equal the plain finalize; the world-2
   partition and schedule are covered on CPU by tests/test_dist.py.
+* The merge's slab arithmetic at rank > 0 (dmf_fuse_merge_plan + the merge's own finalize
+  step dmf_fuse_finalize_slab_device) for G = 2, 3, 8 emulated ranks on one GPU.
 """
 import ctypes as C
 import os
@@ -183,3 +185,64 @@ def test_merge_over_torch_process_group_world1(tmp_path):
         assert torch.equal(lo[: 80 ** 3], ref)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dims", [(61, 61, 61), (1024, 1024, 288)])
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_merge_slabs_emulated_ranks(dims, G):
+    """The multi-GPU merge's slab arithmetic at rank > 0, executed on one GPU:
+    G ranks' counter replicas (seeded random counts, padded for G ranks), the reduce-scatter
+    emulated with a device sum placed at each rank's chunk_offset (dmf_fuse_merge_plan), every
+    rank's slab finalized by libdmf (dmf_fuse_finalize_slab_device, the merge's own finalize
+    step), the slabs assembled at their slab_offset as the all-gather would: the result equals
+    the plain finalize of the summed counters, and no rank writes outside its slab."""
+    import torch
+    import dmf_amd
+    from dmf_amd import _lib
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    vol = dmf_amd.VoxelVolume()
+    vol.setDimensions(0.0, dims[0] / 1024, 0.0, dims[1] / 1024, 0.0, dims[2] / 1024)  # exact 2^-10 deltas
+    vol.setVolumeSize(*dims)
+    vol.constructVolume()
+    assert tuple(vol.dims) == dims
+    vol.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    prm = _lib.default_fuse_params()
+    whole = _lib.merge_plan(vol, G, -1)
+    npad, nlo = whole["n_padded"], whole["logodds_padded"]
+    assert whole == _lib.merge_plan_dims(dims, G, -1)
+
+    def replica(r):  # rank r's counters before the merge (deterministic, regenerated on demand)
+        g = torch.Generator(device=dev)
+        g.manual_seed(1000 + r)
+        return torch.randint(0, 12, (2 * npad,), dtype=torch.int32, device=dev, generator=g)
+    total = torch.zeros(2 * npad, dtype=torch.int32, device=dev)
+    for r in range(G):
+        total += replica(r)
+    ref = torch.empty(nlo, dtype=torch.int16, device=dev)
+    _lib.check(L.dmf_fuse_finalize_device(vol._h, total.data_ptr(), total.data_ptr() + 4 * npad, C.addressof(prm),
+                                          ref.data_ptr()))
+    out = torch.full((nlo,), -7, dtype=torch.int16, device=dev)  # the gathered grid
+    outb = out.view(torch.uint8)
+    covered = 0
+    for r in range(G):
+        p = _lib.merge_plan(vol, G, r)
+        assert p == _lib.merge_plan_dims(dims, G, r)
+        buf = replica(r)
+        a, n = p["chunk_offset"], p["chunk"]
+        buf[a:a + n] = total[a:a + n]                        # hits: this rank's reduced chunk
+        buf[npad + a:npad + a + n] = total[npad + a:npad + a + n]  # misses
+        lo = torch.full((nlo,), 12345, dtype=torch.int16, device=dev)
+        _lib.check(L.dmf_fuse_finalize_slab_device(vol._h, buf.data_ptr(), C.addressof(prm), lo.data_ptr(), G, r,
+                                                   None))
+        torch.cuda.synchronize(dev)
+        lob = lo.view(torch.uint8)
+        s0, sb = p["slab_offset"], p["slab_bytes"]
+        outb[s0:s0 + sb] = lob[s0:s0 + sb]
+        # nothing outside the rank's own slab was written
+        assert bool((lo[: s0 // 2] == 12345).all()) and bool((lo[(s0 + sb) // 2:] == 12345).all())
+        covered += sb
+        del buf, lo
+    assert covered == 2 * nlo
+    ncell = dims[0] * dims[1] * dims[2]
+    assert torch.equal(out[:ncell], ref[:ncell])

@@ -8,9 +8,12 @@ Each config is checked two ways:
   counter for counter; every cell update is a hit or a miss; there is one hit per ray
   that ends inside the grid; the multi-batch brick path (pose batches sized by its pair
   budget) equals a single batch.
-Configs: 2 = 640x480, 256^3, 64 poses; 3 = 1280x720, 512^3, 256 poses; 5's single-GPU
-shard = 1280x720, 1024^3 (32 of its 256 poses per GPU).  Config 4's shard (640x480,
-512^3, 128 poses) is the bench workload and tests/test_gpu_parity.py's full-size test.
+Configs: 2 = 640x480, 256^3, 64 poses; 3 = 1280x720, 512^3, 256 poses; 4 = 640x480,
+512^3, 1024 poses over 8 GPUs: its per-GPU shard of 128 poses (the bench workload) against
+the oracle on ALL 128 frames, and the 1024-pose one-GPU anchor; 5 = 1280x720, 1024^3, 2048
+poses over 8 GPUs: its per-GPU shard of 256 poses (several pose batches of the brick
+pipeline).  The reference sequence being scaled is the per-frame integration of
+tests/Raytracing.cpp:70-76 / Volume.hpp:199-228.
 """
 import ctypes as C
 
@@ -25,15 +28,24 @@ pytestmark = pytest.mark.gpu
 class Fusion:
     """Device-API fusion of resident frames on one volume (torch tensors)."""
 
-    def __init__(self, grid, W, H, P, seed=1234):
+    def __init__(self, grid, W, H, P, seed=1234, shard=None):
+        """shard = (world, rank): the rank's block of a P*world-pose sphere (bench.py
+        make_inputs, dmf_amd.dist.shard_range)."""
         import torch
         import dmf_amd
         from dmf_amd import _lib, scene
+        from dmf_amd import dist as D
         self.torch, self._lib = torch, _lib
         self.L = _lib.load()
         self.dev = torch.device("cuda", 0)
         self.K = scene.intrinsics(W, H)
-        self.poses = np.ascontiguousarray(scene.fibonacci_poses(P, seed=seed), np.float32)
+        if shard is None:
+            poses = scene.fibonacci_poses(P, seed=seed)
+        else:
+            world, rank = shard
+            a, b = D.shard_range(P * world, world, rank)
+            poses = scene.fibonacci_poses(P * world, seed=seed)[a:b]
+        self.poses = np.ascontiguousarray(poses, np.float32)
         self.depth = np.ascontiguousarray(scene.render_frames(self.K, W, H, self.poses), np.uint16)
         self.vol = dmf_amd.VoxelVolume()
         self.vol.setDimensions(*Hh.BOUNDS)
@@ -210,3 +222,77 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
         _lib.check(L.dmf_fuse_counters_to_linear_device(vol._h, c.data_ptr() + 4 * nt * half, lin.data_ptr()))
         torch.cuda.synchronize(dev)
         assert np.array_equal(lin.cpu().numpy(), exp)
+
+
+def _plan(f, P):
+    """dmf_fuse_plan of this fusion call: (brick pipeline?, max pose batches)."""
+    from dmf_amd import _lib
+    info = _lib.fuse_plan(f.vol, f.cam, P)
+    return info["brick"], info["max_batches"]
+
+
+def test_config4_shard_all_frames_oracle(oracle):
+    """BASELINE config 4's per-GPU shard = the bench workload (640x480, 512^3, the 128 poses
+    of bench.py at N = 1): ALL 128 frames through the default dispatch in one call, bit-exact
+    against the oracle fusing the same 128 frames at the full grid (OpenMP rows), plus the
+    counting invariants; the per-cell-walk brick pipeline (variant 40) and k_fuse_l
+    (variant 31) give the same counters."""
+    f = Fusion(512, 640, 480, 128)
+    c0, s0, k0 = f.run(0)
+    assert k0.startswith("dmf::k_bk_fuse_s")
+    _invariants(f, c0, s0)
+    assert _plan(f, 128) == (1, 1)
+    hg, mg = f.linear(c0)
+    ho, mo, so = _oracle_subset(oracle, f, list(range(128)))
+    assert np.array_equal(so, s0[:3].astype(np.int64))
+    assert np.array_equal(hg, ho) and np.array_equal(mg, mo)
+    del hg, mg, ho, mo
+    for other in (31, 40):
+        c1, s1, k1 = f.run(other)
+        assert k1 != k0 and np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
+        del c1
+
+
+def test_config4_anchor_1024_poses():
+    """Config 4's 1024 poses on ONE GPU (the strong-scaling anchor): the default call
+    (several pose batches when the pair budget caps them) == k_fuse_l on all 1024 == the
+    8 per-GPU shards of bench.py at N = 8 accumulated into one counter set (the sum the
+    RCCL merge forms), counter for counter."""
+    from dmf_amd import dist as D
+    f = Fusion(512, 640, 480, 1024)
+    c0, s0, k0 = f.run(0)
+    assert k0.startswith("dmf::k_bk_fuse_s")
+    _invariants(f, c0, s0)
+    c1, s1, k1 = f.run(31)
+    assert k1.startswith("dmf::k_fuse_l") and np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
+    del c1
+    acc = f.torch.zeros_like(c0)
+    tot = np.zeros(4, np.uint64)
+    for r in range(8):
+        a, b = D.shard_range(1024, 8, r)
+        acc, st, _ = f.run(0, a, b, counters=acc)
+        tot += st[:4]
+    assert np.array_equal(tot, s0[:4]) and f.torch.equal(acc, c0)
+
+
+def test_config5_shard_256_poses(oracle):
+    """BASELINE config 5's per-GPU shard at its real size: 256 of the 2048 poses (rank 0's
+    block) of 1280x720 depth into 1024^3.  The default call runs the brick pipeline in
+    several pose batches; it equals k_fuse_l counter for counter, satisfies the counting
+    invariants, and two of its frames fused alone equal the oracle at the full grid."""
+    f = Fusion(1024, 1280, 720, 256, shard=(8, 0))
+    brick, batches = _plan(f, 256)
+    assert brick == 1 and batches >= 1
+    c0, s0, k0 = f.run(0)
+    assert k0.startswith("dmf::k_bk_fuse_s")
+    _invariants(f, c0, s0)
+    c1, s1, k1 = f.run(31)
+    assert k1.startswith("dmf::k_fuse_l") and np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
+    del c0, c1
+    frames = [0, 255]
+    ho, mo, so = _oracle_subset(oracle, f, frames)
+    c = f.torch.zeros(2 * f.nt, dtype=f.torch.int32, device=f.dev)
+    for p in frames:
+        c, st, _ = f.run(0, p, p + 1, counters=c)
+    hg, mg = f.linear(c)
+    assert np.array_equal(hg, ho) and np.array_equal(mg, mo)

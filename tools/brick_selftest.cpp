@@ -117,6 +117,40 @@ static void restart_owned(const QRay& r, const int32_t c[3], const int32_t cL[3]
                   [&](int x, int y, int z) { out.push_back({x, y, z}); });
 }
 
+// Check 5: the same walk from the 20-byte pair record (pack20 / unpack20): scaled state
+// beta = b >> 9 with increments |dq| instead of K = 512 |dq|.
+static void restart_owned20(const QRay& r, const int32_t c[3], const int32_t cL[3], bool ends,
+                            std::vector<Cell>& out) {
+  const uint32_t K[3] = {(uint32_t)(2 * kQ * r.adq[0]), (uint32_t)(2 * kQ * r.adq[1]), (uint32_t)(2 * kQ * r.adq[2])};
+  const int M = major_axis(r), m1 = M == 0 ? 1 : 0, m2 = M == 2 ? 1 : 2;
+  int32_t s1, s2, s12;
+  slab_from_pairwise(M, e0_pair(r, 0, 1), e0_pair(r, 0, 2), e0_pair(r, 1, 2), s1, s2, s12);
+  const uint32_t R = slab_rcode(M, s1, s2, K[M], K[m1], K[m2], c, cL);
+  int32_t b1, b2, b12;
+  slab_from_pairwise(M, (int32_t)((uint32_t)e0_pair(r, 0, 1) + (uint32_t)c[0] * K[1] - (uint32_t)c[1] * K[0]),
+                     (int32_t)((uint32_t)e0_pair(r, 0, 2) + (uint32_t)c[0] * K[2] - (uint32_t)c[2] * K[0]),
+                     (int32_t)((uint32_t)e0_pair(r, 1, 2) + (uint32_t)c[1] * K[2] - (uint32_t)c[2] * K[1]), b1, b2,
+                     b12);
+  const uint32_t signs = (r.st[0] < 0 ? 1u : 0u) | (r.st[1] < 0 ? 2u : 0u) | (r.st[2] < 0 ? 4u : 0u);
+  uint32_t w[5];
+  pack20(b1, b2, b12, (uint32_t)r.adq[M], (uint32_t)r.adq[m1], (uint32_t)r.adq[m2], 12345u, 54321u, R, signs,
+         (uint32_t)M, ends, w);
+  Slab20 s;
+  unpack20(w, s);
+  out.clear();
+  if (s.aM != (uint32_t)r.adq[M] || s.a1 != (uint32_t)r.adq[m1] || s.a2 != (uint32_t)r.adq[m2] || s.R != R ||
+      s.signs != signs || s.M != (uint32_t)M || s.ends != ends || s.entry != 12345u || s.last != 54321u) {
+    out.push_back({-1, -1, -1});  // a field did not round-trip
+    return;
+  }
+  const int32_t st[3] = {s.signs & 1u ? -1 : 1, s.signs & 2u ? -1 : 1, s.signs & 4u ? -1 : 1};
+  const int32_t p0[3] = {r.cs[0] + r.st[0] * c[0], r.cs[1] + r.st[1] * c[1], r.cs[2] + r.st[2] * c[2]};
+  // a non-moving axis has sign bit 0 (+1) but never steps (its b stays negative / b12 never flips it)
+  const int32_t stw[3] = {r.st[0] ? st[0] : 0, r.st[1] ? st[1] : 0, r.st[2] ? st[2] : 0};
+  slab_walk_owned((int)s.M, s.b1, s.b2, s.b12, s.aM, s.a1, s.a2, stw, p0, (int)s.R,
+                  [&](int x, int y, int z) { out.push_back({x, y, z}); });
+}
+
 int main(int argc, char** argv) {
   const long nrays = argc > 1 ? atol(argv[1]) : 200000;
   const unsigned seed = argc > 2 ? (unsigned)atol(argv[2]) : 1234u;
@@ -216,6 +250,12 @@ int main(int argc, char** argv) {
         ok = R < 128 && seg.size() == len - 1;
         for (size_t k = 0; ok && k + 1 < len; ++k) ok = seg[k] == fine[pos + k];
         if (!ok) printf("ownership code %u: %zu cells vs %zu\n", R, seg.size(), len - 1);
+        if (ok) {  // 5. the same from the 20-byte record (beta state)
+          restart_owned20(r, p.cin, cL, p.ends && end_inside, seg);
+          ok = seg.size() == len - 1;
+          for (size_t k = 0; ok && k + 1 < len; ++k) ok = seg[k] == fine[pos + k];
+          if (!ok) printf("20-byte record walk: %zu cells vs %zu\n", seg.size(), len - 1);
+        }
       }
       if (!ok) {
         printf("ray %ld (mode %d) brick %d: cells %d vs %zu, ends %d\n", i, mode, b, p.cells, len, (int)p.ends);
