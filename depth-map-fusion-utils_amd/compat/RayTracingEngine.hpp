@@ -3,6 +3,8 @@
 // MI355X through include/dmf.h.  Cheap to copy (holds only the camera), as the
 // reference's callers pass it by value (Algorithms.hpp:364, tests/SetCover.cpp:218).
 #pragma once
+#include <cstdint>
+#include <stdexcept>
 #include <utility>
 #include <vector>
 
@@ -61,6 +63,49 @@ class RayTracingEngine {
     }
     return res;
   }
+  // Extension (BASELINE.json north_star; no reference counterpart): 3D-DDA
+  // log-odds fusion of P depth frames -- the per-frame back-project + integrate loop of
+  // tests/Raytracing.cpp:70-76 / Volume.hpp:199-228 as one GPU call.  depth: P frames of
+  // cam_ height x width uint16 millimetres (row-major), poses: the frames' camera -> world
+  // transforms; hit / miss counts accumulate into `acc` (x-major over the volume's grid,
+  // sized on first use).  dmf_fuse_depth in include/dmf.h.
+  struct FusionCounts {
+    std::vector<int32_t> hits, misses;  // per voxel, x-major (the reference's voxel order)
+    int64_t updates = 0, rays = 0, hit_rays = 0;
+  };
+  FusionCounts& fuseDepth(VoxelVolume& volume, const std::vector<uint16_t>& depth,
+                          const std::vector<Eigen::Affine3f>& poses, FusionCounts& acc,
+                          const dmf_fuse_params* params = nullptr) {
+    const size_t P = poses.size(), HW = (size_t)cam_.getHeight() * (size_t)cam_.getWidth();
+    if (depth.size() != P * HW) throw std::invalid_argument("fuseDepth: depth must hold P frames of height x width");
+    const size_t n = (size_t)volume.xdim_ * volume.ydim_ * volume.zdim_;
+    if (acc.hits.size() != n) acc.hits.assign(n, 0);
+    if (acc.misses.size() != n) acc.misses.assign(n, 0);
+    std::vector<float> p(12 * P);
+    for (size_t i = 0; i < P; ++i) dmf_compat::pose12(poses[i], &p[12 * i]);
+    dmf_fuse_params prm;
+    dmf_fuse_params_default(&prm);
+    if (params) prm = *params;
+    const dmf_camera c = cam_.abi();
+    int64_t st[3] = {0, 0, 0};
+    dmf_check(dmf_fuse_depth(volume.handle(), &c, depth.data(), p.data(), (int32_t)P, &prm, acc.hits.data(),
+                             acc.misses.data(), st));
+    acc.updates += st[0];
+    acc.rays += st[1];
+    acc.hit_rays += st[2];
+    return acc;
+  }
+  // The clamped int16 log-odds grid of fused counts (x-major): clamp(hits * l_hit + misses *
+  // l_miss, l_min, l_max) milli-logit (dmf_fuse_finalize).
+  std::vector<int16_t> logOdds(VoxelVolume& volume, const FusionCounts& acc, const dmf_fuse_params* params = nullptr) {
+    dmf_fuse_params prm;
+    dmf_fuse_params_default(&prm);
+    if (params) prm = *params;
+    std::vector<int16_t> out(acc.hits.size());
+    dmf_check(dmf_fuse_finalize(volume.handle(), acc.hits.data(), acc.misses.data(), &prm, out.data()));
+    return out;
+  }
+
   // RayTracingEngine.hpp:229-264
   int rayTraceAndGetMinimum(VoxelVolume& volume, Eigen::Affine3f& T, int zdelta = 1, bool sparse = true) {
     float p[12];

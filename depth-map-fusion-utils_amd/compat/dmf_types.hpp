@@ -6,7 +6,8 @@
 // Arithmetic follows Eigen 3.3 for fixed-size 3-vectors: a 3-term sum is a0 + (a1 + a2)
 // (redux_novec_unroller), Transform * Vector = t + linear * p, Affine inverse by 3x3
 // cofactors.  Define DMF_COMPAT_REAL_EIGEN / DMF_COMPAT_REAL_PCL to use
-// the real libraries' types instead (the engine only needs the 3x4 pose floats).
+// the real libraries' types instead (the engine only needs the 3x4 pose floats); the
+// third-party shims live in compat/shims/ and go on the include path only without them.
 #pragma once
 #include <cmath>
 #include <cstdint>
@@ -213,14 +214,23 @@ inline void pose12(const T& t, float* out) {
 
 }  // namespace dmf_compat
 
-#ifndef DMF_COMPAT_REAL_EIGEN
+// The vocabulary's source: the real Eigen / PCL when the caller defines
+// DMF_COMPAT_REAL_EIGEN / DMF_COMPAT_REAL_PCL (their headers first on the include path, and
+// compat/shims NOT on it: INTEGRATION.md §2), else the lite types above (the shims in
+// compat/shims/ forward <Eigen/Dense>, <pcl/point_types.h>, ... here).
+#ifdef DMF_COMPAT_REAL_EIGEN
+#include <Eigen/Dense>
+#else
 namespace Eigen {
 using Affine3f = dmf_compat::Affine3f;
 using Vector3f = dmf_compat::Vector3f;
 }  // namespace Eigen
 #endif
 
-#ifndef DMF_COMPAT_REAL_PCL
+#ifdef DMF_COMPAT_REAL_PCL
+#include <pcl/point_cloud.h>
+#include <pcl/point_types.h>
+#else
 namespace pcl {
 using PointXYZ = dmf_compat::PointXYZ;
 using PointXYZRGB = dmf_compat::PointXYZRGB;

@@ -8,7 +8,10 @@
 //     of positionCameras(downsample(cloud)) (Algorithms/PCL, out of scope);
 //   - instead of the GUI (addVolumeWithVoxelsClassified + spinViewer) the classified
 //     voxels are printed.
-// usage: raytracing_headless cloud.bin poses.txt
+//   - (extension, BASELINE.json north_star) with depth.bin: the first P poses' 640x480
+//     uint16 depth frames fused by RayTracingEngine::fuseDepth (3D-DDA log-odds), the
+//     counts and log-odds written to out.bin (int32 hits | int32 misses | int16 log-odds).
+// usage: raytracing_headless cloud.bin poses.txt [depth.bin P out.bin]
 #include <algorithm>
 #include <cstdio>
 #include <fstream>
@@ -133,5 +136,27 @@ int main(int argc, char** argv) {
     cout << " " << PathPlanning::willCollide(volume, a, b);
   }
   cout << "\n";
+  if (argc >= 6) {  // fusion of P depth frames into the same volume's grid
+    const int P = stoi(argv[4]);
+    vector<uint16_t> depth((size_t)P * 480 * 640);
+    ifstream f(argv[3], ios::binary);
+    if (!f.read(reinterpret_cast<char*>(depth.data()), (streamsize)(depth.size() * sizeof(uint16_t)))) {
+      cerr << "short depth file\n";
+      return 3;
+    }
+    vector<Eigen::Affine3f> fposes(camera_locations.begin(), camera_locations.begin() + P);
+    dmf_fuse_params prm;
+    dmf_fuse_params_default(&prm);
+    prm.dmin_mm = 200;
+    prm.dmax_mm = 1000;
+    RayTracingEngine::FusionCounts acc;
+    engine.fuseDepth(volume, depth, fposes, acc, &prm);
+    const vector<int16_t> lo = engine.logOdds(volume, acc, &prm);
+    cout << "fusion " << acc.updates << " " << acc.rays << " " << acc.hit_rays << "\n";
+    ofstream o(argv[5], ios::binary);
+    o.write(reinterpret_cast<const char*>(acc.hits.data()), (streamsize)(acc.hits.size() * sizeof(int32_t)));
+    o.write(reinterpret_cast<const char*>(acc.misses.data()), (streamsize)(acc.misses.size() * sizeof(int32_t)));
+    o.write(reinterpret_cast<const char*>(lo.data()), (streamsize)(lo.size() * sizeof(int16_t)));
+  }
   return 0;
 }

@@ -5,7 +5,7 @@
 #include <cfloat>
 #include <cmath>
 
-#include "../../dmf_types.hpp"
+#include "../../../dmf_types.hpp"
 
 namespace pcl {
 template <typename PointT>

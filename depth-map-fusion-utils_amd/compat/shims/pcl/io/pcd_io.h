@@ -12,7 +12,7 @@
 #include <string>
 #include <vector>
 
-#include "../../dmf_types.hpp"
+#include "../../../dmf_types.hpp"
 
 namespace pcl {
 namespace io {

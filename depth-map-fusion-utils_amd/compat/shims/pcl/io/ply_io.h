@@ -3,7 +3,7 @@
 #pragma once
 #include <string>
 
-#include "../../dmf_types.hpp"
+#include "../../../dmf_types.hpp"
 
 namespace pcl {
 struct PLYReader {

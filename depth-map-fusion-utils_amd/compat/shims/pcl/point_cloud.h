@@ -1,3 +1,3 @@
 // pcl/point_cloud.h for the drop-in build: PointCloud<T> of dmf_types.hpp.
 #pragma once
-#include "../dmf_types.hpp"
+#include "../../dmf_types.hpp"

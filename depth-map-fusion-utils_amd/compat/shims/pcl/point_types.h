@@ -1,3 +1,3 @@
 // pcl/point_types.h for the drop-in build: point types of dmf_types.hpp.
 #pragma once
-#include "../dmf_types.hpp"
+#include "../../dmf_types.hpp"

@@ -5,7 +5,7 @@
 #include <memory>
 #include <string>
 
-#include "../../dmf_types.hpp"
+#include "../../../dmf_types.hpp"
 
 #define PCL_ERROR(...) std::fprintf(stderr, __VA_ARGS__)
 

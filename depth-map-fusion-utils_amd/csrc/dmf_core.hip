@@ -734,9 +734,9 @@ int dmf_volume_create(dmf_volume** out, int32_t device) {
   auto* v = new dmf_volume();
   v->device = device;
   v->dstar = angle_threshold();
-  // brick-fusion pair budget: a third of the device's HBM (~96 GB of MI355X's 288 GB), at
-  // least 8 GiB -- the lists are sized by a geometric bound several times the pairs a scene
-  // makes, and every pose batch the budget forces costs its own passes and counter flushes
+  // brick-fusion scratch budget: a third of the device's HBM (~96 GB of MI355X's 288 GB), at
+  // least 8 GiB -- every pose batch a smaller pair capacity forces costs its own passes and
+  // counter flushes (the device cuts the batches by the pairs a call really makes)
   v->bk_budget = std::max<uint64_t>(8ull << 30, (uint64_t)prop.totalGlobalMem / 3);
   *out = v;
   return DMF_OK;
@@ -751,9 +751,6 @@ int dmf_volume_destroy(dmf_volume* v) {
   (void)hipDeviceSynchronize();
   free_state(v);
   if (v->switch_ev) (void)hipEventDestroy(v->switch_ev);
-  for (hipEvent_t e : v->bk_ev)
-    if (e) (void)hipEventDestroy(e);
-  if (v->bk_side) (void)hipStreamDestroy(v->bk_side);
   delete v;
   return DMF_OK;
   DMF_API_END

@@ -779,7 +779,6 @@ constexpr int kBkThreads = 1024;
 // 1024 lanes when it is large (over 8192 bricks: one workgroup per CU by LDS)
 constexpr int kBkPassThreads = 256, kBkPassThreadsBig = 1024, kBkBigHist = 8192;
 constexpr int kBkScanMax = 32768;  // bricks the scan holds in LDS (the brick path: <= 1024 cells per axis)
-constexpr int kBkPipeDefault = 1;  // pipelined pose batches per call (DMF_BK_PIPE; 1 = off)
 constexpr uint32_t kBkPartMax = 65535;  // pairs per part: 16-bit miss / hit fields never carry
 // LDS box of phase F: cell (x, y, z) of the brick at word x*kSx + y*kSy + z.  The skew
 // (kSy = 33, kSx = 32*33 + 1) puts the cell in bank (x + y + z) mod 32 instead of z alone,
@@ -850,34 +849,40 @@ __device__ inline uint32_t hist_take_agg(uint32_t* hist, int b) {
   return slot;
 }
 
-// Pass A.  Workgroup = 4 waves over a span of 8x8 packets; ray index = packet * 64 + lane.
+// Pass A.  Workgroup = 4 (or 16) waves over a span of 8x8 packets of ONE pose (wg_pose
+// workgroups per pose, the last one of a pose shorter); ray index = packet * 64 + lane.
+// Counts are kept per (pose, brick): pose_cnt[p][b] (the workgroup's base inside that
+// count is wg_base[wg][b]) and per pose: pose_pairs[p], so that the device can cut the
+// call into pose batches by the pairs they really make (k_bk_batches) and any batch's
+// per-brick lists can be laid out (k_bk_batch_counts) without re-running this pass.
 __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam, const uint16_t* __restrict__ depth,
                                                         const PoseX* __restrict__ poses, int dmin, int dmax,
-                                                        int packets_x, int packets_pose, int64_t npackets, int span,
+                                                        int packets_x, int packets_pose, int wg_pose, int span,
                                                         BkGeom bg, ulonglong2* __restrict__ rays,
-                                                        uint32_t* __restrict__ brick_count,
+                                                        uint32_t* __restrict__ pose_cnt,
                                                         uint32_t* __restrict__ wg_base,
+                                                        unsigned long long* __restrict__ pose_pairs,
                                                         unsigned long long* __restrict__ stats) {
   extern __shared__ uint32_t hist[];
   stats = stat_slot(stats);
   for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const int64_t pk0 = (int64_t)blockIdx.x * span, pk1 = min(npackets, pk0 + span);
+  const int pw = (int)(blockIdx.x / (unsigned)wg_pose);
+  const int q0 = (int)(blockIdx.x - (unsigned)pw * (unsigned)wg_pose) * span;
+  const int64_t pk0 = (int64_t)pw * packets_pose + q0, pk1 = (int64_t)pw * packets_pose + min(packets_pose, q0 + span);
   unsigned long long upd = 0, nvalid = 0, nhit = 0;
   // (loading the next packet's depth one packet ahead measured slower: 0.79 -> 0.84 ms)
-  int pcur = -1;  // pose of the cached grid origin (a wave's packets rarely change pose)
-  double go[3] = {0.0, 0.0, 0.0};
+  double go[3];
+  {
+    const float O[3] = {poses[pw].f[3], poses[pw].f[7], poses[pw].f[11]};
+    grid_origin(g, O, go);
+  }
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
-    const int p = (int)(pk / packets_pose);
+    const int p = pw;
     const int q = (int)(pk - (int64_t)p * packets_pose);
     const int r = (q / packets_x) * 8 + (l >> 3), c = (q % packets_x) * 8 + (l & 7);
     const int d = pixel_depth(cam, depth, p, r, c);
-    if (p != pcur) {
-      const float O[3] = {poses[p].f[3], poses[p].f[7], poses[p].f[11]};
-      grid_origin(g, O, go);
-      pcur = p;
-    }
     int64_t qs[3], qe[3];
     bool inside, valid;
     ulonglong2 rec;
@@ -898,11 +903,84 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
     rays[pk * 64 + l] = rec;
   }
   __syncthreads();
+  uint32_t* const pc = pose_cnt + (size_t)pw * bg.nbricks;
+  unsigned long long mine = 0;
   for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) {
     const uint32_t n = hist[i];
-    if (n) wg_base[(size_t)blockIdx.x * bg.nbricks + i] = atomicAdd(&brick_count[i], n);
+    if (n) {
+      wg_base[(size_t)blockIdx.x * bg.nbricks + i] = atomicAdd(&pc[i], n);
+      mine += n;
+    }
   }
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o, 64);
+  if (l == 0 && mine) atomicAdd(&pose_pairs[pw], mine);
   if (stats) wave_stats(stats, upd, nvalid, nhit);
+}
+
+// Pose batches of a call by the pairs pass A counted (one workgroup): greedy over the poses
+// in order, a batch closes before a pose that would take it past `cap` pairs or
+// `max_poses` poses (every pose alone fits: cap >= one pose's geometric bound, bk_plan).
+// bt[0] = batches J, bt[1 + j] = first pose of batch j, bt[1 + J] = P.
+__global__ __launch_bounds__(1024) void k_bk_batches(int P, const unsigned long long* __restrict__ pose_pairs,
+                                                     unsigned long long cap, int max_poses,
+                                                     uint32_t* __restrict__ bt) {
+  constexpr int kChunk = 4096;  // pose counts staged in LDS per round (32 KiB)
+  __shared__ unsigned long long spp[kChunk];
+  uint32_t J = 0;
+  unsigned long long sum = 0;
+  int n = 0;
+  for (int c0 = 0; c0 < P; c0 += kChunk) {
+    const int c1 = min(P, c0 + kChunk);
+    __syncthreads();
+    for (int i = c0 + (int)threadIdx.x; i < c1; i += blockDim.x) spp[i - c0] = pose_pairs[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int p = c0; p < c1; ++p) {
+        const unsigned long long c = spp[p - c0];
+        if (n == 0 || sum + c > cap || n >= max_poses) {
+          bt[1 + J] = (uint32_t)p;
+          ++J;
+          sum = 0;
+          n = 0;
+        }
+        sum += c;
+        ++n;
+      }
+    }
+  }
+  if (threadIdx.x == 0) {
+    bt[1 + J] = (uint32_t)P;
+    bt[0] = J;
+  }
+}
+
+// Brick lists of batch j (grid over bricks): cnt[b] = the batch's pairs in brick b, and
+// pose_base[p][b] = pairs of the batch's earlier poses in brick b (pass B places pose p's
+// pairs of brick b at off[b] + pose_base[p][b] + wg_base[wg][b] + slot).  Batches past
+// bt[0] leave everything untouched (k_bk_scan empties them).
+__global__ __launch_bounds__(256) void k_bk_batch_counts(int nbricks, int j, const uint32_t* __restrict__ bt,
+                                                         const uint32_t* __restrict__ pose_cnt,
+                                                         uint32_t* __restrict__ pose_base,
+                                                         uint32_t* __restrict__ cnt) {
+  const int b = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (b >= nbricks || (uint32_t)j >= bt[0]) return;
+  const int p0 = (int)bt[1 + j], p1 = (int)bt[2 + j];
+  uint32_t acc = 0;
+  int p = p0;
+  for (; p + 4 <= p1; p += 4) {  // four independent loads in flight
+    const uint32_t c0 = pose_cnt[(size_t)p * nbricks + b], c1 = pose_cnt[(size_t)(p + 1) * nbricks + b],
+                   c2 = pose_cnt[(size_t)(p + 2) * nbricks + b], c3 = pose_cnt[(size_t)(p + 3) * nbricks + b];
+    pose_base[(size_t)p * nbricks + b] = acc;
+    pose_base[(size_t)(p + 1) * nbricks + b] = acc + c0;
+    pose_base[(size_t)(p + 2) * nbricks + b] = acc + c0 + c1;
+    pose_base[(size_t)(p + 3) * nbricks + b] = acc + c0 + c1 + c2;
+    acc += c0 + c1 + c2 + c3;
+  }
+  for (; p < p1; ++p) {
+    pose_base[(size_t)p * nbricks + b] = acc;
+    acc += pose_cnt[(size_t)p * nbricks + b];
+  }
+  cnt[b] = acc;
 }
 
 // Scan of the brick counts (one workgroup): list offsets, write cursors, and the part
@@ -916,7 +994,12 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
                                                   uint32_t* __restrict__ off,
                                                   uint32_t* __restrict__ part_pref,
                                                   unsigned long long* __restrict__ ctl,
-                                                  uint2* __restrict__ order, uint32_t part_max) {
+                                                  uint2* __restrict__ order, uint32_t part_max,
+                                                  const uint32_t* __restrict__ bt, int j) {
+  if ((uint32_t)j >= bt[0]) {  // a batch the call does not need: no pairs, no parts
+    if (threadIdx.x == 0) ctl[0] = ctl[1] = 0;
+    return;
+  }
   __shared__ unsigned long long s_pairs[1024];
   __shared__ uint32_t s_parts[1024];
   __shared__ uint32_t s_cls[64];
@@ -1019,22 +1102,30 @@ __device__ inline uint32_t bk_e30(int32_t e) {
 // R20 (SLAB only; the default): the 20-byte record of dmf_brick.hpp pack20 (beta state,
 // pa = words 0-3, pb = word 4 as uint32) instead of the 24-byte one.
 template <bool SLAB, bool AGG = true, bool R20 = false>
-__global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pairs(int64_t npackets, int span, BkGeom bg,
-                                                         const ulonglong2* __restrict__ rays,
+__global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pairs(int packets_pose, int wg_pose, int span,
+                                                         BkGeom bg, const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
-                                                         const uint32_t* __restrict__ wg_base, uint4* __restrict__ pa,
-                                                         void* __restrict__ pbv) {
+                                                         const uint32_t* __restrict__ pose_base,
+                                                         const uint32_t* __restrict__ wg_base,
+                                                         const uint32_t* __restrict__ bt, int j,
+                                                         uint4* __restrict__ pa, void* __restrict__ pbv) {
   static_assert(SLAB || !R20, "the 20-byte record carries the slab state");
   uint2* const pb = (uint2*)pbv;
   uint32_t* const pw = (uint32_t*)pbv;
   extern __shared__ uint32_t hist[];
-  // this workgroup's range in brick i starts at off[i] + wg_base[wg][i] (pass A); entries
-  // of bricks pass A did not count for this workgroup are never used
+  // the workgroups of pass A (one pose each); only those of batch j's poses run
+  const int pz = (int)(blockIdx.x / (unsigned)wg_pose);
+  if ((uint32_t)j >= bt[0] || (uint32_t)pz < bt[1 + j] || (uint32_t)pz >= bt[2 + j]) return;
+  // this workgroup's range in brick i starts at off[i] + pose_base[p][i] + wg_base[wg][i]
+  // (k_bk_scan, k_bk_batch_counts, pass A); entries of bricks pass A did not count for
+  // this workgroup are never used
   const uint32_t* wb = wg_base + (size_t)blockIdx.x * bg.nbricks;
-  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = off[i] + wb[i];
+  const uint32_t* pbz = pose_base + (size_t)pz * bg.nbricks;
+  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = off[i] + pbz[i] + wb[i];
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const int64_t pk0 = (int64_t)blockIdx.x * span, pk1 = min(npackets, pk0 + span);
+  const int q0 = (int)(blockIdx.x - (unsigned)pz * (unsigned)wg_pose) * span;
+  const int64_t pk0 = (int64_t)pz * packets_pose + q0, pk1 = (int64_t)pz * packets_pose + min(packets_pose, q0 + span);
   constexpr uint32_t m5 = bk::kB - 1;
   // the next packet's ray record is loaded one packet ahead: its HBM latency hides behind
   // this packet's coarse walk (B 2.03 -> 1.92 ms) instead of stalling the wave per packet
@@ -1883,33 +1974,36 @@ static int cu_count(int device) {
   return n;
 }
 
-// Pair-buffer budget of the brick pipeline.  The number of (ray, brick) pairs of a batch is
-// known only on the device (pass A), so the host sizes the pair lists by the geometric
-// bound rays x (1 + brick boundaries a grid-crossing ray can pass), and the fusion call
-// never reads anything back: no host synchronisation, no allocation once reserved
-// (dmf_fuse_reserve).  The bound is ~4-8x the pairs of typical scenes, so the per-volume
-// budget caps the poses per batch instead (default a third of the device's HBM, ~96 GB of
-// MI355X's 288 GB: a 512^3 / 640x480 128-frame call and a 1024^3 / 1280x720 32-frame call
-// each fit one batch).
+// Batching of the brick pipeline.  The (ray, brick) pairs a call makes are known only on
+// the device (pass A), and the fusion call never reads anything back (no host sync, no
+// allocation once reserved: dmf_fuse_reserve).  So the host plans by bounds and the device
+// decides: pass A runs once over a super-batch of poses (all P when their ray records fit
+// half the budget), counting pairs per (pose, brick); k_bk_batches cuts the poses into
+// batches by the pairs they really make against the pair capacity (the rest of the budget,
+// at most the geometric bound of the super-batch); the host launches jmax = the batches the
+// geometric bound rays x (1 + brick boundaries) would need, and the launches past the
+// device's batch count exit at once.  Budget: a third of the device's HBM by default
+// (~96 GB of MI355X's 288 GB): the 1024-pose 512^3 anchor and the 256-pose 1024^3 shard
+// each run as one batch.
 
 struct BkPlan {
   BkGeom bg;
   int pkx = 0, pky = 0;
-  int64_t ppose = 0, max_pairs_ray = 0, PB = 0;
-  int ab_threads = 0, span = 0;
-  int sets = 1;  // scratch buffer sets: 2 = pose batches pipelined (A/S/B of batch j+1 beside F of j)
+  int64_t ppose = 0;          // 8x8 packets per pose
+  int64_t max_pairs_ray = 0;  // geometric bound of (ray, brick) pairs per ray
+  int64_t PS = 0;             // poses per super-batch (one pass A over all of them)
+  int64_t PBg = 0;            // poses per batch under the geometric bound (>= 1)
+  int max_poses = 0;          // cap of poses per batch (DMF_BK_BATCH_POSES test hook; else PS)
+  int ab_threads = 0, span = 0, wg_pose = 0;
   uint32_t part_max = kBkPartMax;  // pairs per part of phase F (DMF_BK_PART_MAX: A/B)
   size_t rec_bytes = 24;           // bytes per pair record: 16 (pa) + 8 (pb) or, 20-B records, 16 + 4
-  size_t hist_bytes = 0, nwg_max = 0, pair_cap = 0;
+  size_t hist_bytes = 0;
+  uint64_t pair_cap = 0;      // pair records reserved (shared by the batches of a call)
+  uint64_t per_pose_bytes = 0;
+  int64_t jmax(int64_t ps) const { return (ps + PBg - 1) / PBg; }
+  int64_t max_batches(int64_t P) const { return (P / PS) * jmax(PS) + (P % PS ? jmax(P % PS) : 0); }
+  size_t max_parts() const { return (size_t)bg.nbricks + pair_cap / part_max + 1; }
 };
-
-// Pose batches a call is cut into so that passes A/S/B of one batch run beside phase F of
-// the previous one (DMF_BK_PIPE; 1 = one batch when it fits the budget, no side stream).
-static int bk_pipe_chunks() {
-  const char* e = getenv("DMF_BK_PIPE");
-  const int n = e ? atoi(e) : kBkPipeDefault;
-  return std::max(1, std::min(n, 64));
-}
 
 static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, BkPlan& pl) {
   pl.bg = brick_geom(g);
@@ -1917,23 +2011,10 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   pl.pky = (cp.H + 7) / 8;
   pl.ppose = (int64_t)pl.pkx * pl.pky;
   pl.max_pairs_ray = 1 + (pl.bg.nb[0] - 1) + (pl.bg.nb[1] - 1) + (pl.bg.nb[2] - 1);
-  const int64_t rays_pose = pl.ppose * 64;
-  const int64_t ray_cap = (int64_t)UINT32_MAX / pl.max_pairs_ray;  // pair offsets are 32-bit
   pl.rec_bytes = is_rec20_variant(fuse_variant()) ? 20 : 24;
-  const uint64_t per_pose = (uint64_t)rays_pose * (uint64_t)pl.max_pairs_ray * pl.rec_bytes;
-  const int chunks = bk_pipe_chunks();
-  // two buffer sets share the budget when the batches are pipelined (opt-in: measured
-  // slower, DESIGN.md §5.3 -- A/B beside F slow down 2-5x and F by ~7 %)
-  pl.sets = (P >= 2 && chunks > 1) ? 2 : 1;
-  int64_t PB = std::min<int64_t>(P, ray_cap / rays_pose);
-  PB = std::min<int64_t>(PB, (int64_t)(v->bk_budget / pl.sets / per_pose));
-  PB = std::min<int64_t>(PB, ((int64_t)P + chunks - 1) / chunks);
-  if (const char* e = getenv("DMF_BK_BATCH_POSES")) {  // test hook: cap the poses per batch
-    const int64_t cap = (int64_t)atoll(e);
-    if (cap > 0) PB = std::min<int64_t>(PB, cap);
-  }
-  if (PB < 1) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion pair budget (dmf_fuse_reserve)");
-  pl.PB = PB;
+  const int64_t rays_pose = pl.ppose * 64;
+  const uint64_t one_pose = (uint64_t)rays_pose * (uint64_t)pl.max_pairs_ray;  // pairs of one pose, at most
+  if (one_pose > (uint64_t)UINT32_MAX) return fail(DMF_ERR_RANGE, "one frame exceeds the 32-bit pair offsets");
   pl.ab_threads = pl.bg.nbricks > kBkBigHist ? kBkPassThreadsBig : kBkPassThreads;
   // packets per workgroup of passes A/B (>= 16 per wave; the histogram's zero + flush
   // amortised over >= 64 packets per 1k bricks).  Up to 512 bricks (grids <= 256^3) the
@@ -1943,9 +2024,27 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   if (const char* e = getenv("DMF_BK_SPAN")) pl.span = std::max(4, std::min(atoi(e), 4096));  // A/B
   if (const char* e = getenv("DMF_BK_PART_MAX"))
     pl.part_max = (uint32_t)std::max(1024, std::min(atoi(e), (int)kBkPartMax));
+  pl.wg_pose = (int)((pl.ppose + pl.span - 1) / pl.span);
   pl.hist_bytes = sizeof(uint32_t) * (size_t)pl.bg.nbricks;
-  pl.nwg_max = (size_t)((PB * pl.ppose + pl.span - 1) / pl.span);
-  pl.pair_cap = (size_t)(PB * rays_pose * pl.max_pairs_ray);
+  // per pose: ray records, per-workgroup brick bases, pose counts and bases, pose pairs + batch table
+  pl.per_pose_bytes = (uint64_t)rays_pose * sizeof(ulonglong2) + (uint64_t)pl.wg_pose * pl.hist_bytes +
+                      2 * (uint64_t)pl.hist_bytes + sizeof(unsigned long long) + sizeof(uint32_t);
+  const uint64_t budget = v->bk_budget;
+  pl.PS = std::min<int64_t>(P, (int64_t)(budget / 2 / pl.per_pose_bytes));
+  if (pl.PS < 1) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion budget (dmf_fuse_reserve)");
+  pl.pair_cap = std::min<uint64_t>({(budget - (uint64_t)pl.PS * pl.per_pose_bytes) / pl.rec_bytes,
+                                    (uint64_t)pl.PS * one_pose, (uint64_t)UINT32_MAX});
+  if (pl.pair_cap < one_pose) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion pair budget (dmf_fuse_reserve)");
+  if (const char* e = getenv("DMF_BK_PAIR_CAP")) {  // test hook: a pair capacity below one pose's bound
+    const int64_t c = (int64_t)atoll(e);             // (the caller guarantees it holds any one pose's pairs)
+    if (c > 0) pl.pair_cap = std::min<uint64_t>(pl.pair_cap, (uint64_t)c);
+  }
+  pl.max_poses = (int)pl.PS;
+  if (const char* e = getenv("DMF_BK_BATCH_POSES")) {  // test hook: cap the poses per batch
+    const int64_t c = (int64_t)atoll(e);
+    if (c > 0) pl.max_poses = (int)std::min<int64_t>(pl.PS, c);
+  }
+  pl.PBg = std::max<int64_t>(1, std::min<int64_t>(pl.max_poses, (int64_t)(pl.pair_cap / one_pose)));
   return DMF_OK;
 }
 
@@ -1953,130 +2052,119 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
 static int bk_attributes() {
   static std::atomic<bool> attr_set{false};
   if (!attr_set.load()) {
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(uint32_t) * 32768)));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(uint32_t) * 32768)));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(uint32_t) * 32768)));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(uint32_t) * 32768)));
+    const int lds = (int)(sizeof(uint32_t) * 32768);
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(uint32_t) * 32768)));
+                                lds));
     attr_set.store(true);
   }
   return DMF_OK;
 }
 
-// One scratch set of a plan: ray records, brick counts / offsets / part prefix, queue
-// control words, per-workgroup bases, pair records.
+// The scratch of a plan: ray records, brick counts / offsets / part table / part order,
+// queue control words, per-workgroup and per-pose brick bases, pose pair counts and the
+// batch table, pair records.
 struct BkBufs {
   ulonglong2* rays = nullptr;
   uint32_t *cnt = nullptr, *off = nullptr, *part_pref = nullptr, *wgb = nullptr;
+  uint32_t *pose_cnt = nullptr, *pose_base = nullptr, *bt = nullptr;
+  unsigned long long* pose_pairs = nullptr;
   uint2* order = nullptr;
   unsigned long long* ctl = nullptr;
   uint4* pra = nullptr;
   void* prb = nullptr;  // uint2 per pair (24-B records) or uint32 (20-B records)
 };
 
-// Scratch set `set` of a plan (allocates only when a slot is too small).
-static int bk_scratch(dmf_volume* v, const BkPlan& pl, int set, BkBufs& b) {
-  const int o = set * kScBkSetStride;
-  void *rays, *bricks, *ctl, *wgb, *pra, *prb;
-  DMF_TRY(scratch(v, kScBkRays + o, sizeof(ulonglong2) * (size_t)(pl.PB * pl.ppose * 64), &rays));
-  // cnt | off | part_pref (nbricks + 1) | order (uint2 per part: <= nbricks + pairs / 65535)
-  const size_t max_parts = (size_t)pl.bg.nbricks + pl.pair_cap / pl.part_max + 1;
-  DMF_TRY(scratch(v, kScBkBricks + o, sizeof(uint32_t) * (3 * (size_t)pl.bg.nbricks + 6 + 2 * max_parts), &bricks));
-  DMF_TRY(scratch(v, kScBkCtl + o, sizeof(unsigned long long) * 4, &ctl));
-  // per-workgroup base inside each brick (pass A -> pass B)
-  DMF_TRY(scratch(v, kScBkWgBase + o, sizeof(uint32_t) * pl.nwg_max * (size_t)pl.bg.nbricks, &wgb));
-  DMF_TRY(scratch(v, kScBkPairs + o, sizeof(uint4) * pl.pair_cap, &pra));
-  DMF_TRY(scratch(v, kScBkPairsB + o, (pl.rec_bytes - sizeof(uint4)) * pl.pair_cap, &prb));
+// Allocates only when a slot is too small.
+static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b) {
+  const size_t PS = (size_t)pl.PS, nb = (size_t)pl.bg.nbricks;
+  void *rays, *bricks, *ctl, *wgb, *pra, *prb, *pcnt, *pbase, *batch;
+  DMF_TRY(scratch(v, kScBkRays, sizeof(ulonglong2) * (size_t)(pl.PS * pl.ppose * 64), &rays));
+  // cnt | off | part_pref (nbricks + 1) | order (uint2 per part)
+  DMF_TRY(scratch(v, kScBkBricks, sizeof(uint32_t) * (3 * nb + 6 + 2 * pl.max_parts()), &bricks));
+  DMF_TRY(scratch(v, kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
+  DMF_TRY(scratch(v, kScBkWgBase, pl.hist_bytes * (size_t)pl.wg_pose * PS, &wgb));
+  DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * (size_t)pl.pair_cap, &pra));
+  DMF_TRY(scratch(v, kScBkPairsB, (pl.rec_bytes - sizeof(uint4)) * (size_t)pl.pair_cap, &prb));
+  DMF_TRY(scratch(v, kScBkPoseCnt, pl.hist_bytes * PS, &pcnt));
+  DMF_TRY(scratch(v, kScBkPoseBase, pl.hist_bytes * PS, &pbase));
+  DMF_TRY(scratch(v, kScBkBatch, sizeof(unsigned long long) * PS + sizeof(uint32_t) * (PS + 4), &batch));
   b.rays = (ulonglong2*)rays;
   b.cnt = (uint32_t*)bricks;
-  b.off = b.cnt + pl.bg.nbricks;
-  b.part_pref = b.off + pl.bg.nbricks;  // nbricks + 1
-  b.order = (uint2*)(b.part_pref + pl.bg.nbricks + 4 + (pl.bg.nbricks & 1));  // 8-B aligned
+  b.off = b.cnt + nb;
+  b.part_pref = b.off + nb;  // nbricks + 1
+  b.order = (uint2*)(b.part_pref + nb + 4 + (nb & 1));  // 8-B aligned
   b.wgb = (uint32_t*)wgb;
   b.ctl = (unsigned long long*)ctl;
   b.pra = (uint4*)pra;
   b.prb = prb;
+  b.pose_cnt = (uint32_t*)pcnt;
+  b.pose_base = (uint32_t*)pbase;
+  b.pose_pairs = (unsigned long long*)batch;
+  b.bt = (uint32_t*)(b.pose_pairs + PS);
   return DMF_OK;
 }
 
-// The side stream and events of pipelined batches (created once per volume).
-static int bk_side(dmf_volume* v) {
-  if (!v->bk_side) DMF_HIP(hipStreamCreateWithFlags(&v->bk_side, hipStreamNonBlocking));
-  for (hipEvent_t& e : v->bk_ev)
-    if (!e) DMF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  return DMF_OK;
-}
-
-// Brick-owned fusion of P frames (kernels above), in pose batches sized by bk_plan.  Only
-// enqueues work: pass S leaves the pair and part counts on the device, pass B writes the
-// pairs below the planned bound, phase F reads the part count itself (its persistent
-// workgroups exit when the queue is empty).  With two scratch sets, batch j's passes A/S/B
-// run on the volume's side stream (after the call's earlier work and after F(j-2) has freed
-// the set) while F(j-1) runs on the caller's stream: F occupies 135 KB of LDS and a quarter
-// of the registers per CU, so an A/B workgroup fits beside it (opt-in, DMF_BK_PIPE: the
-// co-resident kernels slow each other more than they hide).  Every side-stream operation is joined back into the caller's stream (F(j) waits for
-// B(j)), so the call keeps plain stream semantics and stays capturable.
+// Brick-owned fusion of P frames (kernels above).  Only enqueues work: per super-batch,
+// pass A over all its poses, the device's batch cut, then per batch launch the brick
+// layout (k_bk_batch_counts, k_bk_scan), pass B and phase F; a launch past the device's
+// batch count exits at once.  Phase F reads its part count itself (its persistent
+// workgroups exit when the queue is empty).
 static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint16_t* d_depth, const PoseX* tab, int P,
                        const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses, unsigned long long* st) {
   BkPlan pl;
   DMF_TRY(bk_plan(v, cp, g, P, pl));
   const BkGeom& bg = pl.bg;
   DMF_TRY(bk_attributes());
-  BkBufs set[2];
-  for (int k = 0; k < pl.sets; ++k) DMF_TRY(bk_scratch(v, pl, k, set[k]));
-  const bool pipe = pl.sets == 2 && P > pl.PB;
-  hipStream_t sa = v->stream;  // stream of passes A, S, B
-  if (pipe) {
-    DMF_TRY(bk_side(v));
-    sa = v->bk_side;
-    DMF_HIP(hipEventRecord(v->bk_ev[0], v->stream));
-    DMF_HIP(hipStreamWaitEvent(sa, v->bk_ev[0], 0));
-  }
+  BkBufs b;
+  DMF_TRY(bk_scratch(v, pl, b));
+  const hipStream_t sa = v->stream;
   const unsigned nf = (unsigned)cu_count(v->device);
   const int fv = fuse_variant();
   const bool lpt_on = [] {  // A/B: DMF_BK_LPT=0 hands the parts out in brick order
     const char* e = getenv("DMF_BK_LPT");
     return !(e && atoi(e) == 0);
   }();
-  int64_t j = 0;
-  for (int64_t p0 = 0; p0 < P; p0 += pl.PB, ++j) {
-    const BkBufs& b = set[pipe ? j & 1 : 0];
-    const uint2* lpt = lpt_on ? b.order : nullptr;
-    const int64_t pb = std::min<int64_t>(pl.PB, P - p0);
-    const int64_t npk = pb * pl.ppose;
-    const unsigned nwg = (unsigned)((npk + pl.span - 1) / pl.span);
-    if (pipe && j >= 2) DMF_HIP(hipStreamWaitEvent(sa, v->bk_ev[3 + (j & 1)], 0));  // F(j-2) is done with the set
-    DMF_HIP(hipMemsetAsync(b.cnt, 0, pl.hist_bytes, sa));
-    DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sa));
+  const uint2* lpt = lpt_on ? b.order : nullptr;
+  for (int64_t s0 = 0; s0 < P; s0 += pl.PS) {
+    const int64_t ps = std::min<int64_t>(pl.PS, P - s0);
+    const unsigned nwg = (unsigned)(ps * pl.wg_pose);
+    DMF_HIP(hipMemsetAsync(b.pose_cnt, 0, pl.hist_bytes * (size_t)ps, sa));
+    DMF_HIP(hipMemsetAsync(b.pose_pairs, 0, sizeof(unsigned long long) * (size_t)ps, sa));
     hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, g, cp,
-                       d_depth + (size_t)p0 * cp.H * cp.W, tab + p0, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
-                       npk, pl.span, bg, b.rays, b.cnt, b.wgb, st);
+                       d_depth + (size_t)s0 * cp.H * cp.W, tab + s0, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
+                       pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.pose_pairs, st);
     DMF_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off, b.part_pref,
-                       b.ctl, b.order, pl.part_max);
+    hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sa, (int)ps, (const unsigned long long*)b.pose_pairs,
+                       (unsigned long long)pl.pair_cap, pl.max_poses, b.bt);
     DMF_LAUNCH_CHECK();
-    if (fv == 48)  // wave-aggregated slot atomics (the previous default)
-      hipLaunchKernelGGL((k_bk_pairs<true, true>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
-                         (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
-    else if (is_rec20_variant(fv))
-      hipLaunchKernelGGL((k_bk_pairs<true, false, true>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span,
-                         bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
-    else if (is_slab_variant(fv))
-      hipLaunchKernelGGL((k_bk_pairs<true, false>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
-                         (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
-    else
-      hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, npk, pl.span, bg,
-                         (const ulonglong2*)b.rays, (const uint32_t*)b.off, (const uint32_t*)b.wgb, b.pra, b.prb);
-    DMF_LAUNCH_CHECK();
-    if (pipe) {
-      DMF_HIP(hipEventRecord(v->bk_ev[1 + (j & 1)], sa));
-      DMF_HIP(hipStreamWaitEvent(v->stream, v->bk_ev[1 + (j & 1)], 0));
-    }
+    v->bk_last_bt = b.bt;
+    const int64_t jm = pl.jmax(ps);
+    for (int64_t j = 0; j < jm; ++j) {
+      DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sa));
+      hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sa, bg.nbricks,
+                         (int)j, (const uint32_t*)b.bt, (const uint32_t*)b.pose_cnt, b.pose_base, b.cnt);
+      DMF_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off, b.part_pref,
+                         b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j);
+      DMF_LAUNCH_CHECK();
+#define DMF_BK_PAIRS(...)                                                                                          \
+  hipLaunchKernelGGL((k_bk_pairs<__VA_ARGS__>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,  \
+                     pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off,                   \
+                     (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j, b.pra, b.prb)
+      if (fv == 48)  // wave-aggregated slot atomics (the previous default)
+        DMF_BK_PAIRS(true, true);
+      else if (is_rec20_variant(fv))
+        DMF_BK_PAIRS(true, false, true);
+      else if (is_slab_variant(fv))
+        DMF_BK_PAIRS(true, false);
+      else
+        DMF_BK_PAIRS(false);
+#undef DMF_BK_PAIRS
+      DMF_LAUNCH_CHECK();
 #define DMF_BK_FUSE(R, S, U, N, C, B)                                                                           \
   hipLaunchKernelGGL((k_bk_fuse<R, S, U, N, C, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,            \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
@@ -2093,32 +2181,32 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,          \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
                      (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st)
-    switch (fv) {
-      case 40: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
-      case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
-      case 42: DMF_BK_FUSE(32, 8, 8, 2, 0, false); break;
-      case 43: DMF_BK_FUSE(16, 8, 8, 1, 256, true); break;
-      case 45: DMF_BK_FUSE_S(24, 8, 4, 1); break;
-      case 46: DMF_BK_FUSE_S(32, 8, 4, 1); break;
-      case 47: DMF_BK_FUSE_S(40, 8, 4, 1); break;
-      case 48: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // with k_bk_pairs<true, true>
-      case 49: DMF_BK_FUSE_S(32, 8, 4, 2); break;
-      case 50: DMF_BK_FUSE_SB(16, 8, 4, 1); break;
-      case 51: DMF_BK_FUSE_SB(32, 8, 4, 2); break;
-      case 44: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // the previous default
-      case 52: DMF_BK_FUSE_S(24, 16, 4, 1); break;  // the default until the ownership-code walk
-      case 54: DMF_BK_FUSE_S(24, 64, 4, 1); break;
-      case 55: DMF_BK_FUSE_S(20, 32, 4, 1); break;
-      case 56: DMF_BK_FUSE_S(28, 32, 4, 1); break;
-      case 53: DMF_BK_FUSE_S(24, 32, 4, 1); break;  // 24-B records (the round-2 default)
-      default: DMF_BK_FUSE_S20(24, 32, 4, 1); break;  // 0, 57
-    }
+      switch (fv) {
+        case 40: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
+        case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
+        case 42: DMF_BK_FUSE(32, 8, 8, 2, 0, false); break;
+        case 43: DMF_BK_FUSE(16, 8, 8, 1, 256, true); break;
+        case 45: DMF_BK_FUSE_S(24, 8, 4, 1); break;
+        case 46: DMF_BK_FUSE_S(32, 8, 4, 1); break;
+        case 47: DMF_BK_FUSE_S(40, 8, 4, 1); break;
+        case 48: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // with k_bk_pairs<true, true>
+        case 49: DMF_BK_FUSE_S(32, 8, 4, 2); break;
+        case 50: DMF_BK_FUSE_SB(16, 8, 4, 1); break;
+        case 51: DMF_BK_FUSE_SB(32, 8, 4, 2); break;
+        case 44: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // the round-1 default
+        case 52: DMF_BK_FUSE_S(24, 16, 4, 1); break;  // the default until the ownership-code walk
+        case 53: DMF_BK_FUSE_S(24, 32, 4, 1); break;  // 24-B records (the round-2 default)
+        case 54: DMF_BK_FUSE_S(24, 64, 4, 1); break;
+        case 55: DMF_BK_FUSE_S(20, 32, 4, 1); break;
+        case 56: DMF_BK_FUSE_S(28, 32, 4, 1); break;
+        default: DMF_BK_FUSE_S20(24, 32, 4, 1); break;  // 0, 57
+      }
 #undef DMF_BK_FUSE
 #undef DMF_BK_FUSE_S
-#undef DMF_BK_FUSE_SB
 #undef DMF_BK_FUSE_S20
-    DMF_LAUNCH_CHECK();
-    if (pipe) DMF_HIP(hipEventRecord(v->bk_ev[3 + (j & 1)], v->stream));
+#undef DMF_BK_FUSE_SB
+      DMF_LAUNCH_CHECK();
+    }
   }
   return DMF_OK;
 }
@@ -2217,8 +2305,7 @@ int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t m
     DMF_TRY(bk_plan(v, cp, g, P, pl));
     DMF_TRY(bk_attributes());
     BkBufs set;
-    for (int k = 0; k < pl.sets; ++k) DMF_TRY(bk_scratch(v, pl, k, set));
-    if (pl.sets == 2) DMF_TRY(bk_side(v));
+    DMF_TRY(bk_scratch(v, pl, set));
   }
   DMF_HIP(hipStreamSynchronize(v->stream));
   return DMF_OK;
@@ -2238,14 +2325,28 @@ int dmf_fuse_plan(const dmf_volume* v, const dmf_camera* cam, int32_t P, dmf_fus
     BkPlan pl;
     DMF_TRY(bk_plan(v, cam_params(cam), g, P, pl));
     out->brick = 1;
-    out->poses_per_batch = (int32_t)pl.PB;
-    out->max_batches = (int32_t)((P + pl.PB - 1) / pl.PB);
+    out->poses_per_batch = (int32_t)pl.PBg;
+    out->max_batches = (int32_t)pl.max_batches(P);
     out->record_bytes = (int32_t)pl.rec_bytes;
     out->pair_capacity = (uint64_t)pl.pair_cap;
-    out->scratch_bytes = (uint64_t)pl.sets * (uint64_t)(pl.pair_cap * pl.rec_bytes +
-                                                         sizeof(ulonglong2) * (size_t)(pl.PB * pl.ppose * 64) +
-                                                         sizeof(uint32_t) * pl.nwg_max * (size_t)pl.bg.nbricks);
+    out->scratch_bytes = pl.pair_cap * pl.rec_bytes + (uint64_t)pl.PS * pl.per_pose_bytes +
+                         sizeof(uint32_t) * (3 * (uint64_t)pl.bg.nbricks + 2 * pl.max_parts());
+    out->super_batch_poses = (int32_t)pl.PS;
   }
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_fuse_batches_used(dmf_volume* v, int32_t* batches) {
+  DMF_API_BEGIN
+  if (!batches) return fail(DMF_ERR_INVALID, "null argument");
+  DMF_TRY(require_constructed(v));
+  *batches = 0;
+  if (!v->bk_last_bt) return DMF_OK;
+  uint32_t J = 0;
+  DMF_HIP(hipMemcpyAsync(&J, v->bk_last_bt, sizeof(J), hipMemcpyDeviceToHost, v->stream));
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  *batches = (int32_t)J;
   return DMF_OK;
   DMF_API_END
 }

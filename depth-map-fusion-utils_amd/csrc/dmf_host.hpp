@@ -50,13 +50,10 @@ int scratch(dmf_volume* v, int k, size_t bytes, void** out);
 enum ScratchSlot {
   kScPoses = 0, kScHost0, kScHost1, kScHost2, kScOut0, kScOut1, kScOut2, kScOut3, kScTmp, kScSort0,
   kScSort1, kScSort2, kScSort3, kScCount, kScStats,
-  // brick-owned fusion (dmf_fuse.hip): two buffer sets of six slots (pipelined pose batches)
-  kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkWgBase, kScBkCtl,
-  kScBkRays2, kScBkPairs2, kScBkPairsB2, kScBkBricks2, kScBkWgBase2, kScBkCtl2,
+  // brick-owned fusion (dmf_fuse.hip)
+  kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkWgBase, kScBkCtl, kScBkPoseCnt, kScBkPoseBase, kScBkBatch,
   kScOgP0, kScOgP1, kScOgFinal, kScOgOcc  // OccupancyGrid reorganization (dmf_ogrid.hip)
 };
-constexpr int kScBkSetStride = kScBkRays2 - kScBkRays;
-static_assert(kScBkCtl2 - kScBkCtl == kScBkSetStride, "brick scratch sets must be laid out alike");
 
 // Striped statistics: kernels add into slot (block % kStatSlots) of a zeroed buffer
 // of kStatSlots x kStatWidth counters (one hot address per counter serialises at the

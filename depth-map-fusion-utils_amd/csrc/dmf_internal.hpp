@@ -256,12 +256,9 @@ struct dmf_volume {
   int32_t nax[3] = {0, 0, 0};
   uint32_t* d_enum = nullptr;  // occupied enumeration indices, enumeration order
   int64_t nenum = 0, enum_cap = 0, enum_hazards = 0;
-  // brick fusion pair-list budget (dmf_fuse_reserve)
+  // brick fusion scratch budget (dmf_fuse_reserve)
   uint64_t bk_budget = 48ull << 30;  // set from the device's memory by dmf_volume_create
-  // pipelined pose batches: passes A/S/B run on bk_side while phase F of the previous batch
-  // runs on `stream`; events: [0] call start, [1+s] set s written (B done), [3+s] set s free (F done)
-  hipStream_t bk_side = nullptr;
-  hipEvent_t bk_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint32_t* bk_last_bt = nullptr;     // the batch table of the latest brick-pipeline super-batch (diagnostic)
   // scratch arena
   std::vector<std::pair<void*, size_t>> scratch;
 

@@ -48,7 +48,8 @@ class dmf_volume_info(C.Structure):
 
 class dmf_fuse_plan_info(C.Structure):
     _fields_ = [("brick", C.c_int32), ("max_batches", C.c_int32), ("poses_per_batch", C.c_int32),
-                ("record_bytes", C.c_int32), ("pair_capacity", C.c_uint64), ("scratch_bytes", C.c_uint64)]
+                ("record_bytes", C.c_int32), ("pair_capacity", C.c_uint64), ("scratch_bytes", C.c_uint64),
+                ("super_batch_poses", C.c_int32), ("reserved", C.c_int32)]
 
 
 class dmf_merge_plan(C.Structure):
@@ -119,6 +120,7 @@ SIGNATURES = {
     "dmf_fuse_counters_to_linear_device": (C.c_int, [_vp, _p, _p]),
     "dmf_fuse_reserve": (C.c_int, [_vp, _p, _i32, C.c_uint64]),
     "dmf_fuse_plan": (C.c_int, [_vp, _p, _i32, _p]),
+    "dmf_fuse_batches_used": (C.c_int, [_vp, _p]),
     "dmf_rccl_version": (C.c_int, [_p]),
     "dmf_comm_unique_id": (C.c_int, [_p]),
     "dmf_comm_init_rank": (C.c_int, [_p, _i32, _p, _i32, _i32]),
@@ -235,3 +237,10 @@ def merge_plan_dims(dims, nranks, rank):
     check(load().dmf_fuse_merge_plan_dims(int(dims[0]), int(dims[1]), int(dims[2]), int(nranks), int(rank),
                                           C.addressof(out)))
     return {k: getattr(out, k) for k, _ in dmf_merge_plan._fields_}
+
+
+def fuse_batches_used(vol):
+    """dmf_fuse_batches_used: pose batches of the latest brick-pipeline super-batch."""
+    n = C.c_int32()
+    check(load().dmf_fuse_batches_used(vol._h, C.addressof(n)))
+    return n.value

@@ -237,16 +237,18 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
                           int32_t* d_misses, uint64_t* d_stats);
 /* Pre-allocate the fusion scratch for calls of up to P frames of `cam`'s size on this
  * volume, so that dmf_fuse_depth_device then neither allocates nor synchronises (e.g. for
- * hipGraph capture).  The brick pipeline sizes its (ray, brick) pair lists by a geometric
- * bound and splits larger calls into pose batches that fit max_scratch_bytes (0 = keep the
- * current budget; default a third of the device's memory, ~96 GB on MI355X).  Synchronises
- * the stream once. */
+ * hipGraph capture).  The brick pipeline fits its ray records, brick tables and (ray,
+ * brick) pair records into max_scratch_bytes (0 = keep the current budget; default a third
+ * of the device's memory, ~96 GB on MI355X): a call whose pairs exceed the pair capacity
+ * is cut into pose batches on the device (dmf_fuse_plan).  Synchronises the stream once. */
 int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t max_scratch_bytes);
 /* How a fusion call of P frames of `cam`'s size on this volume is executed (no GPU work,
- * no allocation): brick = 1 for the brick-owned pipeline (k_bk_*), 0 for k_fuse_l; the
- * call is cut into at most max_batches pose batches of poses_per_batch frames, each with
- * pair_capacity (ray, brick) pair records of record_bytes; scratch_bytes = the pipeline's
- * device scratch for that (ray records + pair records + per-workgroup brick bases). */
+ * no allocation): brick = 1 for the brick-owned pipeline (k_bk_*), 0 for k_fuse_l.  The
+ * brick pipeline runs pass A over super-batches of super_batch_poses frames; the DEVICE cuts
+ * each into pose batches by the (ray, brick) pairs they really make against pair_capacity
+ * records of record_bytes (no host synchronisation); at most max_batches batches, each of at
+ * least poses_per_batch frames (the geometric bound rays x (1 + brick boundaries));
+ * scratch_bytes = the pipeline's device scratch. */
 typedef struct dmf_fuse_plan_info {
   int32_t brick;
   int32_t max_batches;
@@ -254,8 +256,13 @@ typedef struct dmf_fuse_plan_info {
   int32_t record_bytes;
   uint64_t pair_capacity;
   uint64_t scratch_bytes;
+  int32_t super_batch_poses;
+  int32_t reserved;
 } dmf_fuse_plan_info;
 int dmf_fuse_plan(const dmf_volume* v, const dmf_camera* cam, int32_t P, dmf_fuse_plan_info* out);
+/* Diagnostic (synchronises the stream): the pose batches the device cut the latest
+ * brick-pipeline super-batch of this volume into (0 before any brick-pipeline call). */
+int dmf_fuse_batches_used(dmf_volume* v, int32_t* batches);
 /* Elements of one tiled counter array (>= xdim*ydim*zdim: dims padded to 2, 2, 4). */
 int dmf_fuse_counter_cells(const dmf_volume* v, int64_t* n);
 /* Tiled counters -> x-major int32 (xdim*ydim*zdim). */

@@ -72,3 +72,39 @@ def test_raytracing_driver_matches_oracle(tmp_path, oracle):
     cm = oracle.collision_cost_map(ov, poses)
     assert got["costmap"] == [int(x) for x in cm.ravel()]
     assert got["collide_from_0"] == [int(x == 2**31 - 1) for x in cm[0]]
+
+
+def test_raytracing_driver_fuse_depth_matches_oracle(tmp_path, oracle):
+    """The C++ drop-in's fusion extension (compat RayTracingEngine::fuseDepth + logOdds over
+    dmf_fuse_depth / dmf_fuse_finalize), driven from the headless driver after the reference
+    sequence: 3 depth frames fused into the driver's own volume give the oracle's hit / miss
+    counts and log-odds bit for bit (the per-frame integration of
+    tests/Raytracing.cpp:70-76 as one call)."""
+    assert os.path.exists(DRIVER), "build the driver: make -C depth-map-fusion-utils_amd"
+    pts, nrm = Hh.cloud()
+    fposes, fdepth, _ = Hh.frames()
+    poses = np.concatenate([fposes[:3], Hh.ref_style_poses()[:2]])
+    cloud = np.concatenate([pts, nrm], axis=1).astype(np.float32)
+    cloud.tofile(tmp_path / "cloud.bin")
+    scene.write_pose_file(tmp_path / "poses.txt", poses)
+    np.ascontiguousarray(fdepth[:3], np.uint16).tofile(tmp_path / "depth.bin")
+    out = subprocess.run([DRIVER, str(tmp_path / "cloud.bin"), str(tmp_path / "poses.txt"), str(tmp_path / "depth.bin"),
+                          "3", str(tmp_path / "fused.bin")], check=True, capture_output=True, text=True,
+                         timeout=600).stdout
+    line = [ln for ln in out.splitlines() if ln.startswith("fusion ")][0].split()
+    lo, hi = pts.min(0), pts.max(0)
+    ov = oracle.Volume()
+    ov.setDimensions(float(lo[0]), float(hi[0]), float(lo[1]), float(hi[1]), float(lo[2]), float(hi[2]))
+    ext = [int(np.float32(hi[i] - lo[i]) * np.float32(125)) for i in range(3)]
+    ov.setVolumeSize(*ext)
+    ov.constructVolume()
+    ho, mo, so = oracle.fuse_depth(ov, Hh.K, fdepth[:3], poses[:3], dmin=200, dmax=1000)
+    n = int(np.prod(ov.dims))
+    raw = np.fromfile(tmp_path / "fused.bin", np.uint8)
+    assert raw.size == 10 * n
+    hg = raw[: 4 * n].view(np.int32)
+    mg = raw[4 * n: 8 * n].view(np.int32)
+    lg = raw[8 * n:].view(np.int16)
+    assert [int(x) for x in line[1:4]] == [int(x) for x in so] and so[0] > 0
+    assert np.array_equal(hg, ho) and np.array_equal(mg, mo)
+    assert np.array_equal(lg, oracle.fuse_finalize(ho, mo))

@@ -150,12 +150,14 @@ def test_config_full_poses(cfg):
 
 
 def test_config3_batches_equal_single_batch(monkeypatch):
-    """Config 3's frames through the brick pipeline in batches of 7 poses == the budget's
-    default batching (pose batches accumulate into the same counters)."""
+    """Config 3's frames through the brick pipeline in batches of 7 poses (48 frames: 7
+    batches) == the default (one batch: the device's cut by the real pair count)."""
     f = Fusion(512, 1280, 720, 48, seed=99)
-    c0, s0, _ = f.run(53)
+    c0, s0, _ = f.run(57)
+    assert f._lib.fuse_batches_used(f.vol) == 1
     monkeypatch.setenv("DMF_BK_BATCH_POSES", "7")
-    c1, s1, _ = f.run(53)
+    c1, s1, _ = f.run(57)
+    assert f._lib.fuse_batches_used(f.vol) == 7
     assert np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
 
 
@@ -189,7 +191,7 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
     d_poses = torch.from_numpy(poses).to(dev)
     out = {}
     try:
-        for variant in (53, 40, 31):
+        for variant in (57, 40, 31):
             _lib.check(L.dmf_fuse_set_variant(variant))
             c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
             st = torch.zeros(8, dtype=torch.int64, device=dev)
@@ -199,7 +201,7 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
             out[variant] = (c, st.cpu().numpy(), L.dmf_fuse_kernel().decode())
     finally:
         _lib.check(L.dmf_fuse_set_variant(0))
-    (c0, s0, k0), (c1, s1, k1), (c2, s2, k2) = out[53], out[31], out[40]
+    (c0, s0, k0), (c1, s1, k1), (c2, s2, k2) = out[57], out[31], out[40]
     assert k0.startswith("dmf::k_bk_fuse_s") and k1.startswith("dmf::k_fuse_l") and k2.startswith("dmf::k_bk_fuse<")
     assert s0[0] > 10 ** 8 and np.array_equal(s0[:4], s1[:4]) and torch.equal(c0, c1)
     assert np.array_equal(s0[:4], s2[:4]) and torch.equal(c0, c2)
@@ -210,7 +212,7 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
     ov.constructVolume()
     ho, mo, _ = oracle.fuse_depth(ov, K, depth[2:3], poses[2:3], dmin=scene.DEPTH_MIN_MM, dmax=scene.DEPTH_MAX_MM,
                                   threads=16)
-    _lib.check(L.dmf_fuse_set_variant(53))
+    _lib.check(L.dmf_fuse_set_variant(57))
     try:
         c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
         _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth[2].data_ptr(), d_poses[2].data_ptr(), 1,
@@ -263,6 +265,8 @@ def test_config4_anchor_1024_poses():
     c0, s0, k0 = f.run(0)
     assert k0.startswith("dmf::k_bk_fuse_s")
     _invariants(f, c0, s0)
+    # the geometric bound would need several batches; the device's cut by the real pairs, one
+    assert _plan(f, 1024)[1] > 1 and f._lib.fuse_batches_used(f.vol) == 1
     c1, s1, k1 = f.run(31)
     assert k1.startswith("dmf::k_fuse_l") and np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
     del c1
@@ -277,8 +281,9 @@ def test_config4_anchor_1024_poses():
 
 def test_config5_shard_256_poses(oracle):
     """BASELINE config 5's per-GPU shard at its real size: 256 of the 2048 poses (rank 0's
-    block) of 1280x720 depth into 1024^3.  The default call runs the brick pipeline in
-    several pose batches; it equals k_fuse_l counter for counter, satisfies the counting
+    block) of 1280x720 depth into 1024^3.  The default call runs the brick pipeline (the
+    geometric bound would cut it into several pose batches; the device cuts it by the pairs
+    it really makes); it equals k_fuse_l counter for counter, satisfies the counting
     invariants, and two of its frames fused alone equal the oracle at the full grid."""
     f = Fusion(1024, 1280, 720, 256, shard=(8, 0))
     brick, batches = _plan(f, 256)
@@ -286,6 +291,7 @@ def test_config5_shard_256_poses(oracle):
     c0, s0, k0 = f.run(0)
     assert k0.startswith("dmf::k_bk_fuse_s")
     _invariants(f, c0, s0)
+    assert f._lib.fuse_batches_used(f.vol) >= 1
     c1, s1, k1 = f.run(31)
     assert k1.startswith("dmf::k_fuse_l") and np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
     del c0, c1

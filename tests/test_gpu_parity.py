@@ -580,13 +580,14 @@ def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
             L.dmf_device_free(h, p_)
 
 
-@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56])
+@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57])
 def brick_variant(dmf, request):
     """Select a brick-owned fusion variant for one test: DMF_FUSE_VARIANT 40-43 = the
     per-cell walk (k_bk_fuse: refill threshold, pair order, interleaving), 44-51 = the
     slab walk (k_bk_fuse_s, the default: refill threshold, unroll, two pairs per lane,
     branch-free body), 52-56 = refill threshold 20 / 24 / 28 with pair order spread
-    16 / 32 / 64 (53 = <24, 32>, the default)."""
+    16 / 32 / 64 on 24-B pair records (53 = <24, 32>, the round-2 default), 57 = <24, 32> on
+    20-B records (the default: the walk on beta = b >> 9, dmf_brick.hpp pack20)."""
     from dmf_amd import _lib
     L = _lib.load()
     _lib.check(L.dmf_fuse_set_variant(request.param))
@@ -694,12 +695,14 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
     assert int(c0[:nt].astype(np.int64).sum()) == int(s0[2])  # one hit per ray ending inside
 
 
-@pytest.mark.parametrize("pipe", ["1", "3"])
-def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, pipe):
-    """The brick pipeline (variants 53 = the default slab walk, 40 = per-cell walk) split into several pose
-    batches (DMF_BK_BATCH_POSES=2 over 5 frames: batches of 2, 2, 1) accumulates the same
-    counters as the oracle -- one after another, and pipelined over two scratch sets with
-    passes A/S/B on the volume's side stream (DMF_BK_PIPE=3)."""
+@pytest.mark.parametrize("mode", ["poses2", "paircap"])
+def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, mode):
+    """The brick pipeline (variants 0 = the default 20-B record slab walk, 53 = the 24-B
+    record, 40 = per-cell walk) cut into several pose batches accumulates the same counters
+    as the oracle.  poses2: at most 2 poses per batch (DMF_BK_BATCH_POSES) over 5 frames;
+    paircap: a pair capacity of 1.6 x the largest frame's pairs (DMF_BK_PAIR_CAP), so the
+    DEVICE cuts the batches by the pairs each frame really makes (k_bk_batches) and the host's
+    geometric-bound launches past the device's batch count exit at once."""
     poses, depth, _ = Hh.frames()
     poses, depth = poses[:5], depth[:5]
     ov = Hh.oracle_volume(oracle, n=80, clouds=[])
@@ -707,13 +710,48 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, pipe):
     gv = Hh.gpu_volume(n=80, clouds=[])
     from dmf_amd import _lib
     L = _lib.load()
-    monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
-    monkeypatch.setenv("DMF_BK_PIPE", pipe)
-    for variant, name in ((53, "dmf::k_bk_fuse_s<24, 32, 4, 1, false>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
-        _lib.check(L.dmf_fuse_set_variant(variant))  # the brick pipeline at this small grid
+    prm = dmf.FuseParams(dmin_mm=200, dmax_mm=1000)
+    if mode == "poses2":
+        monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
+        expect = 3
+    else:  # pairs per frame from single-frame device calls (stats[4] = pairs)
+        import ctypes as C
+        import torch
+        dev = torch.device("cuda", 0)
+        gv.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        nct = C.c_int64()
+        _lib.check(L.dmf_fuse_counter_cells(gv._h, C.addressof(nct)))
+        d_depth = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).to(dev)
+        d_poses = torch.from_numpy(np.ascontiguousarray(poses, np.float32)).to(dev)
+        cam = _lib.make_camera(K, 480, 640)
+        cnt = torch.zeros(2 * nct.value, dtype=torch.int32, device=dev)
+        _lib.check(L.dmf_fuse_set_variant(57))
+        per = []
         try:
-            hg, mg, sg = engine.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
+            for i in range(5):
+                st = torch.zeros(8, dtype=torch.int64, device=dev)
+                _lib.check(L.dmf_fuse_depth_device(gv._h, C.addressof(cam), d_depth[i].data_ptr(), d_poses[i].data_ptr(),
+                                                   1, C.addressof(prm), cnt.data_ptr(), cnt.data_ptr() + 4 * nct.value,
+                                                   st.data_ptr()))
+                torch.cuda.synchronize(dev)
+                per.append(int(st[4].item()))
+        finally:
+            _lib.check(L.dmf_fuse_set_variant(0))
+        cap = int(1.6 * max(per))
+        monkeypatch.setenv("DMF_BK_PAIR_CAP", str(cap))
+        expect, acc = 0, None  # the greedy cut, restated
+        for c in per:
+            if acc is None or acc + c > cap:
+                expect, acc = expect + 1, 0
+            acc += c
+        assert expect >= 3
+    for variant, name in ((0, "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true>"),
+                          (53, "dmf::k_bk_fuse_s<24, 32, 4, 1, false>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
+        _lib.check(L.dmf_fuse_set_variant(variant if variant else 57))  # the brick pipeline at this small grid
+        try:
+            hg, mg, sg = engine.fuse_depth(gv, depth, poses, prm)
             assert L.dmf_fuse_kernel().decode() == name
+            assert _lib.fuse_batches_used(gv) == expect
         finally:
             _lib.check(L.dmf_fuse_set_variant(0))
         assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)

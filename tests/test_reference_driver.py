@@ -39,7 +39,8 @@ K_REF = np.array([602.39306640625, 0.0, 314.6370849609375, 0.0, 602.39306640625,
 @pytest.mark.parametrize("src", [REF_SRC, REF_SC])
 def test_reference_drivers_compile_unchanged(tmp_path, src):
     exe = tmp_path / "driver"
-    r = subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(PKG, "compat"), "-I", os.path.join(ROOT, "include"),
+    r = subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(PKG, "compat"), "-I",
+                        os.path.join(PKG, "compat", "shims"), "-I", os.path.join(ROOT, "include"),
                         src, "-o", str(exe), "-L", os.path.join(PKG, "build"), "-ldmf", "-lpthread"],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
