@@ -1,0 +1,137 @@
+// dmf_io.hip — persistent form of the fused log-odds grid (optional
+// checkpoint/resume).  Host code only (no GPU needed).
+//
+// The reference's only persistent outputs are text files (writeCameraLocations,
+// FileRoutines.hpp:98-112, and a PCD); the fusion grid it never had.  The file is a
+// fixed little-endian header, the int16 grid in the reference's x-major voxel order, and a
+// CRC-32 of header + grid, so a torn or foreign file is rejected instead of loaded:
+//   "DMFGRID1" | u32 version = 1 | u32 header bytes = 104 | i32 dims[3] | u32 reserved = 0 |
+//   f64 bounds[6] (xmin, xmax, ymin, ymax, zmin, zmax) | i32 fuse params[6] | i16 grid[x*y*z] |
+//   u32 crc32 (IEEE 802.3, reflected 0xEDB88320) of every byte before it
+#include <cstdio>
+#include <cstring>
+#include <memory>
+
+#include "dmf_host.hpp"
+
+namespace dmf {
+namespace {
+
+constexpr char kMagic[8] = {'D', 'M', 'F', 'G', 'R', 'I', 'D', '1'};
+constexpr uint32_t kVersion = 1, kHeaderBytes = 104;
+static_assert(sizeof(dmf_fuse_params) == 24, "six int32 fuse parameters");
+
+struct Crc32 {
+  uint32_t table[256];
+  Crc32() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = c & 1u ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      table[i] = c;
+    }
+  }
+  uint32_t update(uint32_t crc, const void* data, size_t n) const {
+    const uint8_t* p = (const uint8_t*)data;
+    crc = ~crc;
+    for (size_t i = 0; i < n; ++i) crc = table[(crc ^ p[i]) & 0xffu] ^ (crc >> 8);
+    return ~crc;
+  }
+};
+
+const Crc32& crc32() {
+  static const Crc32 c;
+  return c;
+}
+
+void put_header(const dmf_grid_header* h, uint8_t out[kHeaderBytes]) {
+  memset(out, 0, kHeaderBytes);
+  memcpy(out, kMagic, 8);
+  memcpy(out + 8, &kVersion, 4);
+  memcpy(out + 12, &kHeaderBytes, 4);
+  memcpy(out + 16, h->dims, 12);  // bytes 28..31: reserved (0)
+  memcpy(out + 32, h->bounds, 48);
+  memcpy(out + 80, &h->params, 24);
+}
+
+struct File {
+  FILE* f = nullptr;
+  ~File() {
+    if (f) fclose(f);
+  }
+};
+
+int64_t cells_of(const int32_t d[3]) { return (int64_t)d[0] * d[1] * d[2]; }
+
+// Reads and checks the header; leaves the stream at the grid.  crc is updated over it.
+int read_header(FILE* f, dmf_grid_header* h, uint32_t* crc) {
+  uint8_t buf[kHeaderBytes];
+  if (fread(buf, 1, kHeaderBytes, f) != kHeaderBytes) return fail(DMF_ERR_INVALID, "grid file: short header");
+  uint32_t ver, hb, resv;
+  memcpy(&ver, buf + 8, 4);
+  memcpy(&hb, buf + 12, 4);
+  memcpy(&resv, buf + 28, 4);
+  if (memcmp(buf, kMagic, 8) != 0) return fail(DMF_ERR_INVALID, "grid file: bad magic");
+  if (ver != kVersion || hb != kHeaderBytes || resv != 0) return fail(DMF_ERR_INVALID, "grid file: unsupported version");
+  memcpy(h->dims, buf + 16, 12);
+  memcpy(h->bounds, buf + 32, 48);
+  memcpy(&h->params, buf + 80, 24);
+  for (int a = 0; a < 3; ++a)
+    if (h->dims[a] < 1 || h->dims[a] > (1 << 20)) return fail(DMF_ERR_INVALID, "grid file: bad dims");
+  *crc = crc32().update(0, buf, kHeaderBytes);
+  return DMF_OK;
+}
+
+}  // namespace
+}  // namespace dmf
+
+using namespace dmf;
+
+extern "C" {
+
+int dmf_grid_save(const char* path, const dmf_grid_header* h, const int16_t* logodds) {
+  DMF_API_BEGIN
+  if (!path || !h || !logodds) return fail(DMF_ERR_INVALID, "null argument");
+  for (int a = 0; a < 3; ++a)
+    if (h->dims[a] < 1 || h->dims[a] > (1 << 20)) return fail(DMF_ERR_INVALID, "bad dims");
+  uint8_t head[kHeaderBytes];
+  put_header(h, head);
+  File out;
+  out.f = fopen(path, "wb");
+  if (!out.f) return fail(DMF_ERR_INVALID, "cannot open %s for writing", path);
+  const size_t n = (size_t)cells_of(h->dims);
+  uint32_t crc = crc32().update(0, head, sizeof(head));
+  crc = crc32().update(crc, logodds, n * sizeof(int16_t));
+  if (fwrite(head, 1, sizeof(head), out.f) != sizeof(head) ||
+      fwrite(logodds, sizeof(int16_t), n, out.f) != n || fwrite(&crc, 4, 1, out.f) != 1)
+    return fail(DMF_ERR_INVALID, "short write to %s", path);
+  if (fclose(out.f) != 0) {
+    out.f = nullptr;
+    return fail(DMF_ERR_INVALID, "close of %s failed", path);
+  }
+  out.f = nullptr;
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_grid_load(const char* path, dmf_grid_header* h, int16_t* logodds, int64_t cap) {
+  DMF_API_BEGIN
+  if (!path || !h) return fail(DMF_ERR_INVALID, "null argument");
+  File in;
+  in.f = fopen(path, "rb");
+  if (!in.f) return fail(DMF_ERR_INVALID, "cannot open %s", path);
+  uint32_t crc = 0;
+  DMF_TRY(read_header(in.f, h, &crc));
+  const int64_t n = cells_of(h->dims);
+  if (!logodds) return DMF_OK;  // header only
+  if (cap < n) return fail(DMF_ERR_CAPACITY, "grid of %lld cells, buffer of %lld", (long long)n, (long long)cap);
+  if (fread(logodds, sizeof(int16_t), (size_t)n, in.f) != (size_t)n) return fail(DMF_ERR_INVALID, "grid file: short grid");
+  uint32_t stored = 0;
+  if (fread(&stored, 4, 1, in.f) != 1) return fail(DMF_ERR_INVALID, "grid file: missing checksum");
+  crc = crc32().update(crc, logodds, (size_t)n * sizeof(int16_t));
+  if (crc != stored) return fail(DMF_ERR_INVALID, "grid file: checksum mismatch");
+  if (fgetc(in.f) != EOF) return fail(DMF_ERR_INVALID, "grid file: trailing bytes");
+  return DMF_OK;
+  DMF_API_END
+}
+
+}  // extern "C"

@@ -62,6 +62,11 @@ class dmf_fuse_params(C.Structure):
                 ("l_min", C.c_int32), ("l_max", C.c_int32)]
 
 
+class dmf_grid_header(C.Structure):
+    _fields_ = [("dims", C.c_int32 * 3), ("reserved", C.c_int32), ("bounds", C.c_double * 6),
+                ("params", dmf_fuse_params)]
+
+
 _vp = C.c_void_p
 _p = C.c_void_p  # raw pointers are passed as integers (numpy .ctypes.data or device addresses)
 _i32 = C.c_int32
@@ -120,6 +125,8 @@ SIGNATURES = {
     "dmf_fuse_counters_to_linear_device": (C.c_int, [_vp, _p, _p]),
     "dmf_fuse_reserve": (C.c_int, [_vp, _p, _i32, C.c_uint64]),
     "dmf_fuse_plan": (C.c_int, [_vp, _p, _i32, _p]),
+    "dmf_grid_save": (C.c_int, [C.c_char_p, _p, _p]),
+    "dmf_grid_load": (C.c_int, [C.c_char_p, _p, _p, _i64]),
     "dmf_fuse_batches_used": (C.c_int, [_vp, _p]),
     "dmf_rccl_version": (C.c_int, [_p]),
     "dmf_comm_unique_id": (C.c_int, [_p]),
@@ -244,3 +251,29 @@ def fuse_batches_used(vol):
     n = C.c_int32()
     check(load().dmf_fuse_batches_used(vol._h, C.addressof(n)))
     return n.value
+
+
+def grid_save(path, logodds, dims, bounds, params=None):
+    """dmf_grid_save: the int16 log-odds grid (x-major, dims cells) with its geometry and
+    fusion parameters (dmf_fuse_params; None = the defaults) to `path`."""
+    lo = np.ascontiguousarray(logodds, np.int16).reshape(-1)
+    if lo.size != int(np.prod(dims)):
+        raise ValueError(f"logodds has {lo.size} cells, dims {tuple(dims)} need {int(np.prod(dims))}")
+    h = dmf_grid_header()
+    for a in range(3):
+        h.dims[a] = int(dims[a])
+    for i in range(6):
+        h.bounds[i] = float(bounds[i])
+    h.params = params if params is not None else default_fuse_params()
+    check(load().dmf_grid_save(os.fsencode(str(path)), C.addressof(h), lo.ctypes.data))
+
+
+def grid_load(path):
+    """dmf_grid_load -> (logodds int16 (x, y, z), bounds tuple, dmf_fuse_params)."""
+    h = dmf_grid_header()
+    L = load()
+    check(L.dmf_grid_load(os.fsencode(str(path)), C.addressof(h), None, 0))
+    dims = tuple(int(h.dims[a]) for a in range(3))
+    out = np.empty(int(np.prod(dims)), np.int16)
+    check(L.dmf_grid_load(os.fsencode(str(path)), C.addressof(h), out.ctypes.data, out.size))
+    return out.reshape(dims), tuple(float(h.bounds[i]) for i in range(6)), h.params

@@ -334,6 +334,22 @@ int dmf_fuse_merge_finalize_device(dmf_volume* v, int32_t* d_counters, const dmf
  * pose's id: the same when view ids grow with pose order, as in the reference's loops). */
 int dmf_flags_allreduce(dmf_volume* v, void* comm, void* stream);
 
+/* ---- persistent fused grid (checkpoint / resume; host only, no GPU needed) ------
+ * The clamped int16 log-odds grid (x-major, dims[0]*dims[1]*dims[2] cells) with its
+ * geometry and fusion parameters, little-endian, CRC-32 checked (csrc/dmf_io.hip).  The
+ * reference's only persistent outputs are text (FileRoutines.hpp:98-112
+ * writeCameraLocations); this is the fusion engine's counterpart.  dmf_grid_load with
+ * logodds = NULL reads the header only; DMF_ERR_CAPACITY if cap < the grid's cells; a bad
+ * magic, version, size or checksum is DMF_ERR_INVALID. */
+typedef struct dmf_grid_header {
+  int32_t dims[3];
+  int32_t reserved;
+  double bounds[6]; /* xmin, xmax, ymin, ymax, zmin, zmax (setDimensions) */
+  dmf_fuse_params params;
+} dmf_grid_header;
+int dmf_grid_save(const char* path, const dmf_grid_header* h, const int16_t* logodds);
+int dmf_grid_load(const char* path, dmf_grid_header* h, int16_t* logodds, int64_t cap);
+
 /* ---- OccupancyGrid  (include/OccupancyGrid.hpp:50-318) ----------------------- */
 /* The reference's second fusion path.  updateStates is computed in the deterministic
  * single-threaded order (the reference's OpenMP loops race); state is dense, x-major,

@@ -1,0 +1,67 @@
+"""CPU: the persistent log-odds grid (dmf_grid_save / dmf_grid_load, csrc/dmf_io.hip;
+SURVEY.md §5 checkpoint / resume).  Host-only code: round trip of grid, geometry and fusion
+parameters; header-only reads; the file's layout (magic, little-endian header, x-major
+int16 grid, CRC-32 = zlib.crc32 of every byte before it); torn, corrupted and foreign files
+are rejected; a too-small buffer reports DMF_ERR_CAPACITY."""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from dmf_amd import _lib
+
+
+def _grid(dims, seed=0):
+    return np.random.default_rng(seed).integers(-2000, 3512, size=dims).astype(np.int16)
+
+
+@pytest.mark.parametrize("dims", [(1, 1, 1), (5, 3, 7), (64, 33, 17)])
+def test_round_trip(tmp_path, dims):
+    g = _grid(dims)
+    bounds = (-0.5, 0.5, -0.25, 0.75, 0.0, 1.0 / 3)
+    prm = _lib.default_fuse_params(dmin_mm=200, dmax_mm=1000)
+    path = tmp_path / "grid.dmf"
+    _lib.grid_save(path, g, dims, bounds, prm)
+    g2, b2, p2 = _lib.grid_load(path)
+    assert g2.shape == dims and np.array_equal(g2, g)
+    assert b2 == bounds
+    assert (p2.dmin_mm, p2.dmax_mm, p2.l_hit, p2.l_miss, p2.l_min, p2.l_max) == (200, 1000, 847, -405, -2000, 3511)
+    raw = path.read_bytes()
+    n = int(np.prod(dims))
+    assert len(raw) == 104 + 2 * n + 4 and raw[:8] == b"DMFGRID1"
+    assert struct.unpack_from("<III", raw, 8) == (1, 104, dims[0])
+    assert struct.unpack_from("<6d", raw, 32) == bounds
+    assert np.array_equal(np.frombuffer(raw, "<i2", count=n, offset=104), g.reshape(-1))
+    assert struct.unpack_from("<I", raw, 104 + 2 * n)[0] == zlib.crc32(raw[:104 + 2 * n])
+
+
+def test_rejects_bad_files(tmp_path):
+    g = _grid((6, 5, 4), 1)
+    path = tmp_path / "g.dmf"
+    _lib.grid_save(path, g, g.shape, (0, 1, 0, 1, 0, 1))
+    raw = bytearray(path.read_bytes())
+    L = _lib.load()
+    h = _lib.dmf_grid_header()
+    buf = np.empty(g.size, np.int16)
+
+    def load(data, cap=g.size):
+        p = tmp_path / "x.dmf"
+        p.write_bytes(bytes(data))
+        import ctypes as C
+        return L.dmf_grid_load(str(p).encode(), C.addressof(h), buf.ctypes.data, cap)
+    assert load(raw) == _lib.DMF_OK and np.array_equal(buf.reshape(g.shape), g)
+    bad = bytearray(raw)
+    bad[104 + 7] ^= 0x40  # one grid bit
+    assert load(bad) == _lib.DMF_ERR_INVALID
+    assert load(raw[:-3]) == _lib.DMF_ERR_INVALID  # torn
+    assert load(raw + b"\0") == _lib.DMF_ERR_INVALID  # trailing bytes
+    bad = bytearray(raw)
+    bad[0:8] = b"NOTAGRID"
+    assert load(bad) == _lib.DMF_ERR_INVALID
+    bad = bytearray(raw)
+    bad[8] = 2  # version
+    assert load(bad) == _lib.DMF_ERR_INVALID
+    assert load(raw, cap=g.size - 1) == _lib.DMF_ERR_CAPACITY
+    with pytest.raises(ValueError):
+        _lib.grid_save(path, g, (6, 5, 5), (0, 1, 0, 1, 0, 1))
