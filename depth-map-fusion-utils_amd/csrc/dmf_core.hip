@@ -649,6 +649,7 @@ dmf::Geom dmf_volume::geom() const {
     g.vlo[a] = lo;
     g.vhi[a] = hi;
   }
+  fbin_setup(g);
   return g;
 }
 

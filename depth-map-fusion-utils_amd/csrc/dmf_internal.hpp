@@ -9,11 +9,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 #include <string>
 #include <vector>
 
 #include "dmf.h"
+#include "dmf_geom.hpp"
 
 namespace dmf {
 
@@ -23,19 +25,6 @@ constexpr double kZMin = 0.20, kZMax = 1.0;    // RayTracingEngine.hpp:24-25
 constexpr int kWave = 64;
 
 // ---------------------------------------------------------------- geometry
-// Volume.hpp:54-60 fields needed on device.
-struct Geom {
-  double mn[3];   // xmin_, ymin_, zmin_
-  double mx[3];   // xmax_, ymax_, zmax_
-  double dl[3];   // xdelta_, ...
-  double hdl[3];  // xdelta_/2.0 (exact halving)
-  double inv[3];  // 1/delta when delta is a power of two (then x*inv == x/delta exactly)
-  int pow2;       // all three deltas are powers of two
-  int n[3];       // xdim_, ydim_, zdim_ after constructVolume truncation
-  float vlo[3];   // smallest float x with (double)x > mn  (validPoints as float compares)
-  float vhi[3];   // largest float x with (double)x < mx
-};
-
 // Camera.hpp:26 fx=K[0], cx=K[2], fy=K[4], cy=K[5] promoted to double.
 struct CamP {
   double fx, cx, fy, cy;
@@ -124,14 +113,6 @@ __device__ inline bool deproject_valid(const CamP& c, float x, float y, float z,
 __device__ inline bool valid_points(const Geom& g, float x, float y, float z) {
   return !((double)x >= g.mx[0] || (double)y >= g.mx[1] || (double)z >= g.mx[2] ||
            (double)x <= g.mn[0] || (double)y <= g.mn[1] || (double)z <= g.mn[2]);
-}
-
-// Volume.hpp:150-156 getVoxel: floor((x - min)/delta) in double.  For power-of-two
-// deltas the multiply by the exact reciprocal gives the identical double.
-__device__ inline int bin_axis(const Geom& g, int a, float x) {
-  const double t = (double)x - g.mn[a];
-  const double q = g.pow2 ? t * g.inv[a] : t / g.dl[a];
-  return (int)floor(q);
 }
 
 // Volume.hpp:167-170 validCoords

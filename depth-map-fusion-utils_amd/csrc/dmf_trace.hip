@@ -204,6 +204,7 @@ __global__ __launch_bounds__(256) void k_reverse(Geom g, DevVol vd, CamP cam, co
 struct RevLane {
   float cen[3], v[3], rv[3];
   int cx, cy, cz;
+  bool fdiv;            // march_sample_fast is exact for this lane's v
   int s;                // next sample index
   uint32_t known_full;  // last brick found occupied / not skippable
   int item;             // local item index, -1 = idle
@@ -213,8 +214,43 @@ struct RevLane {
 };
 
 __device__ inline bool valid_points_f(const Geom& g, const float p[3]) {
-  return p[0] >= g.vlo[0] && p[0] <= g.vhi[0] && p[1] >= g.vlo[1] && p[1] <= g.vhi[1] && p[2] >= g.vlo[2] &&
-         p[2] <= g.vhi[2];
+  // one combined mask (no per-axis branches)
+  return (p[0] >= g.vlo[0]) & (p[0] <= g.vhi[0]) & (p[1] >= g.vlo[1]) & (p[1] <= g.vhi[1]) & (p[2] >= g.vlo[2]) &
+         (p[2] <= g.vhi[2]);
+}
+
+// march_sample without div_rn's range guard: exact when every non-zero |v_a| >= 2^-30, so
+// that |v_a * depth| lies in div_rn's checked domain [2^-40, 2^40] (tools/fastdiv_selftest.cpp)
+// or is +-0 (whose sign no later step can see: it is only added to the centre and then
+// compared / binned).  Lanes flag it at setup (RevLane::fdiv); a wave takes this path when
+// all its busy lanes do.
+__device__ inline void march_sample_fast(const float cen[3], const float v[3], int depth, float p[3]) {
+  const float fd = (float)depth, y = 1.0f / 1000.0f;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const float n = v[a] * fd;
+    const float q0 = n * y;
+    const float r = fmaf(-1000.0f, q0, n);
+    p[a] = cen[a] + fmaf(r, y, q0);
+  }
+}
+
+template <bool kFastDiv>
+__device__ inline void rev_sample(const float cen[3], const float v[3], int depth, float p[3]) {
+  if (kFastDiv) march_sample_fast(cen, v, depth, p);
+  else march_sample(cen, v, depth, p);
+}
+
+// getVoxel of a point inside the volume: the certified float bins (dmf_geom.hpp
+// bin_axis_f), the double bins only for lanes whose estimate is within eps of a boundary
+// (the branch is skipped when no lane needs it).
+__device__ inline void bin_point(const Geom& g, const float p[3], int& a, int& b, int& c) {
+  const int ok = (int)bin_axis_f(g, 0, p[0], &a) & (int)bin_axis_f(g, 1, p[1], &b) & (int)bin_axis_f(g, 2, p[2], &c);
+  if (!(g.fbin && ok)) {
+    a = bin_axis(g, 0, p[0]);
+    b = bin_axis(g, 1, p[1]);
+    c = bin_axis(g, 2, p[2]);
+  }
 }
 
 // One sample of the reverse march (RayTracingEngine.hpp:172-200): 0 = continue,
@@ -227,14 +263,16 @@ __device__ inline bool valid_points_f(const Geom& g, const float p[3]) {
 // (and inside the volume) so does every sample between them — none can hit an
 // occupied cell, the centroid's cell (occupied) or leave the volume.  j is estimated
 // from the cube faces and verified by evaluating sample j exactly.
+template <bool kFastDiv>
 __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int depth0, int max_steps,
                                int64_t& samples) {
   if (L.s >= max_steps) return 3;
   float p[3];
-  march_sample(L.cen, L.v, depth0 + L.s, p);
+  rev_sample<kFastDiv>(L.cen, L.v, depth0 + L.s, p);
   ++samples;
   if (!valid_points_f(g, p)) return 2;
-  const int a = bin_axis(g, 0, p[0]), b = bin_axis(g, 1, p[1]), c = bin_axis(g, 2, p[2]);
+  int a, b, c;
+  bin_point(g, p, a, b, c);
   if (a == L.cx && b == L.cy && c == L.cz) { ++L.s; return 0; }
   if (!valid_coords(g, a, b, c)) return 2;
   const uint32_t ob = occ_bit(g, a, b, c);
@@ -261,10 +299,11 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
       if (jf > (float)(L.s + 1) && jf < (float)max_steps) {
         const int j = (int)jf;
         float q[3];
-        march_sample(L.cen, L.v, depth0 + j, q);
+        rev_sample<kFastDiv>(L.cen, L.v, depth0 + j, q);
         ++samples;
         if (valid_points_f(g, q)) {
-          const int qa = bin_axis(g, 0, q[0]), qb = bin_axis(g, 1, q[1]), qc = bin_axis(g, 2, q[2]);
+          int qa, qb, qc;
+          bin_point(g, q, qa, qb, qc);
           if (qa >= clo[0] && qa < chi[0] && qb >= clo[1] && qb < chi[1] && qc >= clo[2] && qc < chi[2]) {
             L.s = j + 1;  // samples s+1 .. j lie inside the empty cube
             return 0;
@@ -344,6 +383,9 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
               L.cen[a] = cen[a];
               L.rv[a] = L.v[a] != 0.0f ? 1000.0f / L.v[a] : 0.0f;
             }
+            L.fdiv = true;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) L.fdiv &= L.v[a] == 0.0f || fabsf(L.v[a]) >= 0x1p-30f;
             L.cx = bin_axis(g, 0, cen[0]);
             L.cy = bin_axis(g, 1, cen[1]);
             L.cz = bin_axis(g, 2, cen[2]);
@@ -362,12 +404,21 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
       if (next >= nitems) break;
       continue;
     }
-    // march: up to kBurst samples per busy lane
+    // march: up to kBurst samples per busy lane (the guard-free division when every busy
+    // lane allows it: a wave-uniform choice)
     int st = 0;
+    if (__builtin_amdgcn_ballot_w64(L.item >= 0 && !L.fdiv) == 0) {
 #pragma unroll 1
-    for (int b = 0; b < kBurst; ++b) {
-      if (L.item >= 0 && st == 0) st = rev_step(g, vd, L, depth0, max_steps, samples);
-      if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
+      for (int b = 0; b < kBurst; ++b) {
+        if (L.item >= 0 && st == 0) st = rev_step<true>(g, vd, L, depth0, max_steps, samples);
+        if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
+      }
+    } else {
+#pragma unroll 1
+      for (int b = 0; b < kBurst; ++b) {
+        if (L.item >= 0 && st == 0) st = rev_step<false>(g, vd, L, depth0, max_steps, samples);
+        if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
+      }
     }
     if (L.item >= 0 && st != 0) {
       if (st == 3) ++ncap;

@@ -3,6 +3,8 @@
   restarts the fine walk on exactly the cells the plain walk visits in each brick;
 * tools/fastdiv_selftest.cpp — div_rn (dmf_internal.hpp) equals IEEE division over the
   projection and reverse-march domains;
+* tools/binning_selftest.cpp — the marches' certified float binning (dmf_geom.hpp
+  bin_axis_f) equals the reference getVoxel binning in double whenever it certifies;
 * ASan + UBSan builds of both self-tests and of the CPU oracle
   (tools/oracle_sanitize.cpp drives every oracle entry point on a small scene): undefined
   behaviour or an out-of-bounds access in the checkers fails the CPU suite."""
@@ -32,6 +34,14 @@ def test_brick_decomposition_selftest(tmp_path):
 
 
 @pytest.mark.timeout(300)
+def test_certified_binning_selftest(tmp_path):
+    r = _build_and_run(os.path.join(ROOT, "tools", "binning_selftest.cpp"), str(tmp_path), ["97"],
+                       ["-I", os.path.join(ROOT, "depth-map-fusion-utils_amd", "csrc")])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches" in r.stdout.splitlines()[-1]
+
+
+@pytest.mark.timeout(300)
 def test_fast_division_selftest(tmp_path):
     r = _build_and_run(os.path.join(ROOT, "tools", "fastdiv_selftest.cpp"), str(tmp_path), [])
     assert r.returncode == 0, r.stdout + r.stderr
@@ -45,6 +55,8 @@ def test_selftests_and_oracle_under_sanitizers(tmp_path):
     assert r.returncode == 0 and " 0 failures" in r.stdout, r.stdout + r.stderr
     r = _build_and_run(os.path.join(ROOT, "tools", "fastdiv_selftest.cpp"), str(tmp_path), ["9973"], (), SAN)
     assert r.returncode == 0 and " 0 mismatches" in r.stdout, r.stdout + r.stderr
+    r = _build_and_run(os.path.join(ROOT, "tools", "binning_selftest.cpp"), str(tmp_path), ["20011"], inc, SAN)
+    assert r.returncode == 0 and " 0 mismatches" in r.stdout.splitlines()[-1], r.stdout + r.stderr
     r = _build_and_run(os.path.join(ROOT, "tools", "oracle_sanitize.cpp"), str(tmp_path), [], ["-fopenmp"], SAN,
                        [os.path.join(ROOT, "oracle", "oracle.cpp")])
     assert r.returncode == 0 and "oracle sanitize ok" in r.stdout, r.stdout + r.stderr
