@@ -198,6 +198,24 @@ __device__ inline void dda_advance(Ray& R) {
   R.c[2] += s2 ? R.st[2] : 0;
 }
 
+// The acceptance of integratePointCloud(cloud, normals) (Volume.hpp:199-228):
+// validPoints(E) && validCoords(getVoxel(E)).  validPoints as float compares (vlo / vhi,
+// dmf_geom.hpp) and the certified float bins (a NaN endpoint, from a non-finite pose, is
+// outside: the reference's getVoxel gives INT_MIN for it, which validCoords rejects).
+__device__ inline bool endpoint_inside(const Geom& g, const float E[3]) {
+  const bool in = (E[0] >= g.vlo[0]) & (E[0] <= g.vhi[0]) & (E[1] >= g.vlo[1]) & (E[1] <= g.vhi[1]) &
+                  (E[2] >= g.vlo[2]) & (E[2] <= g.vhi[2]);
+  if (!in) return false;
+  int a, b, c;
+  const int ok = (int)bin_axis_f(g, 0, E[0], &a) & (int)bin_axis_f(g, 1, E[1], &b) & (int)bin_axis_f(g, 2, E[2], &c);
+  if (!(g.fbin && ok)) {
+    a = bin_axis(g, 0, E[0]);
+    b = bin_axis(g, 1, E[1]);
+    c = bin_axis(g, 2, E[2]);
+  }
+  return valid_coords(g, a, b, c);
+}
+
 // Per-pixel ray: back-projection (Camera.hpp:24-45) + binning of the endpoint
 // (Volume.hpp:150-156, 199-228) + DDA setup.  Returns the update count (0 = no ray).
 __device__ inline int pixel_ray(const Geom& g, const CamP& cam, const uint16_t* __restrict__ depth,
@@ -213,8 +231,7 @@ __device__ inline int pixel_ray(const Geom& g, const CamP& cam, const uint16_t* 
   float pc[3], E[3];
   project(cam, r, c, d, pc);
   xform(T.f, pc[0], pc[1], pc[2], E);
-  bool inside = valid_points(g, E[0], E[1], E[2]);
-  if (inside) inside = valid_coords(g, bin_axis(g, 0, E[0]), bin_axis(g, 1, E[1]), bin_axis(g, 2, E[2]));
+  const bool inside = endpoint_inside(g, E);
   const float O[3] = {T.f[3], T.f[7], T.f[11]};
   if (!dda_setup(g, O, E, inside, R)) { R.left = 0; return 0; }
   return R.left;
@@ -233,8 +250,7 @@ __device__ inline bool pixel_quant_d(const Geom& g, const CamP& cam, int d, cons
   float pc[3], E[3];
   project(cam, r, c, d, pc);
   xform(T.f, pc[0], pc[1], pc[2], E);
-  inside = valid_points(g, E[0], E[1], E[2]);
-  if (inside) inside = valid_coords(g, bin_axis(g, 0, E[0]), bin_axis(g, 1, E[1]), bin_axis(g, 2, E[2]));
+  inside = endpoint_inside(g, E);
   const float O[3] = {T.f[3], T.f[7], T.f[11]};
   return dda_quantize(g, O, E, inside, qs, qe);
 }
@@ -251,8 +267,7 @@ __device__ inline bool pixel_quant_go(const Geom& g, const CamP& cam, int d, con
   float pc[3], E[3];
   project(cam, r, c, d, pc);
   xform(T.f, pc[0], pc[1], pc[2], E);
-  inside = valid_points(g, E[0], E[1], E[2]);
-  if (inside) inside = valid_coords(g, bin_axis(g, 0, E[0]), bin_axis(g, 1, E[1]), bin_axis(g, 2, E[2]));
+  inside = endpoint_inside(g, E);
   return dda_quantize_go(g, go, E, inside, qs, qe);
 }
 

@@ -748,7 +748,7 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, co
       project(cam, r, c, zd, pc);
       xform(m, pc[0], pc[1], pc[2], w);
       ++samples;
-      if (!valid_points(g, w[0], w[1], w[2])) {
+      if (!valid_points_f(g, w)) {
         if (kSkip && !entered) {
           // jump to the last sample before the line enters the volume grown by the margin
           entered = true;  // (once: after the entry the march proceeds normally)
@@ -774,7 +774,7 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, co
             project(cam, r, c, zj, qc);
             xform(m, qc[0], qc[1], qc[2], q);
             ++samples;
-            if (!valid_points(g, q[0], q[1], q[2])) {  // verified: still outside
+            if (!valid_points_f(g, q)) {  // verified: still outside
               k = kj;
               zd = zj;
             }
@@ -783,7 +783,8 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, co
         continue;
       }
       entered = true;
-      const int a = bin_axis(g, 0, w[0]), b = bin_axis(g, 1, w[1]), cc = bin_axis(g, 2, w[2]);
+      int a, b, cc;
+      bin_point(g, w, a, b, cc);
       if (!valid_coords(g, a, b, cc)) {  // reference indexes voxels_ unguarded here (UB)
         atomicAdd(hazards, 1ull);
         continue;
@@ -1087,8 +1088,10 @@ __global__ void k_will_collide(Geom g, const uint32_t* __restrict__ occ, const f
     const float px = a[0] + div_rn(v[0] * fd, 1000.0f, 1.0f / 1000.0f);
     const float py = a[1] + div_rn(v[1] * fd, 1000.0f, 1.0f / 1000.0f);
     const float pz = a[2] + div_rn(v[2] * fd, 1000.0f, 1.0f / 1000.0f);
-    if (!valid_points(g, px, py, pz)) continue;
-    const int x = bin_axis(g, 0, px), y = bin_axis(g, 1, py), z = bin_axis(g, 2, pz);
+    const float pp[3] = {px, py, pz};
+    if (!valid_points_f(g, pp)) continue;
+    int x, y, z;
+    bin_point(g, pp, x, y, z);
     if (!valid_coords(g, x, y, z)) continue;
     if (occ_test(occ, occ_bit(g, x, y, z))) collided = true;
   }
@@ -1134,8 +1137,10 @@ __global__ __launch_bounds__(64 * kCostWaves) void k_cost_map(Geom g, const uint
       const float px = a[0] + div_rn(v[0] * fd, 1000.0f, 1.0f / 1000.0f);
       const float py = a[1] + div_rn(v[1] * fd, 1000.0f, 1.0f / 1000.0f);
       const float pz = a[2] + div_rn(v[2] * fd, 1000.0f, 1.0f / 1000.0f);
-      if (valid_points(g, px, py, pz)) {
-        const int x = bin_axis(g, 0, px), y = bin_axis(g, 1, py), z = bin_axis(g, 2, pz);
+      const float pp[3] = {px, py, pz};
+      if (valid_points_f(g, pp)) {
+        int x, y, z;
+        bin_point(g, pp, x, y, z);
         hit = valid_coords(g, x, y, z) && occ_test(occ, occ_bit(g, x, y, z));
       }
     }
