@@ -1620,6 +1620,12 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     const uint32_t nb_pairs = cnt[b], np = (nb_pairs + part_max - 1) / part_max;
     const uint32_t p0 = off[b] + (uint32_t)(((uint64_t)nb_pairs * j) / np);
     const uint32_t n = (uint32_t)(((uint64_t)nb_pairs * (j + 1)) / np) - (uint32_t)(((uint64_t)nb_pairs * j) / np);
+    // 20-B records: buffer resources over the part's records (32-bit offsets < 2^21, no
+    // 64-bit address math per load; a load past the part returns zeros)
+    const __amdgpu_buffer_rsrc_t rs_a = __builtin_amdgcn_make_buffer_rsrc((void*)(pa + p0), (short)0, (int)(n * 16u),
+                                                                         0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)(pw + p0), (short)0, (int)(n * 4u),
+                                                                         0x00020000);
     const int bz = b % bg.nb[2], by = (b / bg.nb[2]) % bg.nb[1], bx = b / (bg.nb[2] * bg.nb[1]);
     const int lo0 = bx << bk::kLog, lo1 = by << bk::kLog, lo2 = bz << bk::kLog;
     if (tid == 0) {
@@ -1702,11 +1708,15 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
         if ((need[q] >> l) & 1ull) {
           const uint32_t k = base + (uint32_t)lane_prefix(need[q]);
           fok[q] = k < n;
-          if (fok[q]) {
+          if constexpr (R20) {
+            const uint32_t o = bk_order<S_ORDER>(k, n);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_a, o * 16u, 0, 0);
+            ca[q] = make_uint4(v[0], v[1], v[2], v[3]);
+            cb[q].x = __builtin_amdgcn_raw_buffer_load_b32(rs_w, o * 4u, 0, 0);
+          } else if (fok[q]) {
             const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
             ca[q] = pa[i];
-            if constexpr (R20) cb[q] = make_uint2(pw[i], 0u);
-            else cb[q] = pb[i];
+            cb[q] = pb[i];
           }
         }
         base += (uint32_t)__builtin_popcountll(need[q]);
