@@ -263,7 +263,18 @@ __device__ inline void bin_point(const Geom& g, const float p[3], int& a, int& b
 // (and inside the volume) so does every sample between them — none can hit an
 // occupied cell, the centroid's cell (occupied) or leave the volume.  j is estimated
 // from the cube faces and verified by evaluating sample j exactly.
-template <bool kFastDiv>
+template <bool kFBin>
+__device__ inline void bin_point_t(const Geom& g, const float p[3], int& a, int& b, int& c) {
+  if (kFBin) {
+    bin_point(g, p, a, b, c);
+  } else {
+    a = bin_axis(g, 0, p[0]);
+    b = bin_axis(g, 1, p[1]);
+    c = bin_axis(g, 2, p[2]);
+  }
+}
+
+template <bool kFastDiv, bool kFBin>
 __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int depth0, int max_steps,
                                int64_t& samples) {
   if (L.s >= max_steps) return 3;
@@ -272,7 +283,7 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   ++samples;
   if (!valid_points_f(g, p)) return 2;
   int a, b, c;
-  bin_point(g, p, a, b, c);
+  bin_point_t<kFBin>(g, p, a, b, c);
   if (a == L.cx && b == L.cy && c == L.cz) { ++L.s; return 0; }
   if (!valid_coords(g, a, b, c)) return 2;
   const uint32_t ob = occ_bit(g, a, b, c);
@@ -303,7 +314,7 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
         ++samples;
         if (valid_points_f(g, q)) {
           int qa, qb, qc;
-          bin_point(g, q, qa, qb, qc);
+          bin_point_t<kFBin>(g, q, qa, qb, qc);
           if (qa >= clo[0] && qa < chi[0] && qb >= clo[1] && qb < chi[1] && qc >= clo[2] && qc < chi[2]) {
             L.s = j + 1;  // samples s+1 .. j lie inside the empty cube
             return 0;
@@ -317,7 +328,9 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   return 0;
 }
 
-template <bool kEnum, int kItems, int kRefill, int kBurst>
+// kMode (A/B): bit 0 = the guard-free division for waves that allow it, bit 1 = the
+// certified float bins (3 = both, the default)
+template <bool kEnum, int kItems, int kRefill, int kBurst, int kMode = 3>
 __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses,
                                                    int64_t nelem, EnumList el, int depth0, int max_steps, float dstar,
                                                    int viz, int normal_test, uint64_t* __restrict__ vis_mask,
@@ -407,16 +420,17 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
     // march: up to kBurst samples per busy lane (the guard-free division when every busy
     // lane allows it: a wave-uniform choice)
     int st = 0;
-    if (__builtin_amdgcn_ballot_w64(L.item >= 0 && !L.fdiv) == 0) {
+    constexpr bool kFB = (kMode & 2) != 0;
+    if ((kMode & 1) && __builtin_amdgcn_ballot_w64(L.item >= 0 && !L.fdiv) == 0) {
 #pragma unroll 1
       for (int b = 0; b < kBurst; ++b) {
-        if (L.item >= 0 && st == 0) st = rev_step<true>(g, vd, L, depth0, max_steps, samples);
+        if (L.item >= 0 && st == 0) st = rev_step<true, kFB>(g, vd, L, depth0, max_steps, samples);
         if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
       }
     } else {
 #pragma unroll 1
       for (int b = 0; b < kBurst; ++b) {
-        if (L.item >= 0 && st == 0) st = rev_step<false>(g, vd, L, depth0, max_steps, samples);
+        if (L.item >= 0 && st == 0) st = rev_step<false, kFB>(g, vd, L, depth0, max_steps, samples);
         if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
       }
     }
@@ -618,6 +632,10 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
   hipLaunchKernelGGL((k_reverse_q<E, kRevItems, 8, 8>), gridq, dim3(256), 0, v->stream, v->geom(), v->dev(),       \
                      cam_params(cam), tab, nelem, el, depth0, max_march_steps(v), v->dstar, viz, NT, vis, good, words, \
                      st, found, hz)
+#define DMF_REVQM(E, NT, MODE)                                                                                     \
+  hipLaunchKernelGGL((k_reverse_q<E, kRevItems, 8, 8, MODE>), gridq, dim3(256), 0, v->stream, v->geom(), v->dev(), \
+                     cam_params(cam), tab, nelem, el, depth0, max_march_steps(v), v->dstar, viz, NT, vis, good, words, \
+                     st, found, hz)
 #define DMF_REVQX(E, NT, IT, RF, BU)                                                                              \
   hipLaunchKernelGGL((k_reverse_q<E, IT, RF, BU>), dim3((unsigned)((nelem + 4 * IT - 1) / (4 * IT)), (unsigned)P),       \
                      dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab, nelem, el, depth0,             \
@@ -634,6 +652,9 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
         case 6: if (enumerate) DMF_REVQX(true, 0, 1024, 16, 8); else DMF_REVQX(false, 1, 1024, 16, 8); break;
         case 7: if (enumerate) DMF_REVQX(true, 0, 256, 16, 4); else DMF_REVQX(false, 1, 256, 16, 4); break;
         case 8: if (enumerate) DMF_REVQX(true, 0, 512, 24, 4); else DMF_REVQX(false, 1, 512, 24, 4); break;
+        case 9: if (enumerate) DMF_REVQM(true, 0, 0); else DMF_REVQM(false, 1, 0); break;    // round-2 arithmetic
+        case 10: if (enumerate) DMF_REVQM(true, 0, 2); else DMF_REVQM(false, 1, 2); break;   // float bins only
+        case 11: if (enumerate) DMF_REVQM(true, 0, 1); else DMF_REVQM(false, 1, 1); break;   // fast division only
         default: if (enumerate) DMF_REVQ(true, 0); else DMF_REVQ(false, 1); break;
       }
     } else if (enumerate) {
@@ -644,6 +665,7 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
 #undef DMF_REV
 #undef DMF_REVQ
 #undef DMF_REVQX
+#undef DMF_REVQM
     DMF_LAUNCH_CHECK();
   }
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 2));
