@@ -200,20 +200,13 @@ __device__ inline void dda_advance(Ray& R) {
 
 // The acceptance of integratePointCloud(cloud, normals) (Volume.hpp:199-228):
 // validPoints(E) && validCoords(getVoxel(E)).  validPoints as float compares (vlo / vhi,
-// dmf_geom.hpp) and the certified float bins (a NaN endpoint, from a non-finite pose, is
-// outside: the reference's getVoxel gives INT_MIN for it, which validCoords rejects).
+// dmf_geom.hpp; a NaN endpoint, from a non-finite pose, is outside: the reference's getVoxel
+// gives INT_MIN for it, which validCoords rejects), then getVoxel in double.
 __device__ inline bool endpoint_inside(const Geom& g, const float E[3]) {
   const bool in = (E[0] >= g.vlo[0]) & (E[0] <= g.vhi[0]) & (E[1] >= g.vlo[1]) & (E[1] <= g.vhi[1]) &
                   (E[2] >= g.vlo[2]) & (E[2] <= g.vhi[2]);
   if (!in) return false;
-  int a, b, c;
-  const int ok = (int)bin_axis_f(g, 0, E[0], &a) & (int)bin_axis_f(g, 1, E[1], &b) & (int)bin_axis_f(g, 2, E[2], &c);
-  if (!(g.fbin && ok)) {
-    a = bin_axis(g, 0, E[0]);
-    b = bin_axis(g, 1, E[1]);
-    c = bin_axis(g, 2, E[2]);
-  }
-  return valid_coords(g, a, b, c);
+  return valid_coords(g, bin_axis(g, 0, E[0]), bin_axis(g, 1, E[1]), bin_axis(g, 2, E[2]));
 }
 
 // Per-pixel ray: back-projection (Camera.hpp:24-45) + binning of the endpoint
@@ -1958,9 +1951,10 @@ static int fuse_variant() {
 }
 constexpr int kVariantBrick = 40;
 constexpr int kVariantSlab = 44;  // 44..53: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
-constexpr int kVariantLast = 57;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
+constexpr int kVariantLast = 63;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
 constexpr int kVariantRec20 = 57;  // the default: 20-B pair records (beta state, dmf_brick.hpp pack20)
-static bool is_rec20_variant(int v) { return v == 0 || v == kVariantRec20; }
+// 57-63: 20-B records (57 = the default <24, 32, 4>; 58-63 refill / spread / unroll A/B)
+static bool is_rec20_variant(int v) { return v == 0 || (v >= kVariantRec20 && v <= kVariantLast); }
 static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantLast; }
 static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantLast); }
 static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
@@ -2224,6 +2218,12 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         case 54: DMF_BK_FUSE_S(24, 64, 4, 1); break;
         case 55: DMF_BK_FUSE_S(20, 32, 4, 1); break;
         case 56: DMF_BK_FUSE_S(28, 32, 4, 1); break;
+        case 58: DMF_BK_FUSE_S20(20, 32, 4, 1); break;
+        case 59: DMF_BK_FUSE_S20(28, 32, 4, 1); break;
+        case 60: DMF_BK_FUSE_S20(32, 32, 4, 1); break;
+        case 61: DMF_BK_FUSE_S20(24, 16, 4, 1); break;
+        case 62: DMF_BK_FUSE_S20(24, 32, 3, 1); break;
+        case 63: DMF_BK_FUSE_S20(24, 32, 5, 1); break;
         default: DMF_BK_FUSE_S20(24, 32, 4, 1); break;  // 0, 57
       }
 #undef DMF_BK_FUSE
@@ -2298,6 +2298,12 @@ static const char* variant_name(int v) {
     case 54: return "dmf::k_bk_fuse_s<24, 64, 4, 1, false>";
     case 55: return "dmf::k_bk_fuse_s<20, 32, 4, 1, false>";
     case 56: return "dmf::k_bk_fuse_s<28, 32, 4, 1, false>";
+    case 58: return "dmf::k_bk_fuse_s<20, 32, 4, 1, false, true>";
+    case 59: return "dmf::k_bk_fuse_s<28, 32, 4, 1, false, true>";
+    case 60: return "dmf::k_bk_fuse_s<32, 32, 4, 1, false, true>";
+    case 61: return "dmf::k_bk_fuse_s<24, 16, 4, 1, false, true>";
+    case 62: return "dmf::k_bk_fuse_s<24, 32, 3, 1, false, true>";
+    case 63: return "dmf::k_bk_fuse_s<24, 32, 5, 1, false, true>";
     case 53: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false>";
     default: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true>";  // 0, 57; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }

@@ -241,16 +241,20 @@ __device__ inline void rev_sample(const float cen[3], const float v[3], int dept
   else march_sample(cen, v, depth, p);
 }
 
-// getVoxel of a point inside the volume: the certified float bins (dmf_geom.hpp
-// bin_axis_f), the double bins only for lanes whose estimate is within eps of a boundary
-// (the branch is skipped when no lane needs it).
+// getVoxel of a point inside the volume in the reference's double arithmetic (bin_axis).
+// (The certified float bins of dmf_geom.hpp bin_axis_f, exact by tools/binning_selftest.cpp,
+// measured SLOWER in the reverse march: 8.35 vs 7.57 ms per 128-pose batch -- gfx950 runs
+// the fp64 add / mul / floor / converts at the non-packed fp32 rate, and the certification
+// adds instructions and a branch; kept as k_reverse_q mode 2 for A/B.)
 __device__ inline void bin_point(const Geom& g, const float p[3], int& a, int& b, int& c) {
+  a = bin_axis(g, 0, p[0]);
+  b = bin_axis(g, 1, p[1]);
+  c = bin_axis(g, 2, p[2]);
+}
+
+__device__ inline void bin_point_f(const Geom& g, const float p[3], int& a, int& b, int& c) {
   const int ok = (int)bin_axis_f(g, 0, p[0], &a) & (int)bin_axis_f(g, 1, p[1], &b) & (int)bin_axis_f(g, 2, p[2], &c);
-  if (!(g.fbin && ok)) {
-    a = bin_axis(g, 0, p[0]);
-    b = bin_axis(g, 1, p[1]);
-    c = bin_axis(g, 2, p[2]);
-  }
+  if (!(g.fbin && ok)) bin_point(g, p, a, b, c);
 }
 
 // One sample of the reverse march (RayTracingEngine.hpp:172-200): 0 = continue,
@@ -265,13 +269,8 @@ __device__ inline void bin_point(const Geom& g, const float p[3], int& a, int& b
 // from the cube faces and verified by evaluating sample j exactly.
 template <bool kFBin>
 __device__ inline void bin_point_t(const Geom& g, const float p[3], int& a, int& b, int& c) {
-  if (kFBin) {
-    bin_point(g, p, a, b, c);
-  } else {
-    a = bin_axis(g, 0, p[0]);
-    b = bin_axis(g, 1, p[1]);
-    c = bin_axis(g, 2, p[2]);
-  }
+  if (kFBin) bin_point_f(g, p, a, b, c);
+  else bin_point(g, p, a, b, c);
 }
 
 template <bool kFastDiv, bool kFBin>
@@ -329,8 +328,9 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
 }
 
 // kMode (A/B): bit 0 = the guard-free division for waves that allow it, bit 1 = the
-// certified float bins (3 = both, the default)
-template <bool kEnum, int kItems, int kRefill, int kBurst, int kMode = 3>
+// certified float bins.  Measured per 128-pose batch (414k voxels): 0 7.57-7.61 ms,
+// 1 7.55-7.59, 2 8.35, 3 8.73: the default is 0.
+template <bool kEnum, int kItems, int kRefill, int kBurst, int kMode = 0>
 __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses,
                                                    int64_t nelem, EnumList el, int depth0, int max_steps, float dstar,
                                                    int viz, int normal_test, uint64_t* __restrict__ vis_mask,
@@ -652,7 +652,7 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
         case 6: if (enumerate) DMF_REVQX(true, 0, 1024, 16, 8); else DMF_REVQX(false, 1, 1024, 16, 8); break;
         case 7: if (enumerate) DMF_REVQX(true, 0, 256, 16, 4); else DMF_REVQX(false, 1, 256, 16, 4); break;
         case 8: if (enumerate) DMF_REVQX(true, 0, 512, 24, 4); else DMF_REVQX(false, 1, 512, 24, 4); break;
-        case 9: if (enumerate) DMF_REVQM(true, 0, 0); else DMF_REVQM(false, 1, 0); break;    // round-2 arithmetic
+        case 9: if (enumerate) DMF_REVQM(true, 0, 3); else DMF_REVQM(false, 1, 3); break;    // fast division + float bins
         case 10: if (enumerate) DMF_REVQM(true, 0, 2); else DMF_REVQM(false, 1, 2); break;   // float bins only
         case 11: if (enumerate) DMF_REVQM(true, 0, 1); else DMF_REVQM(false, 1, 1); break;   // fast division only
         default: if (enumerate) DMF_REVQ(true, 0); else DMF_REVQ(false, 1); break;
