@@ -558,7 +558,7 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses_h,
     V = vol.info()["num_occupied"]
     words = (V + 63) // 64
     good = torch.empty(P * words, dtype=torch.int64, device=dev)
-    st = torch.zeros(2, dtype=torch.int64, device=dev)
+    st = torch.zeros(16, dtype=torch.int64, device=dev)  # [samples, rays] (+ diagnostic-build counters)
 
     def run():
         _lib.check(L.dmf_reverse_visibility_device(vol._h, C.addressof(cam), d_poses.data_ptr(), P, 0, None,
@@ -653,7 +653,13 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses_h,
         "cpu_baseline": rev_cpu,
         "roofline": None,  # issue-bound pricing from the PMC passes (attach_pmc); the march reads an
                            # L2-resident bitmask, so SURVEY 8d's 2 B per sample is reported, not a bound:
-        "algorithmic_bytes_per_launch": bytes_launch}}
+        "algorithmic_bytes_per_launch": bytes_launch,
+        **({"diagnostics": dict(zip(REV_DIAG, (float(x) for x in s[2:2 + len(REV_DIAG)])))} if s[2:].any() else {})}}
+
+
+# counters 2.. of the DMF_EXP_STATS library's reverse march (per batch; dmf_trace.hip DMF_RS)
+REV_DIAG = ["centroid_cell_samples", "stepped_samples", "jump_tries", "jumps", "jumped_samples", "collided",
+            "exited", "marched_rays", "burst_iterations", "burst_active_lanes", "jump_too_short"]
 
 
 if __name__ == "__main__":

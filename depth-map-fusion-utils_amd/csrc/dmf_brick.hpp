@@ -130,6 +130,60 @@ __host__ __device__ inline void counts_at(const QRay& r, int a, int32_t k, int32
   for (int b = 0; b < 3; ++b) c[b] = (b == a) ? k + 1 : count_at(r, b, a, Ha);
 }
 
+// counts_at for an axis a that differs between the lanes of a wave (pass B's boundary
+// events): one straight code path of selects.  counts_at's constant-axis branches run
+// once per distinct axis among a wave's lanes; here the two other axes (ascending:
+// o1 = a == 0 ? 1 : 0, o2 = a == 2 ? 1 : 2) are picked and counted by the same code, with
+// count_at's tie rule as a bias (b > a: X - 1).  The quotient's remainder is taken in 32
+// bits: with q within 1 of floor(X / Y) it lies in (-Y, 2Y), |.| < 2^28 (Y = 2Q|dq_a| <
+// 2^27), so the wrapped difference of the low words is exact.  A non-moving axis (n = 0)
+// is clamped to 0 whatever its quotient.  Checked against counts_at by the brick self-test.
+__host__ __device__ inline int32_t quot_small32(int64_t X, int32_t Y) {
+  const float xf = (float)(int32_t)(X >> 20) * 1048576.0f + (float)(int32_t)(X & 0xfffff);
+  const float yf = (float)Y;
+#if defined(__HIP_DEVICE_COMPILE__)
+  int32_t q = (int32_t)(xf * __builtin_amdgcn_rcpf(yf));
+#else
+  int32_t q = (int32_t)(xf / yf);
+#endif
+  const int32_t rm = (int32_t)((uint32_t)X - (uint32_t)q * (uint32_t)Y);
+  q += rm < 0 ? -1 : (rm >= Y ? 1 : 0);
+  return q;
+}
+
+// The value of x, opaque to the optimiser: a select between struct fields must stay a
+// register select (folded into a select of addresses, the fields go to scratch memory).
+__host__ __device__ inline int32_t opaque(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+
+__host__ __device__ inline int32_t sel3(bool a0, bool a1, int32_t v0, int32_t v1, int32_t v2) {
+  return a0 ? opaque(v0) : (a1 ? opaque(v1) : opaque(v2));
+}
+
+__host__ __device__ inline void counts_at_sel(const QRay& r, int a, int32_t k, int32_t c[3]) {
+  const bool a0 = a == 0, a1 = a == 1, a2 = a == 2;
+  const int32_t ha = sel3(a0, a1, r.h0[0], r.h0[1], r.h0[2]);
+  const int32_t da = sel3(a0, a1, r.adq[0], r.adq[1], r.adq[2]);
+  const int64_t Ha = (int64_t)ha + 2 * kQ * (int64_t)k;
+  const int32_t Y = (int32_t)(2 * kQ) * da;
+  auto cnt = [&](int32_t adb, int32_t hb, int32_t nb, bool after) -> int32_t {
+    const int64_t X = Ha * (int64_t)adb - (int64_t)hb * (int64_t)da - (after ? 1 : 0);
+    const int32_t q = quot_small32(X < 0 ? 0 : X, Y) + 1;
+    return X < 0 ? 0 : (q < 0 ? 0 : (q > nb ? nb : q));
+  };
+  const int32_t c1 = cnt(a0 ? opaque(r.adq[1]) : opaque(r.adq[0]), a0 ? opaque(r.h0[1]) : opaque(r.h0[0]),
+                         a0 ? opaque(r.n[1]) : opaque(r.n[0]), a0);
+  const int32_t c2 = cnt(a2 ? opaque(r.adq[1]) : opaque(r.adq[2]), a2 ? opaque(r.h0[1]) : opaque(r.h0[2]),
+                         a2 ? opaque(r.n[1]) : opaque(r.n[2]), !a2);
+  c[0] = a0 ? k + 1 : c1;
+  c[1] = a1 ? k + 1 : (a0 ? c1 : c2);
+  c[2] = a2 ? k + 1 : c2;
+}
+
 // One (ray, brick) pair: where the fine walk enters brick (bx, by, bz), how many
 // cells it visits there, and whether the last of them is the ray's end cell.
 struct Pair {

@@ -1109,7 +1109,9 @@ __device__ inline uint32_t bk_e30(int32_t e) {
 #endif
 // R20 (SLAB only; the default): the 20-byte record of dmf_brick.hpp pack20 (beta state,
 // pa = words 0-3, pb = word 4 as uint32) instead of the 24-byte one.
-template <bool SLAB, bool AGG = true, bool R20 = false>
+// SEL: boundary-event counts by bk::counts_at_sel (one code path for every crossing axis;
+// counts_at's per-axis branches run once per distinct axis among a wave's lanes).
+template <bool SLAB, bool AGG = true, bool R20 = false, bool SEL = false>
 __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pairs(int packets_pose, int wg_pose, int span,
                                                          BkGeom bg, const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
@@ -1229,10 +1231,17 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
     bk_coarse(bg, R, [&](int b, int a, int bx, int by, int bz) {
       if (a >= 0) {
         int32_t c[3];
-        // constant axis in each call: no dynamically indexed (scratch) arrays
-        if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
-        else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
-        else bk::counts_at(R, 2, boundary_k(2, bz), c);
+        if constexpr (SEL) {
+          const int32_t sa = bk::sel3(a == 0, a == 1, R.st[0], R.st[1], R.st[2]);
+          const int32_t ca = bk::sel3(a == 0, a == 1, R.cs[0], R.cs[1], R.cs[2]);
+          const int32_t nb = (a == 0 ? bx : (a == 1 ? by : bz)) << bk::kLog;
+          bk::counts_at_sel(R, a, sa > 0 ? nb - ca - 1 : ca - nb - bk::kB, c);
+        } else {
+          // constant axis in each call: no dynamically indexed (scratch) arrays
+          if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
+          else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
+          else bk::counts_at(R, 2, boundary_k(2, bz), c);
+        }
         put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
         cur = entry(c);
         idx = c[0] + c[1] + c[2];
@@ -1544,7 +1553,10 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
 // are idle, from per-slot records prefetched one refill ahead.
 // R20: 20-byte records (dmf_brick.hpp pack20): the walk runs on the beta state with
 // increments |dq| (exactly the same decisions as b with K = 512 |dq|).
-template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, bool BL = false, bool R20 = false>
+// POOL (20-B records, NSLOT 1): a wave takes pair indices from its own pool of 64, grabbed
+// from the part's LDS counter one refill AHEAD (the grab's latency, which waits for the
+// wave's queued walk adds, hides behind the next walk block instead of stalling the refill).
+template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, bool BL = false, bool R20 = false, bool POOL = false>
 __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, const uint4* __restrict__ pa,
                                                           const void* __restrict__ pbv,
                                                           const uint32_t* __restrict__ off,
@@ -1686,9 +1698,52 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       atomicAdd(&box[ra.w >> 16], (rb.y >> 26) & 1u ? 0x10000u : 1u);
     };
     bool more = true;
+    // POOL: this wave's index pool [pl_lo, pl_hi) and the grab in flight (lane 0's return)
+    constexpr uint32_t kGrab = 64;
+    static_assert(!POOL || (NSLOT == 1 && R20), "index pool: one slot, 20-B records");
+    uint32_t pl_lo = 0, pl_hi = 0, pend = 0;
+    bool in_flight = false;
+    auto grab = [&]() {
+      uint32_t b0 = 0;
+      if (l == 0) b0 = atomicAdd(&sh[1], kGrab);
+      pend = b0;
+      in_flight = true;
+    };
+    if constexpr (POOL) grab();
+    auto prefetch_pool = [&](uint64_t need) {
+      const uint32_t nn = (uint32_t)__builtin_popcountll(need), left = pl_hi - pl_lo;
+      uint32_t nbase = 0, nb = 0;
+      if (left < nn && in_flight) {  // the grab issued one refill ago
+        nbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+        nb = kGrab;
+        in_flight = false;
+      }
+      if ((need >> l) & 1ull) {
+        const uint32_t i = (uint32_t)lane_prefix(need);
+        const uint32_t k = i < left ? pl_lo + i : (i - left < nb ? nbase + (i - left) : 0xffffffffu);
+        fok[0] = k < n;
+        const uint32_t o = bk_order<S_ORDER>(k, n);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_a, o * 16u, 0, 0);
+        ca[0] = make_uint4(v[0], v[1], v[2], v[3]);
+        cb[0].x = __builtin_amdgcn_raw_buffer_load_b32(rs_w, o * 4u, 0, 0);
+      }
+      if (nn <= left) {
+        pl_lo += nn;
+      } else {
+        pl_lo = nbase + (nn - left);
+        pl_hi = nbase + nb;
+        if (nb == 0) pl_lo = pl_hi = n;  // nothing left to hand out
+      }
+      if (pl_lo >= n) more = false;  // every later grab lies past n too
+      else if (!in_flight) grab();     // keep one grab in flight
+    };
     // lanes in need[q] take the next pair indices (one LDS counter atomic for all slots)
     // and load their records into slot q
     auto prefetch = [&](const uint64_t* need) {
+      if constexpr (POOL) {
+        prefetch_pool(need[0]);
+        return;
+      }
       uint32_t nn = 0;
 #pragma unroll
       for (int q = 0; q < NSLOT; ++q) nn += (uint32_t)__builtin_popcountll(need[q]);
@@ -1951,7 +2006,7 @@ static int fuse_variant() {
 }
 constexpr int kVariantBrick = 40;
 constexpr int kVariantSlab = 44;  // 44..53: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
-constexpr int kVariantLast = 63;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
+constexpr int kVariantLast = 65;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
 constexpr int kVariantRec20 = 57;  // the default: 20-B pair records (beta state, dmf_brick.hpp pack20)
 // 57-63: 20-B records (57 = the default <24, 32, 4>; 58-63 refill / spread / unroll A/B)
 static bool is_rec20_variant(int v) { return v == 0 || (v >= kVariantRec20 && v <= kVariantLast); }
@@ -2078,6 +2133,8 @@ static int bk_attributes() {
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set.store(true);
   }
   return DMF_OK;
@@ -2176,6 +2233,8 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                      (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j, b.pra, b.prb)
       if (fv == 48)  // wave-aggregated slot atomics (the previous default)
         DMF_BK_PAIRS(true, true);
+      else if (fv == 65)
+        DMF_BK_PAIRS(true, false, true, true);
       else if (is_rec20_variant(fv))
         DMF_BK_PAIRS(true, false, true);
       else if (is_slab_variant(fv))
@@ -2224,6 +2283,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         case 61: DMF_BK_FUSE_S20(24, 16, 4, 1); break;
         case 62: DMF_BK_FUSE_S20(24, 32, 3, 1); break;
         case 63: DMF_BK_FUSE_S20(24, 32, 5, 1); break;
+        case 64:
+          hipLaunchKernelGGL((k_bk_fuse_s<24, 32, 4, 1, false, true, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g,
+                             bg, (const uint4*)b.pra, (const void*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
+                             (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st);
+          break;
         default: DMF_BK_FUSE_S20(24, 32, 4, 1); break;  // 0, 57
       }
 #undef DMF_BK_FUSE
@@ -2304,6 +2368,7 @@ static const char* variant_name(int v) {
     case 61: return "dmf::k_bk_fuse_s<24, 16, 4, 1, false, true>";
     case 62: return "dmf::k_bk_fuse_s<24, 32, 3, 1, false, true>";
     case 63: return "dmf::k_bk_fuse_s<24, 32, 5, 1, false, true>";
+    case 64: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true, true>";
     case 53: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false>";
     default: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true>";  // 0, 57; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }

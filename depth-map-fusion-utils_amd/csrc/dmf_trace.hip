@@ -273,9 +273,18 @@ __device__ inline void bin_point_t(const Geom& g, const float p[3], int& a, int&
   else bin_point(g, p, a, b, c);
 }
 
+// Diagnostic build (DMF_EXP_STATS): sample categories into stats[2..12] (tools/gpu_rev_stats.sh)
+#if defined(DMF_EXP_STATS)
+#define DMF_RS(i, x) (rst[(i) - 2] += (unsigned long long)(x))
+#else
+#define DMF_RS(i, x) ((void)0)
+#endif
+constexpr int kRevStatN = 11;
+
 template <bool kFastDiv, bool kFBin>
 __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int depth0, int max_steps,
-                               int64_t& samples) {
+                               int64_t& samples, unsigned long long* rst) {
+  (void)rst;
   if (L.s >= max_steps) return 3;
   float p[3];
   rev_sample<kFastDiv>(L.cen, L.v, depth0 + L.s, p);
@@ -283,7 +292,7 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   if (!valid_points_f(g, p)) return 2;
   int a, b, c;
   bin_point_t<kFBin>(g, p, a, b, c);
-  if (a == L.cx && b == L.cy && c == L.cz) { ++L.s; return 0; }
+  if (a == L.cx && b == L.cy && c == L.cz) { DMF_RS(2, 1); ++L.s; return 0; }
   if (!valid_coords(g, a, b, c)) return 2;
   const uint32_t ob = occ_bit(g, a, b, c);
   if ((ob >> 5) != L.occi) { L.occi = ob >> 5; L.occw = vd.occ[L.occi]; }
@@ -311,18 +320,24 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
         float q[3];
         rev_sample<kFastDiv>(L.cen, L.v, depth0 + j, q);
         ++samples;
+        DMF_RS(4, 1);
         if (valid_points_f(g, q)) {
           int qa, qb, qc;
           bin_point_t<kFBin>(g, q, qa, qb, qc);
           if (qa >= clo[0] && qa < chi[0] && qb >= clo[1] && qb < chi[1] && qc >= clo[2] && qc < chi[2]) {
+            DMF_RS(5, 1);
+            DMF_RS(6, j - L.s);
             L.s = j + 1;  // samples s+1 .. j lie inside the empty cube
             return 0;
           }
         }
+      } else {
+        DMF_RS(12, 1);
       }
     }
     L.known_full = bl;  // occupied brick, or the jump failed: step through it
   }
+  DMF_RS(3, 1);
   ++L.s;
   return 0;
 }
@@ -348,6 +363,7 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
   const PoseX& T = poses[p];
   int64_t samples = 0, rays = 0;
   unsigned long long ncap = 0;
+  unsigned long long rst[kRevStatN] = {};
   bool any_vis = false;
   RevLane L;
   L.item = -1;
@@ -408,6 +424,7 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
             L.item = it;
             L.slot = slot;
             L.tz = t[2];
+            DMF_RS(9, 1);
           }
         }
       }
@@ -424,17 +441,21 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
     if ((kMode & 1) && __builtin_amdgcn_ballot_w64(L.item >= 0 && !L.fdiv) == 0) {
 #pragma unroll 1
       for (int b = 0; b < kBurst; ++b) {
-        if (L.item >= 0 && st == 0) st = rev_step<true, kFB>(g, vd, L, depth0, max_steps, samples);
+        if (L.item >= 0 && st == 0) st = rev_step<true, kFB>(g, vd, L, depth0, max_steps, samples, rst);
         if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
       }
     } else {
 #pragma unroll 1
       for (int b = 0; b < kBurst; ++b) {
-        if (L.item >= 0 && st == 0) st = rev_step<false, kFB>(g, vd, L, depth0, max_steps, samples);
+        DMF_RS(10, l == 0);
+        DMF_RS(11, L.item >= 0 && st == 0);
+        if (L.item >= 0 && st == 0) st = rev_step<false, kFB>(g, vd, L, depth0, max_steps, samples, rst);
         if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
       }
     }
     if (L.item >= 0 && st != 0) {
+      DMF_RS(7, st == 1);
+      DMF_RS(8, st == 2);
       if (st == 3) ++ncap;
       if (st == 2) {
         any_vis = true;
@@ -477,6 +498,10 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
   if (stats) {
     wave_add_u64(&stats[0], (unsigned long long)samples);
     wave_add_u64(&stats[1], (unsigned long long)rays);
+#if defined(DMF_EXP_STATS)
+#pragma unroll
+    for (int i = 0; i < kRevStatN; ++i) wave_add_u64(&stats[2 + i], rst[i]);
+#endif
   }
 }
 
@@ -668,7 +693,11 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
 #undef DMF_REVQM
     DMF_LAUNCH_CHECK();
   }
+#if defined(DMF_EXP_STATS)
+  if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 2 + kRevStatN));
+#else
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 2));
+#endif
   if (found_h) {
     found_h->assign(P, 0);
     unsigned long long hzh = 0;

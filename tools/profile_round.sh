@@ -17,5 +17,20 @@ for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_su
   i=$((i+1))
   timeout -k 10 400 rocprofv3 --pmc $pmc --output-format csv -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-frames 0 --no-secondary --pmc off ${BENCHARGS} > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || exit 2
 done
+# extra counter groups (";"-separated in $EXTRA_PMC); counters the box does not list are dropped
+if [ -n "$EXTRA_PMC" ]; then
+  timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+  IFS=';' read -ra GROUPS_X <<< "$EXTRA_PMC"
+  for grp in "${GROUPS_X[@]}"; do
+    keep=""
+    for c in $grp; do
+      base=${c%_sum}
+      if grep -qw -- "$base" "$OUT/counters.txt"; then keep="$keep $c"; else echo "counter $c not listed: dropped"; fi
+    done
+    [ -z "$keep" ] && continue
+    i=$((i+1))
+    timeout -s KILL 120 rocprofv3 --pmc $keep --output-format csv -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-frames 0 --no-secondary --pmc off ${BENCHARGS} > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || exit 2
+  done
+fi
 python3 tools/pmc_summary.py "$OUT" "profiles/$TAG" || exit 3
 echo "profile $TAG collected"
