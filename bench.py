@@ -400,10 +400,10 @@ def main():
         ms = elapsed / args.steps * 1e3
         kname = L.dmf_fuse_kernel().decode()
         if kname.startswith("dmf::k_bk_fuse"):
-            # brick-owned pipeline: kernel_ms spans all four launches
-            pipeline = ["dmf::k_bk_rays", "dmf::k_bk_scan",
-                        "dmf::k_bk_pairs<true, false>" if kname.startswith("dmf::k_bk_fuse_s") else "dmf::k_bk_pairs<false, true>",
-                        kname]
+            # brick-owned pipeline: kernel_ms spans every launch of the call
+            # (A, the device-side batch cut, and per pose batch S, B, F)
+            pipeline = ["dmf::k_bk_rays", "dmf::k_bk_batches", "dmf::k_bk_batch_counts", "dmf::k_bk_scan",
+                        "dmf::k_bk_pairs", kname]
             diagnostics = {"pairs": int(st[4]) // args.steps, "parts": int(st[5]) // args.steps,
                            "flushed_cells": int(st[6]) // args.steps,
                            "updates_per_pair": float(st[0]) / max(float(st[4]), 1.0),

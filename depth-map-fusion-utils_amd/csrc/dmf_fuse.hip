@@ -1111,7 +1111,12 @@ __device__ inline uint32_t bk_e30(int32_t e) {
 // pa = words 0-3, pb = word 4 as uint32) instead of the 24-byte one.
 // SEL: boundary-event counts by bk::counts_at_sel (one code path for every crossing axis;
 // counts_at's per-axis branches run once per distinct axis among a wave's lanes).
-template <bool SLAB, bool AGG = true, bool R20 = false, bool SEL = false>
+// RUN (with SEL): slots by runs of adjacent lanes entering the same brick -- one LDS atomic
+// per run, by its first lane (same-address atomics of one instruction serialise: pass B's
+// LDS bank-conflict cycles were ~26 % of its time).  The coarse loop runs wave-uniform with
+// per-lane liveness so that every lane is active where the run's base is fetched from its
+// first lane (DPP wave_shr for the neighbour's brick, ds_bpermute for the base).
+template <bool SLAB, bool AGG = true, bool R20 = false, bool SEL = false, bool RUN = false>
 __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pairs(int packets_pose, int wg_pose, int span,
                                                          BkGeom bg, const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
@@ -1144,7 +1149,8 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
     const ulonglong2 rec = rnext;
     if (pk + nw < pk1) rnext = rays[(pk + nw) * 64 + l];
-    if (!(rec.y >> 63)) continue;
+    const bool valid = (rec.y >> 63) != 0;
+    if (!RUN && !valid) continue;
     bk::QRay R;
     bk::decode_ray(rec.x, rec.y, R);
     const uint32_t K0 = (uint32_t)(2 * bk::kQ) * (uint32_t)R.adq[0], K1 = (uint32_t)(2 * bk::kQ) * (uint32_t)R.adq[1],
@@ -1196,8 +1202,12 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
         uint32_t w[5];
         bk::pack20((int32_t)e.x, (int32_t)e.y, (int32_t)e.z, aM, a1, a2, e.w, last, steps, signs >> 22, (uint32_t)M,
                    ends, w);
+#if defined(DMF_DIAG_B_NOSTORE)  // diagnostic build (wrong results): pass B without its record stores
+        if ((w[0] ^ w[1] ^ w[2] ^ w[3] ^ w[4] ^ slot) == 0x9e3779b9u) pw[0] = 0;  // keep the record live
+#else
         pa[slot] = make_uint4(w[0], w[1], w[2], w[3]);
         pw[slot] = w[4];
+#endif
       } else {
         e.x = bk_e30((int32_t)e.x) | (steps & 3u) << 30;
         e.y = bk_e30((int32_t)e.y) | ((steps >> 2) & 3u) << 30;
@@ -1227,6 +1237,65 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
       const int32_t cin[3] = {ci0, ci1, ci2}, cL[3] = {L0, L1, L2};
       return bk::slab_rcode(M, sb1, sb2, KM, Km1, Km2, cin, cL);
     };
+    if constexpr (RUN) {
+      // run-aggregated slot take (wave-uniform): the run of live lanes starting at this
+      // lane's run leader adds its length once; this lane's slot = the leader's old + rank
+      uint32_t old = 0;
+      int start = 0, rank = 0;
+      auto take = [&](bool live, int b) {
+        const uint64_t act = __builtin_amdgcn_ballot_w64(live);
+        const int pb = __builtin_amdgcn_update_dpp(b, b, 0x138, 0xf, 0xf, false);  // wave_shr:1
+        const bool lead = live && (l == 0 || !((act >> (l - 1)) & 1ull) || pb != b);
+        const uint64_t leaders = __builtin_amdgcn_ballot_w64(lead);
+        const uint64_t stops = leaders | ~act;
+        const uint64_t above = l == 63 ? 0ull : (stops >> (l + 1)) << (l + 1);
+        const int end = above ? __builtin_ctzll(above) : 64;
+        if (lead) old = atomicAdd(&hist[b], (uint32_t)(end - l));
+        const uint64_t upto = leaders & (~0ull >> (63 - l));
+        start = upto ? 63 - __builtin_clzll(upto) : l;
+        rank = l - start;
+      };
+      auto slot_of = [&]() {
+        return (uint32_t)__builtin_amdgcn_ds_bpermute(start << 2, (int)old) + (uint32_t)rank;
+      };
+      int bx = R.cs[0] >> bk::kLog, by = R.cs[1] >> bk::kLog, bz = R.cs[2] >> bk::kLog;
+      bk::Coarse cw;
+      bk::coarse_init(R, cw);
+      const int total = valid ? cw.total : -1;
+      take(valid, bk_index(bg, bx, by, bz));
+      // iteration t: boundary t for live lanes (t < total); at t == total the lane stores its
+      // last pair, with the slot of its last take (every take overwrites the run bases, so
+      // each slot is fetched in the iteration right after its take)
+      for (int t = 0;; ++t) {
+        const bool live = t < total, fin = t == total;
+        if (__builtin_amdgcn_ballot_w64(live || fin) == 0) break;
+        int a = 0;
+        int32_t c[3] = {0, 0, 0};
+        if (live) {
+          a = bk::coarse_next(cw);
+          bx += a == 0 ? R.st[0] : 0;
+          by += a == 1 ? R.st[1] : 0;
+          bz += a == 2 ? R.st[2] : 0;
+          const int32_t sa = bk::sel3(a == 0, a == 1, R.st[0], R.st[1], R.st[2]);
+          const int32_t ca = bk::sel3(a == 0, a == 1, R.cs[0], R.cs[1], R.cs[2]);
+          const int32_t nb = (a == 0 ? bx : (a == 1 ? by : bz)) << bk::kLog;
+          bk::counts_at_sel(R, a, sa > 0 ? nb - ca - 1 : ca - nb - bk::kB, c);
+        }
+        const uint32_t slot = slot_of();  // every lane active: the leaders' bases are readable
+        if (live) {
+          put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
+          cur = entry(c);
+          idx = c[0] + c[1] + c[2];
+          ci0 = c[0];
+          ci1 = c[1];
+          ci2 = c[2];
+        } else if (fin) {
+          put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
+        }
+        take(live, bk_index(bg, bx, by, bz));
+      }
+      continue;
+    }
     uint32_t slot = 0;
     bk_coarse(bg, R, [&](int b, int a, int bx, int by, int bz) {
       if (a >= 0) {
@@ -1249,7 +1318,11 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
         ci1 = c[1];
         ci2 = c[2];
       }
+#if defined(DMF_DIAG_B_NOATOMIC)  // diagnostic build (wrong results): no slot atomics
+      slot = hist[b];  // (every lane of the workgroup writes the range start: no out-of-range store)
+#else
       slot = AGG ? hist_take_agg(hist, b) : atomicAdd(&hist[b], 1u);
+#endif
     });
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }
@@ -2006,7 +2079,7 @@ static int fuse_variant() {
 }
 constexpr int kVariantBrick = 40;
 constexpr int kVariantSlab = 44;  // 44..53: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
-constexpr int kVariantLast = 65;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
+constexpr int kVariantLast = 66;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
 constexpr int kVariantRec20 = 57;  // the default: 20-B pair records (beta state, dmf_brick.hpp pack20)
 // 57-63: 20-B records (57 = the default <24, 32, 4>; 58-63 refill / spread / unroll A/B)
 static bool is_rec20_variant(int v) { return v == 0 || (v >= kVariantRec20 && v <= kVariantLast); }
@@ -2135,6 +2208,8 @@ static int bk_attributes() {
                                 lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false, true, true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false, true, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set.store(true);
   }
   return DMF_OK;
@@ -2235,6 +2310,8 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         DMF_BK_PAIRS(true, true);
       else if (fv == 65)
         DMF_BK_PAIRS(true, false, true, true);
+      else if (fv == 66)
+        DMF_BK_PAIRS(true, false, true, true, true);
       else if (is_rec20_variant(fv))
         DMF_BK_PAIRS(true, false, true);
       else if (is_slab_variant(fv))

@@ -211,6 +211,9 @@ struct RevLane {
   int32_t slot;
   float tz;             // camera-frame z of the centroid (z-range test)
   uint32_t occi, occw;  // cached occupancy word
+  bool pend;            // kDefer: sample s is an unverified jump landing
+  int ps, pR, pb[3];    // its origin sample, cube radius and origin brick
+  uint32_t pbl;         // the origin brick's index
 };
 
 __device__ inline bool valid_points_f(const Geom& g, const float p[3]) {
@@ -281,7 +284,14 @@ __device__ inline void bin_point_t(const Geom& g, const float p[3], int& a, int&
 #endif
 constexpr int kRevStatN = 11;
 
-template <bool kFastDiv, bool kFBin>
+// kDefer: a jump to sample j is not verified in the call that finds it.  The call sets
+// L.s = j and records the cube (origin brick, radius) and the sample it jumped from; the
+// next call evaluates sample j as its ordinary sample and accepts the jump if j lies in
+// the cube (then j is inside the volume, empty and not the centroid's cell, and the brick
+// logic continues from j at once), else it steps on from the origin sample + 1 as the
+// plain march would.  Every call is then one sample evaluation (the landing sample is no
+// longer a second one inside the divergent jump branch).
+template <bool kFastDiv, bool kFBin, bool kDefer = false>
 __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int depth0, int max_steps,
                                int64_t& samples, unsigned long long* rst) {
   (void)rst;
@@ -289,14 +299,33 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   float p[3];
   rev_sample<kFastDiv>(L.cen, L.v, depth0 + L.s, p);
   ++samples;
-  if (!valid_points_f(g, p)) return 2;
   int a, b, c;
-  bin_point_t<kFBin>(g, p, a, b, c);
-  if (a == L.cx && b == L.cy && c == L.cz) { DMF_RS(2, 1); ++L.s; return 0; }
-  if (!valid_coords(g, a, b, c)) return 2;
-  const uint32_t ob = occ_bit(g, a, b, c);
-  if ((ob >> 5) != L.occi) { L.occi = ob >> 5; L.occw = vd.occ[L.occi]; }
-  if ((L.occw >> (ob & 31)) & 1u) return 1;
+  if (kDefer && L.pend) {
+    L.pend = false;
+    bool in = valid_points_f(g, p);
+    if (in) {
+      bin_point_t<kFBin>(g, p, a, b, c);
+      const int R = L.pR;
+      in = a >= 0 && b >= 0 && c >= 0 && a < g.n[0] && b < g.n[1] && c < g.n[2] &&
+           abs((a >> vd.bsh) - L.pb[0]) <= R && abs((b >> vd.bsh) - L.pb[1]) <= R && abs((c >> vd.bsh) - L.pb[2]) <= R;
+    }
+    if (!in) {  // jump rejected: step on from the sample after its origin
+      DMF_RS(12, 1);
+      L.known_full = L.pbl;
+      L.s = L.ps + 1;
+      return 0;
+    }
+    DMF_RS(5, 1);
+    DMF_RS(6, L.s - L.ps - 1);
+  } else {
+    if (!valid_points_f(g, p)) return 2;
+    bin_point_t<kFBin>(g, p, a, b, c);
+    if (a == L.cx && b == L.cy && c == L.cz) { DMF_RS(2, 1); ++L.s; return 0; }
+    if (!valid_coords(g, a, b, c)) return 2;
+    const uint32_t ob = occ_bit(g, a, b, c);
+    if ((ob >> 5) != L.occi) { L.occi = ob >> 5; L.occw = vd.occ[L.occi]; }
+    if ((L.occw >> (ob & 31)) & 1u) return 1;
+  }
   const int ba = a >> vd.bsh, bb = b >> vd.bsh, bc = c >> vd.bsh;
   const uint32_t bl = ((uint32_t)ba * (uint32_t)vd.nb[1] + (uint32_t)bb) * (uint32_t)vd.nb[2] + (uint32_t)bc;
   if (bl != L.known_full) {
@@ -317,23 +346,35 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
       const float jf = floorf(fdmax) - (float)depth0 - 2.0f;
       if (jf > (float)(L.s + 1) && jf < (float)max_steps) {
         const int j = (int)jf;
-        float q[3];
-        rev_sample<kFastDiv>(L.cen, L.v, depth0 + j, q);
-        ++samples;
         DMF_RS(4, 1);
-        if (valid_points_f(g, q)) {
-          int qa, qb, qc;
-          bin_point_t<kFBin>(g, q, qa, qb, qc);
-          if (qa >= clo[0] && qa < chi[0] && qb >= clo[1] && qb < chi[1] && qc >= clo[2] && qc < chi[2]) {
-            DMF_RS(5, 1);
-            DMF_RS(6, j - L.s);
-            L.s = j + 1;  // samples s+1 .. j lie inside the empty cube
-            return 0;
+        if constexpr (kDefer) {
+          L.pend = true;
+          L.ps = L.s;
+          L.pbl = bl;
+          L.pR = R;
+          L.pb[0] = ba;
+          L.pb[1] = bb;
+          L.pb[2] = bc;
+          L.s = j;
+          return 0;
+        } else {
+          float q[3];
+          rev_sample<kFastDiv>(L.cen, L.v, depth0 + j, q);
+          ++samples;
+          if (valid_points_f(g, q)) {
+            int qa, qb, qc;
+            bin_point_t<kFBin>(g, q, qa, qb, qc);
+            if (qa >= clo[0] && qa < chi[0] && qb >= clo[1] && qb < chi[1] && qc >= clo[2] && qc < chi[2]) {
+              DMF_RS(5, 1);
+              DMF_RS(6, j - L.s);
+              L.s = j + 1;  // samples s+1 .. j lie inside the empty cube
+              return 0;
+            }
           }
         }
-      } else {
-        DMF_RS(12, 1);
       }
+    } else {
+      DMF_RS(12, 1);
     }
     L.known_full = bl;  // occupied brick, or the jump failed: step through it
   }
@@ -421,6 +462,7 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
             L.s = 0;
             L.known_full = 0xffffffffu;
             L.occi = 0xffffffffu;
+            L.pend = false;
             L.item = it;
             L.slot = slot;
             L.tz = t[2];
@@ -437,11 +479,11 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
     // march: up to kBurst samples per busy lane (the guard-free division when every busy
     // lane allows it: a wave-uniform choice)
     int st = 0;
-    constexpr bool kFB = (kMode & 2) != 0;
+    constexpr bool kFB = (kMode & 2) != 0, kCH = (kMode & 4) != 0;
     if ((kMode & 1) && __builtin_amdgcn_ballot_w64(L.item >= 0 && !L.fdiv) == 0) {
 #pragma unroll 1
       for (int b = 0; b < kBurst; ++b) {
-        if (L.item >= 0 && st == 0) st = rev_step<true, kFB>(g, vd, L, depth0, max_steps, samples, rst);
+        if (L.item >= 0 && st == 0) st = rev_step<true, kFB, kCH>(g, vd, L, depth0, max_steps, samples, rst);
         if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
       }
     } else {
@@ -449,7 +491,7 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
       for (int b = 0; b < kBurst; ++b) {
         DMF_RS(10, l == 0);
         DMF_RS(11, L.item >= 0 && st == 0);
-        if (L.item >= 0 && st == 0) st = rev_step<false, kFB>(g, vd, L, depth0, max_steps, samples, rst);
+        if (L.item >= 0 && st == 0) st = rev_step<false, kFB, kCH>(g, vd, L, depth0, max_steps, samples, rst);
         if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
       }
     }
@@ -680,6 +722,8 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
         case 9: if (enumerate) DMF_REVQM(true, 0, 3); else DMF_REVQM(false, 1, 3); break;    // fast division + float bins
         case 10: if (enumerate) DMF_REVQM(true, 0, 2); else DMF_REVQM(false, 1, 2); break;   // float bins only
         case 11: if (enumerate) DMF_REVQM(true, 0, 1); else DMF_REVQM(false, 1, 1); break;   // fast division only
+        case 12: if (enumerate) DMF_REVQM(true, 0, 4); else DMF_REVQM(false, 1, 4); break;   // deferred jump verification
+        case 13: if (enumerate) DMF_REVQM(true, 0, 5); else DMF_REVQM(false, 1, 5); break;   // deferred + fast division
         default: if (enumerate) DMF_REVQ(true, 0); else DMF_REVQ(false, 1); break;
       }
     } else if (enumerate) {
