@@ -869,10 +869,13 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
                                                         BkGeom bg, ulonglong2* __restrict__ rays,
                                                         uint32_t* __restrict__ pose_cnt,
                                                         uint32_t* __restrict__ wg_base,
+                                                        uint32_t* __restrict__ wg_list, int wgl_stride,
                                                         unsigned long long* __restrict__ pose_pairs,
                                                         unsigned long long* __restrict__ stats) {
   extern __shared__ uint32_t hist[];
+  __shared__ uint32_t nlist;
   stats = stat_slot(stats);
+  if (threadIdx.x == 0) nlist = 0;
   for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
@@ -912,14 +915,20 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
   }
   __syncthreads();
   uint32_t* const pc = pose_cnt + (size_t)pw * bg.nbricks;
+  // the workgroup's touched bricks: [count | uint16 brick ids] (pass B initialises only these)
+  uint32_t* const row = wg_list + (size_t)blockIdx.x * (size_t)wgl_stride;
+  uint16_t* const ids = (uint16_t*)(row + 1);
   unsigned long long mine = 0;
   for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) {
     const uint32_t n = hist[i];
     if (n) {
       wg_base[(size_t)blockIdx.x * bg.nbricks + i] = atomicAdd(&pc[i], n);
+      ids[atomicAdd(&nlist, 1u)] = (uint16_t)i;
       mine += n;
     }
   }
+  __syncthreads();
+  if (threadIdx.x == 0) row[0] = nlist;
   for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o, 64);
   if (l == 0 && mine) atomicAdd(&pose_pairs[pw], mine);
   if (stats) wave_stats(stats, upd, nvalid, nhit);
@@ -1123,6 +1132,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
                                                          const uint32_t* __restrict__ pose_base,
                                                          const uint32_t* __restrict__ wg_base,
                                                          const uint32_t* __restrict__ bt, int j,
+                                                         const uint32_t* __restrict__ wg_list, int wgl_stride,
                                                          uint4* __restrict__ pa, void* __restrict__ pbv) {
   static_assert(SLAB || !R20, "the 20-byte record carries the slab state");
   uint2* const pb = (uint2*)pbv;
@@ -1136,7 +1146,17 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
   // this workgroup are never used
   const uint32_t* wb = wg_base + (size_t)blockIdx.x * bg.nbricks;
   const uint32_t* pbz = pose_base + (size_t)pz * bg.nbricks;
-  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = off[i] + pbz[i] + wb[i];
+  if (wg_list) {  // only the bricks pass A counted for this workgroup (1024^3: 32768 bricks, ~300 touched)
+    const uint32_t* row = wg_list + (size_t)blockIdx.x * (size_t)wgl_stride;
+    const uint32_t nl = row[0];
+    const uint16_t* ids = (const uint16_t*)(row + 1);
+    for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x) {
+      const int i = ids[k];
+      hist[i] = off[i] + pbz[i] + wb[i];
+    }
+  } else {
+    for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = off[i] + pbz[i] + wb[i];
+  }
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int q0 = (int)(blockIdx.x - (unsigned)pz * (unsigned)wg_pose) * span;
@@ -2141,7 +2161,7 @@ struct BkPlan {
   int64_t PS = 0;             // poses per super-batch (one pass A over all of them)
   int64_t PBg = 0;            // poses per batch under the geometric bound (>= 1)
   int max_poses = 0;          // cap of poses per batch (DMF_BK_BATCH_POSES test hook; else PS)
-  int ab_threads = 0, span = 0, wg_pose = 0;
+  int ab_threads = 0, span = 0, wg_pose = 0, wgl_stride = 0;
   uint32_t part_max = kBkPartMax;  // pairs per part of phase F (DMF_BK_PART_MAX: A/B)
   size_t rec_bytes = 24;           // bytes per pair record: 16 (pa) + 8 (pb) or, 20-B records, 16 + 4
   size_t hist_bytes = 0;
@@ -2174,8 +2194,10 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   pl.wg_pose = (int)((pl.ppose + pl.span - 1) / pl.span);
   pl.hist_bytes = sizeof(uint32_t) * (size_t)pl.bg.nbricks;
   // per pose: ray records, per-workgroup brick bases, pose counts and bases, pose pairs + batch table
+  pl.wgl_stride = 1 + (pl.bg.nbricks + 1) / 2;  // touched-brick list per workgroup: count + uint16 ids
   pl.per_pose_bytes = (uint64_t)rays_pose * sizeof(ulonglong2) + (uint64_t)pl.wg_pose * pl.hist_bytes +
-                      2 * (uint64_t)pl.hist_bytes + sizeof(unsigned long long) + sizeof(uint32_t);
+                      (uint64_t)pl.wg_pose * sizeof(uint32_t) * (uint64_t)pl.wgl_stride + 2 * (uint64_t)pl.hist_bytes +
+                      sizeof(unsigned long long) + sizeof(uint32_t);
   const uint64_t budget = v->bk_budget;
   pl.PS = std::min<int64_t>(P, (int64_t)(budget / 2 / pl.per_pose_bytes));
   if (pl.PS < 1) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion budget (dmf_fuse_reserve)");
@@ -2220,7 +2242,7 @@ static int bk_attributes() {
 // batch table, pair records.
 struct BkBufs {
   ulonglong2* rays = nullptr;
-  uint32_t *cnt = nullptr, *off = nullptr, *part_pref = nullptr, *wgb = nullptr;
+  uint32_t *cnt = nullptr, *off = nullptr, *part_pref = nullptr, *wgb = nullptr, *wgl = nullptr;
   uint32_t *pose_cnt = nullptr, *pose_base = nullptr, *bt = nullptr;
   unsigned long long* pose_pairs = nullptr;
   uint2* order = nullptr;
@@ -2232,12 +2254,13 @@ struct BkBufs {
 // Allocates only when a slot is too small.
 static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b) {
   const size_t PS = (size_t)pl.PS, nb = (size_t)pl.bg.nbricks;
-  void *rays, *bricks, *ctl, *wgb, *pra, *prb, *pcnt, *pbase, *batch;
+  void *rays, *bricks, *ctl, *wgb, *wgl, *pra, *prb, *pcnt, *pbase, *batch;
   DMF_TRY(scratch(v, kScBkRays, sizeof(ulonglong2) * (size_t)(pl.PS * pl.ppose * 64), &rays));
   // cnt | off | part_pref (nbricks + 1) | order (uint2 per part)
   DMF_TRY(scratch(v, kScBkBricks, sizeof(uint32_t) * (3 * nb + 6 + 2 * pl.max_parts()), &bricks));
   DMF_TRY(scratch(v, kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
   DMF_TRY(scratch(v, kScBkWgBase, pl.hist_bytes * (size_t)pl.wg_pose * PS, &wgb));
+  DMF_TRY(scratch(v, kScBkWgList, sizeof(uint32_t) * (size_t)pl.wgl_stride * (size_t)pl.wg_pose * PS, &wgl));
   DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * (size_t)pl.pair_cap, &pra));
   DMF_TRY(scratch(v, kScBkPairsB, (pl.rec_bytes - sizeof(uint4)) * (size_t)pl.pair_cap, &prb));
   DMF_TRY(scratch(v, kScBkPoseCnt, pl.hist_bytes * PS, &pcnt));
@@ -2249,6 +2272,7 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b) {
   b.part_pref = b.off + nb;  // nbricks + 1
   b.order = (uint2*)(b.part_pref + nb + 4 + (nb & 1));  // 8-B aligned
   b.wgb = (uint32_t*)wgb;
+  b.wgl = (uint32_t*)wgl;
   b.ctl = (unsigned long long*)ctl;
   b.pra = (uint4*)pra;
   b.prb = prb;
@@ -2280,6 +2304,10 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     return !(e && atoi(e) == 0);
   }();
   const uint2* lpt = lpt_on ? b.order : nullptr;
+  const bool tlist = [] {  // A/B: DMF_BK_TLIST=0 makes pass B initialise its whole brick histogram
+    const char* e = getenv("DMF_BK_TLIST");
+    return !(e && atoi(e) == 0);
+  }();
   for (int64_t s0 = 0; s0 < P; s0 += pl.PS) {
     const int64_t ps = std::min<int64_t>(pl.PS, P - s0);
     const unsigned nwg = (unsigned)(ps * pl.wg_pose);
@@ -2287,7 +2315,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     DMF_HIP(hipMemsetAsync(b.pose_pairs, 0, sizeof(unsigned long long) * (size_t)ps, sa));
     hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, g, cp,
                        d_depth + (size_t)s0 * cp.H * cp.W, tab + s0, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
-                       pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.pose_pairs, st);
+                       pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st);
     DMF_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sa, (int)ps, (const unsigned long long*)b.pose_pairs,
                        (unsigned long long)pl.pair_cap, pl.max_poses, b.bt);
@@ -2305,7 +2333,8 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
 #define DMF_BK_PAIRS(...)                                                                                          \
   hipLaunchKernelGGL((k_bk_pairs<__VA_ARGS__>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,  \
                      pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off,                   \
-                     (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j, b.pra, b.prb)
+                     (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,             \
+                     tlist ? (const uint32_t*)b.wgl : nullptr, pl.wgl_stride, b.pra, b.prb)
       if (fv == 48)  // wave-aggregated slot atomics (the previous default)
         DMF_BK_PAIRS(true, true);
       else if (fv == 65)

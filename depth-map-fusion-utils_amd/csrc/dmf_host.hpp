@@ -52,6 +52,7 @@ enum ScratchSlot {
   kScSort1, kScSort2, kScSort3, kScCount, kScStats,
   // brick-owned fusion (dmf_fuse.hip)
   kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkWgBase, kScBkCtl, kScBkPoseCnt, kScBkPoseBase, kScBkBatch,
+  kScBkWgList,
   kScOgP0, kScOgP1, kScOgFinal, kScOgOcc  // OccupancyGrid reorganization (dmf_ogrid.hip)
 };
 
