@@ -78,8 +78,10 @@ def workload_name(grid, P, world):
         return "config2"
     if (WIDTH, HEIGHT, grid) == (1280, 720, 512) and P * world == 256:
         return "config3"
+    if (WIDTH, HEIGHT, grid) == (1280, 720, 1024) and P == 256:
+        return "config5-shard (2048 poses / 8 GPUs)"
     if (WIDTH, HEIGHT, grid) == (1280, 720, 1024):
-        return "config5-shard"
+        return "config5-grid (fewer poses than its 256-pose shard)"
     if (WIDTH, HEIGHT, grid) == (640, 480, 512) and P * world == 1024 and world == 1:
         return "config4-anchor (all 1024 poses on one GPU)"
     if (WIDTH, HEIGHT, grid) == (640, 480, 512):
