@@ -246,3 +246,28 @@ def test_merge_slabs_emulated_ranks(dims, G):
     assert covered == 2 * nlo
     ncell = dims[0] * dims[1] * dims[2]
     assert torch.equal(out[:ncell], ref[:ncell])
+
+
+def test_rccl_world2_merge(tmp_path):
+    """World-2 RCCL merge across two GPUs: two processes, each fusing its pose
+    shard of an odd 61^3 grid and merging through dmf_fuse_merge_finalize_device over a
+    libdmf communicator; rank 0's merged log-odds equal one rank fusing every pose.  Runs
+    only where the box has two GPUs (the builder's boxes have one: the slab arithmetic of
+    ranks > 0 is covered by test_merge_slabs_emulated_ranks)."""
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rccl_world2_worker.py")
+    uid = str(tmp_path / "uid")
+    outs = [str(tmp_path / f"r{r}.txt") for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, worker, str(r), uid, outs[r]]) for r in range(2)]
+    try:
+        rcs = [p.wait(timeout=150) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0], rcs
+    assert open(outs[0]).read() == "OK" and open(outs[1]).read() == "OK"
