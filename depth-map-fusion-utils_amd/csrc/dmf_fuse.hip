@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
                                                   uint32_t* __restrict__ part_pref,
                                                   unsigned long long* __restrict__ ctl,
                                                   uint2* __restrict__ order, uint32_t part_max,
-                                                  const uint32_t* __restrict__ bt, int j) {
+                                                  const uint32_t* __restrict__ bt, int j, int split_cu) {
   if ((uint32_t)j >= bt[0]) {  // a batch the call does not need: no pairs, no parts
     if (threadIdx.x == 0) ctl[0] = ctl[1] = 0;
     return;
@@ -1077,10 +1077,26 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
     }
     pbase += np;
   }
+  // Tail split (split_cu = phase F's workgroups | k << 16, 0 = off): with fewer than 8 parts
+  // per workgroup the parts are near equal (dense bricks at 256^3 all reach part_max), so
+  // the last round of the queue leaves most CUs idle.  The last k * workgroups entries of
+  // the order (k = 2: config 2 1.996 -> 1.961 ms; 1 and 4 slower) are cut into quarters
+  // (entry .y = 4j + s with bit 31 set: quarter s of part j), so the queue ends in parts a
+  // quarter of the size.  Only the largest-first order carries them.
+  const uint32_t NP = s_parts[1023];
+  uint32_t S = 0;
+  if (split_cu > 0 && NP < 8u * (uint32_t)(split_cu & 0xffff))
+    S = min(min(NP, 1024u), (uint32_t)(split_cu >> 16) * (uint32_t)(split_cu & 0xffff));
+  __syncthreads();  // every order entry written
+  uint2 e = make_uint2(0, 0);
+  if ((uint32_t)t < S) e = order[NP - S + t];
+  __syncthreads();
+  if ((uint32_t)t < S)
+    for (uint32_t sq = 0; sq < 4; ++sq) order[NP - S + 4 * t + sq] = make_uint2(e.x, (4u * e.y + sq) | 0x80000000u);
   if (t == 1023) {
-    part_pref[nbricks] = s_parts[1023];
+    part_pref[nbricks] = NP;
     ctl[0] = s_pairs[1023];
-    ctl[1] = s_parts[1023];
+    ctl[1] = NP + 3 * S;
   }
 }
 
@@ -1700,10 +1716,12 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     if (sh[0] >= nparts) break;
     int b;
     uint32_t j;
+    uint32_t q4 = 1;  // quarters of the tail split (k_bk_scan)
     if (order) {  // largest parts first, (brick, index) from k_bk_scan
       const uint2 o = order[sh[0]];
       b = (int)o.x;
-      j = o.y;
+      j = o.y & 0x7fffffffu;
+      q4 = o.y >> 31 ? 4u : 1u;
     } else {  // brick order: the last brick b with part_pref[b] <= t
       const uint32_t t = sh[0];
       int lo = 0, hi = bg.nbricks - 1;
@@ -1715,7 +1733,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       b = lo;
       j = t - part_pref[b];
     }
-    const uint32_t nb_pairs = cnt[b], np = (nb_pairs + part_max - 1) / part_max;
+    const uint32_t nb_pairs = cnt[b], np = q4 * ((nb_pairs + part_max - 1) / part_max);
     const uint32_t p0 = off[b] + (uint32_t)(((uint64_t)nb_pairs * j) / np);
     const uint32_t n = (uint32_t)(((uint64_t)nb_pairs * (j + 1)) / np) - (uint32_t)(((uint64_t)nb_pairs * j) / np);
     // 20-B records: buffer resources over the part's records (32-bit offsets < 2^21, no
@@ -2169,7 +2187,8 @@ struct BkPlan {
   uint64_t per_pose_bytes = 0;
   int64_t jmax(int64_t ps) const { return (ps + PBg - 1) / PBg; }
   int64_t max_batches(int64_t P) const { return (P / PS) * jmax(PS) + (P % PS ? jmax(P % PS) : 0); }
-  size_t max_parts() const { return (size_t)bg.nbricks + pair_cap / part_max + 1; }
+  int split_cu = 0;  // k_bk_scan's tail split: F's workgroups | entries split per CU << 16 (0 = off)
+  size_t max_parts() const { return (size_t)bg.nbricks + pair_cap / part_max + 1 + 3 * 1024; }
 };
 
 static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, BkPlan& pl) {
@@ -2214,6 +2233,13 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
     if (c > 0) pl.max_poses = (int)std::min<int64_t>(pl.PS, c);
   }
   pl.PBg = std::max<int64_t>(1, std::min<int64_t>(pl.max_poses, (int64_t)(pl.pair_cap / one_pose)));
+  // tail split of the part queue (k_bk_scan): the largest-first order of k_bk_fuse_s only
+  const char* lpt = getenv("DMF_BK_LPT");
+  const char* ts = getenv("DMF_BK_TAILSPLIT");  // A/B: 0 = off
+  if (is_slab_variant(fuse_variant()) && !(lpt && atoi(lpt) == 0) && !(ts && atoi(ts) == 0)) {
+    const int k = ts ? std::max(1, std::min(atoi(ts), 8)) : 2;  // entries split: k per CU
+    pl.split_cu = std::min(512, cu_count(v->device)) | (k << 16);
+  }
   return DMF_OK;
 }
 
@@ -2328,7 +2354,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                          (int)j, (const uint32_t*)b.bt, (const uint32_t*)b.pose_cnt, b.pose_base, b.cnt);
       DMF_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off, b.part_pref,
-                         b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j);
+                         b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       DMF_LAUNCH_CHECK();
 #define DMF_BK_PAIRS(...)                                                                                          \
   hipLaunchKernelGGL((k_bk_pairs<__VA_ARGS__>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,  \
