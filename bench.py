@@ -288,6 +288,14 @@ def main():
     logodds = torch.empty(nlo.value, dtype=torch.int16, device=dev)
     stats = torch.zeros(20, dtype=torch.int64, device=dev)  # 8 used; diagnostic builds add 7..19
     pcam, pprm = C.addressof(cam), C.addressof(prm)
+    # Pipelined fusion (DMF_BENCH_PIPE=0 = serial): the frames are resident and
+    # never rewritten, so their input stream is an idle one; each call's pass A then runs on
+    # libdmf's staging stream beside the previous call's passes B and F.
+    pipe = os.environ.get("DMF_BENCH_PIPE", "1") != "0"
+    inp = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    if pipe:
+        _lib.check(L.dmf_fuse_set_input_stream(vol._h, inp.cuda_stream))
     # all fusion scratch allocated up front: the timed calls neither allocate nor sync
     _lib.check(L.dmf_fuse_reserve(vol._h, pcam, P, 0))
 
@@ -361,7 +369,9 @@ def main():
                                       "(dmf_fuse_merge_finalize_device)",
                                 "torch": f"torch {'RCCL' if backend == 'nccl' else backend} all-reduce(sum) + finalize"}[merge_mode] if world > 1
                  else "finalize (no collective at N=1)",
-                 "schedule": "merge of step i, then the zeroing of its buffer for step i+2, on the comm stream overlap fuse of step i+1 (2 counter buffers)"}
+                 "schedule": "merge of step i, then the zeroing of its buffer for step i+2, on the comm stream overlap fuse of step i+1 (2 counter buffers)"
+                             + ("; pass A of fuse i+1 on libdmf's staging stream beside passes B and F of fuse i (the 'fuse' span is the "
+                                "compute stream's: batch cut, B and F after waiting for that pass A)" if pipe else "")}
     # grid-wide streaming passes, priced separately: clear writes the
     # 2 tiled int32 counter arrays; finalize reads them and writes int16 log-odds
     clear_bytes = 2 * 4 * nct
@@ -380,7 +390,28 @@ def main():
     # per-launch algorithmic bytes of the fusion launch (all its kernels), this rank
     upd_launch = float(st[0]) / args.steps
     bytes_launch = BYTES_PER_UPDATE * upd_launch + BYTES_PER_DEPTH * P * HEIGHT * WIDTH
-    achieved = bytes_launch / (fuse_ms * 1e-3) / 1e9
+    ms = elapsed / args.steps * 1e3
+    serial_ms = None
+    if pipe:
+        # pipelined calls overlap (pass A of call i+1 beside B and F of call i), so a call's own
+        # event span is no duration: the fusion is priced over the whole step interval (which
+        # also holds the overlapped finalize).  The serial call, timed alone, is reported beside.
+        _lib.check(L.dmf_fuse_set_input_stream(vol._h, None))
+        c = bufs[0]
+        for _ in range(3):
+            fuse(0, 0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        nser = 50
+        e0.record(stream)
+        for _ in range(nser):
+            fuse(0, 0)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        serial_ms = e0.elapsed_time(e1) / nser
+        fuse_kernel_ms = ms
+    else:
+        fuse_kernel_ms = fuse_ms
+    achieved = bytes_launch / (fuse_kernel_ms * 1e-3) / 1e9
 
     result = None
     if rank == 0:
@@ -400,7 +431,6 @@ def main():
             cpu_mt = {"value": ups_mt, "unit": "ray-voxel updates/s", "cores": nt, "kind": "port",
                       "sample": f"oracle fuse (OpenMP rows, atomic counters) of {nf} of the {P} frames, "
                                 f"{dt_mt:.1f}s on {nt} threads; Mrays/s {rps_mt / 1e6:.3f}"}
-        ms = elapsed / args.steps * 1e3
         kname = L.dmf_fuse_kernel().decode()
         if kname.startswith("dmf::k_bk_fuse"):
             # brick-owned pipeline: kernel_ms spans every launch of the call
@@ -453,10 +483,16 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "basis": "effective (algorithmic): SURVEY.md 8d bytes, 4 B per cell update + 2 B per depth "
-                                  "pixel, over the fusion launch's HIP-event time; the brick pipeline accumulates "
-                                  "in LDS, so these bytes are a price, not its HBM traffic",
+                                  "pixel, " + ("over the step interval of the pipelined fusion (elapsed / steps: pass A "
+                                               "of call i+1 runs beside passes B and F of call i, DESIGN.md 5.10)"
+                                               if pipe else "over the fusion launch's HIP-event time")
+                                  + "; the brick pipeline accumulates in LDS, so these bytes are a price, not its "
+                                    "HBM traffic",
                          "measured_frac": None, "traffic_source": None,
-                         "kernel": kname, "kernel_ms": fuse_ms, "pipeline": pipeline,
+                         "kernel": kname, "kernel_ms": fuse_kernel_ms, "pipeline": pipeline,
+                         "pipelined": pipe, "serial_call_ms": serial_ms,
+                         "serial_call_frac": (bytes_launch / (serial_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                              if serial_ms else None),
                          "updates_per_launch": upd_launch, "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,

@@ -103,6 +103,12 @@ int pose_table(dmf_volume* v, const float* poses, int P, bool on_device, PoseX**
   return DMF_OK;
 }
 
+int pose_table_into(const float* d_poses, int P, PoseX* d_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_pose_table, dim3((P + 63) / 64), dim3(64), 0, s, d_poses, P, d_out);
+  DMF_LAUNCH_CHECK();
+  return DMF_OK;
+}
+
 // ---------------------------------------------------------------- striped stats
 int stats_begin(dmf_volume* v, unsigned long long** striped) {
   void* b;
@@ -752,6 +758,9 @@ int dmf_volume_destroy(dmf_volume* v) {
   (void)hipDeviceSynchronize();
   free_state(v);
   if (v->switch_ev) (void)hipEventDestroy(v->switch_ev);
+  for (hipEvent_t e : {v->st_in, v->st_done[0], v->st_done[1], v->st_free[0], v->st_free[1], v->st_b[0], v->st_b[1]})
+    if (e) (void)hipEventDestroy(e);
+  if (v->stage) (void)hipStreamDestroy(v->stage);
   delete v;
   return DMF_OK;
   DMF_API_END

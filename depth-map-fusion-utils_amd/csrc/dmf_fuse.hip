@@ -2006,21 +2006,30 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     }
     DMF_T(tf0);
     __syncthreads();
-    // flush: as k_bk_fuse (one device atomic per non-zero cell and counter)
-    for (int e = tid; e < bk::kCells; e += blockDim.x) {
-      const int tile = e >> 4, w16 = e & 15;
-      const int tx = tile >> (2 * bk::kLog - 3), ty = (tile >> (bk::kLog - 2)) & ((bk::kB >> 1) - 1),
-                tz = tile & ((bk::kB >> 2) - 1);
-      const int lx = tx * 2 + (w16 >> 3), ly = ty * 2 + ((w16 >> 2) & 1), lz = tz * 4 + (w16 & 3);
-      const int li = lx * kBkSx + ly * kBkSy + lz;
-      const uint32_t v = box[li];
-      if (v) {
-        box[li] = 0;
-        const uint32_t ti = tiled_index(tl, lo0 + lx, lo1 + ly, lo2 + lz);
-        const int32_t mi = (int32_t)(v & 0xffffu), hv = (int32_t)(v >> 16);
-        if (mi) atomic_add_dev(&misses[ti], mi);
-        if (hv) atomic_add_dev(&hits[ti], hv);
-        ++nflush;
+    // flush (one device atomic per non-zero cell and counter): lane tid takes cells
+    // e = tid + 1024 k of the brick in the tiled order (16 lanes per 64-B counter line).  The
+    // cell's box word and its counter index inside the brick move by per-k constants, so
+    // the index math is done once per part, not per cell (cell e: tile e >> 4 = (tx, ty, tz)
+    // with tx = k >> 1, ty = 8 (k & 1) + (t0 >> 3), tz = t0 & 7 for t0 = tid >> 4).
+    {
+      static_assert(bk::kLog == 5 && kBkThreads == 1024, "flush strides: 32^3-cell bricks, 1024 lanes");
+      const int t0 = tid >> 4, w16 = tid & 15;
+      const int li0 = (w16 >> 3) * kBkSx + (2 * (t0 >> 3) + ((w16 >> 2) & 1)) * kBkSy + 4 * (t0 & 7) + (w16 & 3);
+      const uint32_t ti0 = tile_base(tl, lo0 >> 1, lo1 >> 1, lo2 >> 2) +
+                           ((((uint32_t)(t0 >> 3)) * tl.nz + (uint32_t)(t0 & 7)) << 4) + (uint32_t)w16;
+      const uint32_t sA = (tl.ny * tl.nz) << 4, sB = (8u * tl.nz) << 4;  // tx + 1, ty + 8
+#pragma unroll 4
+      for (int k = 0; k < bk::kCells / kBkThreads; ++k) {
+        const int li = li0 + (k >> 1) * (2 * kBkSx) + (k & 1) * (16 * kBkSy);
+        const uint32_t v = box[li];
+        if (v) {
+          box[li] = 0;
+          const uint32_t ti = ti0 + (uint32_t)(k >> 1) * sA + (uint32_t)(k & 1) * sB;
+          const int32_t mi = (int32_t)(v & 0xffffu), hv = (int32_t)(v >> 16);
+          if (mi) atomic_add_dev(&misses[ti], mi);
+          if (hv) atomic_add_dev(&hits[ti], hv);
+          ++nflush;
+        }
       }
     }
     __syncthreads();
@@ -2191,6 +2200,14 @@ struct BkPlan {
   size_t max_parts() const { return (size_t)bg.nbricks + pair_cap / part_max + 1 + 3 * 1024; }
 };
 
+// Pipelined fusion: 2 = pass A, the batch layout and pass B of a call run
+// on the staging stream (the default: 512^3 x 128 frames 6.50 -> 6.16 ms per call); 1 = pass A
+// only (6.46 ms; A/B via DMF_BK_STAGE=1)
+static int stage_level() {
+  const char* e = getenv("DMF_BK_STAGE");
+  return e ? std::max(1, std::min(atoi(e), 2)) : 2;
+}
+
 static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, BkPlan& pl) {
   pl.bg = brick_geom(g);
   pl.pkx = (cp.W + 7) / 8;
@@ -2217,8 +2234,13 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   pl.per_pose_bytes = (uint64_t)rays_pose * sizeof(ulonglong2) + (uint64_t)pl.wg_pose * pl.hist_bytes +
                       (uint64_t)pl.wg_pose * sizeof(uint32_t) * (uint64_t)pl.wgl_stride + 2 * (uint64_t)pl.hist_bytes +
                       sizeof(unsigned long long) + sizeof(uint32_t);
-  const uint64_t budget = v->bk_budget;
+  // with pass B staged the two slots each hold pair records: each gets half the budget
+  const uint64_t budget = v->pipelined && stage_level() >= 2 ? v->bk_budget / 2 : v->bk_budget;
   pl.PS = std::min<int64_t>(P, (int64_t)(budget / 2 / pl.per_pose_bytes));
+  if (const char* e = getenv("DMF_BK_SUPER_POSES")) {  // test hook: cap the poses per super-batch
+    const int64_t c = (int64_t)atoll(e);
+    if (c > 0) pl.PS = std::min<int64_t>(pl.PS, c);
+  }
   if (pl.PS < 1) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion budget (dmf_fuse_reserve)");
   pl.pair_cap = std::min<uint64_t>({(budget - (uint64_t)pl.PS * pl.per_pose_bytes) / pl.rec_bytes,
                                     (uint64_t)pl.PS * one_pose, (uint64_t)UINT32_MAX});
@@ -2277,21 +2299,27 @@ struct BkBufs {
   void* prb = nullptr;  // uint2 per pair (24-B records) or uint32 (20-B records)
 };
 
-// Allocates only when a slot is too small.
-static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b) {
+// Allocates only when a slot is too small.  `slot` picks the buffers pass A writes (ray
+// records, workgroup bases and touched-brick lists, pose counts and pair totals + batch
+// table): 0 or 1, the two staging slots of pipelined fusion (slot 0 serially).
+// slot_all: the brick layout, part queue and pair records are per slot too (pass B staged).
+static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b, int slot = 0, bool slot_all = false) {
   const size_t PS = (size_t)pl.PS, nb = (size_t)pl.bg.nbricks;
+  const bool s2 = slot && slot_all;
   void *rays, *bricks, *ctl, *wgb, *wgl, *pra, *prb, *pcnt, *pbase, *batch;
-  DMF_TRY(scratch(v, kScBkRays, sizeof(ulonglong2) * (size_t)(pl.PS * pl.ppose * 64), &rays));
+  DMF_TRY(scratch(v, slot ? kScBkRays1 : kScBkRays, sizeof(ulonglong2) * (size_t)(pl.PS * pl.ppose * 64), &rays));
   // cnt | off | part_pref (nbricks + 1) | order (uint2 per part)
-  DMF_TRY(scratch(v, kScBkBricks, sizeof(uint32_t) * (3 * nb + 6 + 2 * pl.max_parts()), &bricks));
-  DMF_TRY(scratch(v, kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
-  DMF_TRY(scratch(v, kScBkWgBase, pl.hist_bytes * (size_t)pl.wg_pose * PS, &wgb));
-  DMF_TRY(scratch(v, kScBkWgList, sizeof(uint32_t) * (size_t)pl.wgl_stride * (size_t)pl.wg_pose * PS, &wgl));
-  DMF_TRY(scratch(v, kScBkPairs, sizeof(uint4) * (size_t)pl.pair_cap, &pra));
-  DMF_TRY(scratch(v, kScBkPairsB, (pl.rec_bytes - sizeof(uint4)) * (size_t)pl.pair_cap, &prb));
-  DMF_TRY(scratch(v, kScBkPoseCnt, pl.hist_bytes * PS, &pcnt));
-  DMF_TRY(scratch(v, kScBkPoseBase, pl.hist_bytes * PS, &pbase));
-  DMF_TRY(scratch(v, kScBkBatch, sizeof(unsigned long long) * PS + sizeof(uint32_t) * (PS + 4), &batch));
+  DMF_TRY(scratch(v, s2 ? kScBkBricks1 : kScBkBricks, sizeof(uint32_t) * (3 * nb + 6 + 2 * pl.max_parts()), &bricks));
+  DMF_TRY(scratch(v, s2 ? kScBkCtl1 : kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
+  DMF_TRY(scratch(v, slot ? kScBkWgBase1 : kScBkWgBase, pl.hist_bytes * (size_t)pl.wg_pose * PS, &wgb));
+  DMF_TRY(scratch(v, slot ? kScBkWgList1 : kScBkWgList,
+                  sizeof(uint32_t) * (size_t)pl.wgl_stride * (size_t)pl.wg_pose * PS, &wgl));
+  DMF_TRY(scratch(v, s2 ? kScBkPairs1 : kScBkPairs, sizeof(uint4) * (size_t)pl.pair_cap, &pra));
+  DMF_TRY(scratch(v, s2 ? kScBkPairsB1 : kScBkPairsB, (pl.rec_bytes - sizeof(uint4)) * (size_t)pl.pair_cap, &prb));
+  DMF_TRY(scratch(v, slot ? kScBkPoseCnt1 : kScBkPoseCnt, pl.hist_bytes * PS, &pcnt));
+  DMF_TRY(scratch(v, s2 ? kScBkPoseBase1 : kScBkPoseBase, pl.hist_bytes * PS, &pbase));
+  DMF_TRY(scratch(v, slot ? kScBkBatch1 : kScBkBatch, sizeof(unsigned long long) * PS + sizeof(uint32_t) * (PS + 4),
+                  &batch));
   b.rays = (ulonglong2*)rays;
   b.cnt = (uint32_t*)bricks;
   b.off = b.cnt + nb;
@@ -2314,22 +2342,44 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b) {
 // layout (k_bk_batch_counts, k_bk_scan), pass B and phase F; a launch past the device's
 // batch count exits at once.  Phase F reads its part count itself (its persistent
 // workgroups exit when the queue is empty).
-static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint16_t* d_depth, const PoseX* tab, int P,
-                       const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses, unsigned long long* st) {
+// Pipelined (staged): the pose table and pass A of each super-batch run on
+// the volume's staging stream into staging slot s (alternating), after the caller's input
+// stream and after the slot's previous reader (the super-batch two back); the volume's stream
+// waits for them before its batch cut, and the input stream waits for them too (the inputs
+// stay ordered before the caller's next writes).  Pass A's statistics go to the slot's own
+// striped buffer, summed into d_user on the volume's stream.
+
+static int stage_init(dmf_volume* v) {
+  if (v->stage) return DMF_OK;
+  DMF_HIP(hipStreamCreateWithFlags(&v->stage, hipStreamNonBlocking));
+  DMF_HIP(hipEventCreateWithFlags(&v->st_in, hipEventDisableTiming));
+  for (int k = 0; k < 2; ++k) {
+    DMF_HIP(hipEventCreateWithFlags(&v->st_done[k], hipEventDisableTiming));
+    DMF_HIP(hipEventCreateWithFlags(&v->st_free[k], hipEventDisableTiming));
+    DMF_HIP(hipEventCreateWithFlags(&v->st_b[k], hipEventDisableTiming));
+    v->st_free_set[k] = false;
+  }
+  return DMF_OK;
+}
+
+static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint16_t* d_depth, const PoseX* tab,
+                       const float* d_poses, int P, const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses,
+                       unsigned long long* st, uint64_t* d_user, bool staged) {
   BkPlan pl;
   DMF_TRY(bk_plan(v, cp, g, P, pl));
   const BkGeom& bg = pl.bg;
   DMF_TRY(bk_attributes());
   BkBufs b;
-  DMF_TRY(bk_scratch(v, pl, b));
-  const hipStream_t sa = v->stream;
+  if (staged) DMF_TRY(stage_init(v));
+  // staged pass B (DMF_BK_STAGE=2): the batch cut, brick layout and pass B run on the staging
+  // stream too, into the slot's own pair records; only phase F stays on the volume's stream
+  const bool stage_b = staged && stage_level() >= 2;
   const unsigned nf = (unsigned)cu_count(v->device);
   const int fv = fuse_variant();
   const bool lpt_on = [] {  // A/B: DMF_BK_LPT=0 hands the parts out in brick order
     const char* e = getenv("DMF_BK_LPT");
     return !(e && atoi(e) == 0);
   }();
-  const uint2* lpt = lpt_on ? b.order : nullptr;
   const bool tlist = [] {  // A/B: DMF_BK_TLIST=0 makes pass B initialise its whole brick histogram
     const char* e = getenv("DMF_BK_TLIST");
     return !(e && atoi(e) == 0);
@@ -2337,27 +2387,58 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   for (int64_t s0 = 0; s0 < P; s0 += pl.PS) {
     const int64_t ps = std::min<int64_t>(pl.PS, P - s0);
     const unsigned nwg = (unsigned)(ps * pl.wg_pose);
+    const int slot = staged ? v->st_slot : 0;
+    DMF_TRY(bk_scratch(v, pl, b, slot, stage_b));
+    const uint2* lpt = lpt_on ? b.order : nullptr;  // (the tail split needs the order: bk_plan)
+    const hipStream_t sa = staged ? v->stage : v->stream;
+    const PoseX* tab_a = staged ? nullptr : tab + s0;
+    unsigned long long* st_a = st;
+    if (staged) {
+      v->st_slot ^= 1;
+      DMF_HIP(hipEventRecord(v->st_in, v->in_stream));
+      DMF_HIP(hipStreamWaitEvent(sa, v->st_in, 0));
+      if (v->st_free_set[slot]) DMF_HIP(hipStreamWaitEvent(sa, v->st_free[slot], 0));
+      void* t;
+      DMF_TRY(scratch(v, slot ? kScStPoses1 : kScStPoses0, sizeof(PoseX) * (size_t)pl.PS, &t));
+      DMF_TRY(pose_table_into(d_poses + (size_t)s0 * 12, (int)ps, (PoseX*)t, sa));
+      tab_a = (const PoseX*)t;
+      if (st) {
+        void* sb;
+        DMF_TRY(scratch(v, slot ? kScStStats1 : kScStStats0, sizeof(unsigned long long) * kStatSlots * kStatWidth, &sb));
+        DMF_HIP(hipMemsetAsync(sb, 0, sizeof(unsigned long long) * kStatSlots * kStatWidth, sa));
+        st_a = (unsigned long long*)sb;
+      }
+    }
     DMF_HIP(hipMemsetAsync(b.pose_cnt, 0, pl.hist_bytes * (size_t)ps, sa));
     DMF_HIP(hipMemsetAsync(b.pose_pairs, 0, sizeof(unsigned long long) * (size_t)ps, sa));
     hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, g, cp,
-                       d_depth + (size_t)s0 * cp.H * cp.W, tab + s0, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
-                       pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st);
+                       d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
+                       pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st_a);
     DMF_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sa, (int)ps, (const unsigned long long*)b.pose_pairs,
+    if (staged) {
+      DMF_HIP(hipEventRecord(v->st_done[slot], sa));
+      DMF_HIP(hipStreamWaitEvent(v->stream, v->st_done[slot], 0));
+      DMF_HIP(hipStreamWaitEvent(v->in_stream, v->st_done[slot], 0));
+      if (st) DMF_TRY(stats_end(v, st_a, d_user, kStatWidth));
+    }
+    const hipStream_t sl = stage_b ? v->stage : v->stream;  // batch cut, brick layout, pass B
+    hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sl, (int)ps, (const unsigned long long*)b.pose_pairs,
                        (unsigned long long)pl.pair_cap, pl.max_poses, b.bt);
     DMF_LAUNCH_CHECK();
     v->bk_last_bt = b.bt;
     const int64_t jm = pl.jmax(ps);
     for (int64_t j = 0; j < jm; ++j) {
-      DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sa));
-      hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sa, bg.nbricks,
+      // batch j reuses the slot's pair records and part queue: after batch j-1's phase F
+      if (stage_b && j > 0) DMF_HIP(hipStreamWaitEvent(sl, v->st_free[slot], 0));
+      DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sl));
+      hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sl, bg.nbricks,
                          (int)j, (const uint32_t*)b.bt, (const uint32_t*)b.pose_cnt, b.pose_base, b.cnt);
       DMF_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off, b.part_pref,
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, sl, bg.nbricks, (const uint32_t*)b.cnt, b.off, b.part_pref,
                          b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       DMF_LAUNCH_CHECK();
 #define DMF_BK_PAIRS(...)                                                                                          \
-  hipLaunchKernelGGL((k_bk_pairs<__VA_ARGS__>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,  \
+  hipLaunchKernelGGL((k_bk_pairs<__VA_ARGS__>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sl, (int)pl.ppose,  \
                      pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off,                   \
                      (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,             \
                      tlist ? (const uint32_t*)b.wgl : nullptr, pl.wgl_stride, b.pra, b.prb)
@@ -2375,6 +2456,10 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         DMF_BK_PAIRS(false);
 #undef DMF_BK_PAIRS
       DMF_LAUNCH_CHECK();
+      if (stage_b) {
+        DMF_HIP(hipEventRecord(v->st_b[slot], sl));
+        DMF_HIP(hipStreamWaitEvent(v->stream, v->st_b[slot], 0));
+      }
 #define DMF_BK_FUSE(R, S, U, N, C, B)                                                                           \
   hipLaunchKernelGGL((k_bk_fuse<R, S, U, N, C, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,            \
                      (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
@@ -2427,6 +2512,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
 #undef DMF_BK_FUSE_S20
 #undef DMF_BK_FUSE_SB
       DMF_LAUNCH_CHECK();
+      if (stage_b) DMF_HIP(hipEventRecord(v->st_free[slot], v->stream));  // batch j's phase F
+    }
+    if (staged) {  // the slot's last readers (pass B and the batch layout, or phase F) are enqueued
+      DMF_HIP(hipEventRecord(v->st_free[slot], v->stream));
+      v->st_free_set[slot] = true;
     }
   }
   return DMF_OK;
@@ -2534,6 +2624,15 @@ int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t m
     DMF_TRY(bk_attributes());
     BkBufs set;
     DMF_TRY(bk_scratch(v, pl, set));
+    if (v->pipelined) {  // the second staging slot, the staging stream, slot pose tables and statistics
+      DMF_TRY(bk_scratch(v, pl, set, 1, stage_level() >= 2));
+      DMF_TRY(stage_init(v));
+      void* t;
+      for (int k = 0; k < 2; ++k) {
+        DMF_TRY(scratch(v, k ? kScStPoses1 : kScStPoses0, sizeof(PoseX) * (size_t)pl.PS, &t));
+        DMF_TRY(scratch(v, k ? kScStStats1 : kScStStats0, sizeof(unsigned long long) * kStatSlots * kStatWidth, &t));
+      }
+    }
   }
   DMF_HIP(hipStreamSynchronize(v->stream));
   return DMF_OK;
@@ -2600,25 +2699,46 @@ int dmf_fuse_counters_to_linear_device(dmf_volume* v, const int32_t* d_tiled, in
   DMF_API_END
 }
 
-int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth, const float* d_poses,
-                          int32_t P, const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses,
-                          uint64_t* d_stats) {
+int dmf_fuse_set_input_stream(dmf_volume* v, void* stream) {
   DMF_API_BEGIN
+  if (!v) return fail(DMF_ERR_INVALID, "null volume");
+  DMF_TRY(activate(v));
+  v->in_stream = (hipStream_t)stream;
+  v->pipelined = stream != nullptr;
+  return DMF_OK;
+  DMF_API_END
+}
+
+}  // extern "C"
+
+namespace dmf {
+// dmf_fuse_depth_device; allow_stage = false for the host form (its inputs are uploaded on
+// the volume's stream)
+static int fuse_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth, const float* d_poses, int32_t P,
+                       const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses, uint64_t* d_stats,
+                       bool allow_stage) {
   DMF_TRY(check_fuse(v, cam, P, prm));
   if (!d_depth || !d_poses || !d_hits || !d_misses) return fail(DMF_ERR_INVALID, "null device buffer");
-  PoseX* tab;
-  DMF_TRY(pose_table(v, d_poses, P, true, &tab));
   const CamP cp = cam_params(cam);
   const Geom g = v->geom();
-  unsigned long long* st = nullptr;
-  if (d_stats) DMF_TRY(stats_begin(v, &st));
-  const int pkx = (cp.W + 7) / 8;
   // default (variant 0): the brick-owned pipeline where it applies (longest axis 256-1024
   // cells), the LDS-box kernel k_fuse_l<12, 1280> otherwise
   const int fv = fuse_variant();
-  if (brick_path_ok(g) && (is_brick_variant(fv) || (fv == 0 && brick_preferred(g)))) {
+  const bool brick = brick_path_ok(g) && (is_brick_variant(fv) || (fv == 0 && brick_preferred(g)));
+  bool staged = false;
+  if (brick && allow_stage && v->pipelined) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    DMF_HIP(hipStreamIsCapturing(v->stream, &cs));
+    staged = cs == hipStreamCaptureStatusNone;
+  }
+  PoseX* tab = nullptr;
+  if (!staged) DMF_TRY(pose_table(v, d_poses, P, true, &tab));
+  unsigned long long* st = nullptr;
+  if (d_stats) DMF_TRY(stats_begin(v, &st));
+  const int pkx = (cp.W + 7) / 8;
+  if (brick) {
     g_last_kernel.store(variant_name(fv));
-    DMF_TRY(fuse_bricks(v, cp, g, d_depth, tab, P, prm, d_hits, d_misses, st));
+    DMF_TRY(fuse_bricks(v, cp, g, d_depth, tab, d_poses, P, prm, d_hits, d_misses, st, d_stats, staged));
     if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
     DMF_LAUNCH_CHECK();
     return DMF_OK;
@@ -2646,6 +2766,16 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
   DMF_LAUNCH_CHECK();
   return DMF_OK;
+}
+}  // namespace dmf
+
+extern "C" {
+
+int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth, const float* d_poses,
+                          int32_t P, const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses,
+                          uint64_t* d_stats) {
+  DMF_API_BEGIN
+  return fuse_device(v, cam, d_depth, d_poses, P, prm, d_hits, d_misses, d_stats, true);
   DMF_API_END
 }
 
@@ -2678,8 +2808,8 @@ int dmf_fuse_depth(dmf_volume* v, const dmf_camera* cam, const uint16_t* depth, 
   hipLaunchKernelGGL(k_counter_layout<false>, lg, dim3(256), 0, v->stream, g, (const int32_t*)lin, (int32_t*)dm, n);
   DMF_LAUNCH_CHECK();
   DMF_HIP(hipMemsetAsync(ds, 0, sizeof(uint64_t) * 8, v->stream));
-  DMF_TRY(dmf_fuse_depth_device(v, cam, (const uint16_t*)dd, (const float*)dp, P, prm, (int32_t*)dh, (int32_t*)dm,
-                                (uint64_t*)ds));
+  DMF_TRY(fuse_device(v, cam, (const uint16_t*)dd, (const float*)dp, P, prm, (int32_t*)dh, (int32_t*)dm,
+                      (uint64_t*)ds, false));
   uint64_t st[4];
   hipLaunchKernelGGL(k_counter_layout<true>, lg, dim3(256), 0, v->stream, g, (const int32_t*)dh, (int32_t*)lin, n);
   DMF_LAUNCH_CHECK();

@@ -53,6 +53,12 @@ enum ScratchSlot {
   // brick-owned fusion (dmf_fuse.hip)
   kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkWgBase, kScBkCtl, kScBkPoseCnt, kScBkPoseBase, kScBkBatch,
   kScBkWgList,
+  // the second staging slot of pipelined fusion (dmf_fuse_set_input_stream) and the
+  // per-slot pose tables / pass-A statistics
+  kScBkRays1, kScBkWgBase1, kScBkWgList1, kScBkPoseCnt1, kScBkBatch1, kScStPoses0, kScStPoses1, kScStStats0,
+  kScStStats1,
+  // ... and, when pass B is staged as well, the second slot's brick layout and pair records
+  kScBkBricks1, kScBkCtl1, kScBkPairs1, kScBkPairsB1, kScBkPoseBase1,
   kScOgP0, kScOgP1, kScOgFinal, kScOgOcc  // OccupancyGrid reorganization (dmf_ogrid.hip)
 };
 
@@ -72,6 +78,9 @@ __device__ inline unsigned long long* stat_slot(unsigned long long* base) {
 
 // Upload P host poses (or take device poses) and build the PoseX table on device.
 int pose_table(dmf_volume* v, const float* poses, int P, bool poses_on_device, PoseX** d_table);
+// The same table from P device poses into d_out, on stream s (the staging stream of a
+// pipelined fusion call).
+int pose_table_into(const float* d_poses, int P, PoseX* d_out, hipStream_t s);
 
 CamP cam_params(const dmf_camera* c);
 

@@ -240,6 +240,15 @@ struct dmf_volume {
   // brick fusion scratch budget (dmf_fuse_reserve)
   uint64_t bk_budget = 48ull << 30;  // set from the device's memory by dmf_volume_create
   uint32_t* bk_last_bt = nullptr;     // the batch table of the latest brick-pipeline super-batch (diagnostic)
+  // pipelined fusion (dmf_fuse_set_input_stream): pass A of a super-batch
+  // on the staging stream, into one of two slots
+  bool pipelined = false;
+  hipStream_t in_stream = nullptr;  // the caller's input stream
+  hipStream_t stage = nullptr;      // staging stream (created on first use)
+  hipEvent_t st_in = nullptr, st_done[2] = {nullptr, nullptr}, st_free[2] = {nullptr, nullptr};
+  hipEvent_t st_b[2] = {nullptr, nullptr};  // pass B of the slot's batch enqueued (staged pass B)
+  bool st_free_set[2] = {false, false};
+  int st_slot = 0;
   // scratch arena
   std::vector<std::pair<void*, size_t>> scratch;
 

@@ -147,6 +147,11 @@ class VoxelVolume:
     def set_stream(self, stream_ptr):
         check(self._L.dmf_volume_set_stream(self._h, stream_ptr))
 
+    def set_fuse_input_stream(self, stream_ptr):
+        """Pipelined fusion (dmf_fuse_set_input_stream): the device inputs of later fusion
+        calls are ordered on stream_ptr; None restores the serial order."""
+        check(self._L.dmf_fuse_set_input_stream(self._h, stream_ptr))
+
     def synchronize(self):
         check(self._L.dmf_volume_synchronize(self._h))
 

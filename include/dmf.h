@@ -242,6 +242,21 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
  * of the device's memory, ~96 GB on MI355X): a call whose pairs exceed the pair capacity
  * is cut into pose batches on the device (dmf_fuse_plan).  Synchronises the stream once. */
 int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t max_scratch_bytes);
+/* Pipelined fusion (an extension, the reference fuses one frame at a time,
+ * tests/Raytracing.cpp:70-76).  Declares that the device inputs (d_depth, d_poses) of later
+ * dmf_fuse_depth_device calls on this volume are ordered on `stream` (a hipStream_t the
+ * caller writes them on) instead of on the volume's stream.  The brick pipeline then runs
+ * each call's per-frame pass (pose table + pass A: back-projection, ray records, brick
+ * counts), its device-side batch cut and brick layout and its pass B (pair records) on a
+ * staging stream of the volume that waits only for `stream` and for its staging slot's
+ * previous reader, so that they overlap the previous call's phase F; only phase F stays on
+ * the volume's stream.  Two staging slots alternate between super-batches, each with its
+ * own pair records and half of the fusion budget (dmf_fuse_reserve).  `stream` is made to
+ * wait until the call's pass A has read the inputs, so inputs rewritten there afterwards
+ * stay ordered.  Results are identical to the serial order.  stream = NULL restores the serial order (the
+ * default); a volume stream that is capturing a graph always runs serially, and so does the
+ * host form dmf_fuse_depth. */
+int dmf_fuse_set_input_stream(dmf_volume* v, void* stream);
 /* How a fusion call of P frames of `cam`'s size on this volume is executed (no GPU work,
  * no allocation): brick = 1 for the brick-owned pipeline (k_bk_*), 0 for k_fuse_l.  The
  * brick pipeline runs pass A over super-batches of super_batch_poses frames; the DEVICE cuts
