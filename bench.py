@@ -128,7 +128,7 @@ def pmc_measure(args, log_dir=None):
     tmp = tempfile.mkdtemp(prefix="dmf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.abspath(__file__), "--pmc", "off", "--steps", "1", "--warmup", "0",
              "--cpu-frames", "0", "--grid", str(args.grid), "--poses-per-gpu", str(args.poses_per_gpu),
-             "--image", args.image] + (["--no-secondary"] if args.no_secondary else [])
+             "--image", args.image, "--serial-ref", "off"] + (["--no-secondary"] if args.no_secondary else [])
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     env.setdefault("TMPDIR", "/tmp")
     out = {}
@@ -233,6 +233,8 @@ def main():
                     help="auto: at N=1, measure HBM traffic and instruction counts of this workload with "
                          "rocprofv3 PMC passes (child runs) after the timed region")
     ap.add_argument("--pmc-dir", default=None, help="keep the rocprofv3 PMC output here")
+    ap.add_argument("--serial-ref", default="on", choices=["on", "off"],
+                    help="pipelined runs: re-time the serial fusion call after the timed region")
     ap.add_argument("--cpu-reverse-poses", type=int, default=16,
                     help="poses of the multi-core reverseRayTraceFast CPU sample (0 = skip both samples)")
     ap.add_argument("--image", default="640x480", choices=["640x480", "1280x720"],
@@ -392,7 +394,7 @@ def main():
     bytes_launch = BYTES_PER_UPDATE * upd_launch + BYTES_PER_DEPTH * P * HEIGHT * WIDTH
     ms = elapsed / args.steps * 1e3
     serial_ms = None
-    if pipe:
+    if pipe and args.serial_ref == "on":
         # pipelined calls overlap (pass A of call i+1 beside B and F of call i), so a call's own
         # event span is no duration: the fusion is priced over the whole step interval (which
         # also holds the overlapped finalize).  The serial call, timed alone, is reported beside.
@@ -408,6 +410,7 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize(dev)
         serial_ms = e0.elapsed_time(e1) / nser
+    if pipe:
         fuse_kernel_ms = ms
     else:
         fuse_kernel_ms = fuse_ms

@@ -2234,8 +2234,10 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   pl.per_pose_bytes = (uint64_t)rays_pose * sizeof(ulonglong2) + (uint64_t)pl.wg_pose * pl.hist_bytes +
                       (uint64_t)pl.wg_pose * sizeof(uint32_t) * (uint64_t)pl.wgl_stride + 2 * (uint64_t)pl.hist_bytes +
                       sizeof(unsigned long long) + sizeof(uint32_t);
-  // with pass B staged the two slots each hold pair records: each gets half the budget
-  const uint64_t budget = v->pipelined && stage_level() >= 2 ? v->bk_budget / 2 : v->bk_budget;
+  // with pass B staged the two slots each hold pair records: each gets three quarters of the
+  // budget (1.5x in all, ~144 GB of MI355X's 288 GB by default), so that the 1024^3 shard
+  // (2.85G pairs) and the 1024-pose 512^3 anchor (2.0G) still run as one batch per slot
+  const uint64_t budget = v->pipelined && stage_level() >= 2 ? v->bk_budget / 4 * 3 : v->bk_budget;
   pl.PS = std::min<int64_t>(P, (int64_t)(budget / 2 / pl.per_pose_bytes));
   if (const char* e = getenv("DMF_BK_SUPER_POSES")) {  // test hook: cap the poses per super-batch
     const int64_t c = (int64_t)atoll(e);

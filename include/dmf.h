@@ -251,7 +251,7 @@ int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t m
  * staging stream of the volume that waits only for `stream` and for its staging slot's
  * previous reader, so that they overlap the previous call's phase F; only phase F stays on
  * the volume's stream.  Two staging slots alternate between super-batches, each with its
- * own pair records and half of the fusion budget (dmf_fuse_reserve).  `stream` is made to
+ * own pair records and three quarters of the fusion budget (dmf_fuse_reserve).  `stream` is made to
  * wait until the call's pass A has read the inputs, so inputs rewritten there afterwards
  * stay ordered.  Results are identical to the serial order.  stream = NULL restores the serial order (the
  * default); a volume stream that is capturing a graph always runs serially, and so does the
