@@ -777,6 +777,14 @@ __global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t*
 //                   counter).  No device atomic per update.
 namespace bk = dmf::brick;
 
+// Wave issue priority (s_setprio) of a staged pass-A / pass-B wave that shares its CU with
+// phase F (pipelined calls): the SIMD arbiter prefers higher-priority waves.
+__device__ inline void wave_prio(int p) {
+  if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p >= 3) __builtin_amdgcn_s_setprio(3);
+}
+
 struct BkGeom {
   int nb[3];    // bricks per axis
   int nbricks;
@@ -826,6 +834,7 @@ __device__ inline void bk_coarse(const BkGeom& bg, const bk::QRay& R, F&& f) {
 // name the same brick at the same coarse step, so one atomic per distinct brick among
 // the active lanes replaces a same-address atomic per lane (which the LDS serialises).
 // Callable from divergent code: the loop runs over the currently active lanes.
+template <bool H16 = false>
 __device__ inline void hist_add_agg(uint32_t* hist, int b) {
   uint64_t rem = __builtin_amdgcn_ballot_w64(true);
   const int l = (int)(threadIdx.x & 63);
@@ -833,7 +842,10 @@ __device__ inline void hist_add_agg(uint32_t* hist, int b) {
     const int leader = __builtin_ctzll(rem);
     const int bl = __builtin_amdgcn_readlane(b, leader);
     const uint64_t same = __builtin_amdgcn_ballot_w64(b == bl) & rem;
-    if (l == leader) atomicAdd(&hist[bl], (uint32_t)__builtin_popcountll(same));
+    if (l == leader) {
+      if constexpr (H16) atomicAdd(&hist[bl >> 1], (uint32_t)__builtin_popcountll(same) << ((bl & 1) << 4));
+      else atomicAdd(&hist[bl], (uint32_t)__builtin_popcountll(same));
+    }
     rem &= ~same;
   }
 }
@@ -863,6 +875,11 @@ __device__ inline uint32_t hist_take_agg(uint32_t* hist, int b) {
 // count is wg_base[wg][b]) and per pose: pose_pairs[p], so that the device can cut the
 // call into pose batches by the pairs they really make (k_bk_batches) and any batch's
 // per-brick lists can be laid out (k_bk_batch_counts) without re-running this pass.
+// H16: the histogram holds two 16-bit counts per word (brick b in half b & 1 of word b >> 1:
+// a workgroup's rays make at most span * 64 <= 65535 pairs in one brick).  Half the LDS, so
+// that two pass-A workgroups fit beside phase F's box on a CU when calls are pipelined
+// (DESIGN.md §5.10).
+template <bool H16>
 __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam, const uint16_t* __restrict__ depth,
                                                         const PoseX* __restrict__ poses, int dmin, int dmax,
                                                         int packets_x, int packets_pose, int wg_pose, int span,
@@ -871,12 +888,14 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
                                                         uint32_t* __restrict__ wg_base,
                                                         uint32_t* __restrict__ wg_list, int wgl_stride,
                                                         unsigned long long* __restrict__ pose_pairs,
-                                                        unsigned long long* __restrict__ stats) {
+                                                        unsigned long long* __restrict__ stats, int prio) {
   extern __shared__ uint32_t hist[];
   __shared__ uint32_t nlist;
+  wave_prio(prio);
   stats = stat_slot(stats);
   if (threadIdx.x == 0) nlist = 0;
-  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = 0;
+  const int nwords = H16 ? (bg.nbricks + 1) >> 1 : bg.nbricks;
+  for (int i = threadIdx.x; i < nwords; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int pw = (int)(blockIdx.x / (unsigned)wg_pose);
@@ -908,7 +927,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
       bk::decode_ray(A, B, R);
       upd += (unsigned long long)(R.nsteps + 1);
       nhit += inside ? 1 : 0;
-      bk_coarse(bg, R, [&](int b, int, int, int, int) { hist_add_agg(hist, b); });
+      bk_coarse(bg, R, [&](int b, int, int, int, int) { hist_add_agg<H16>(hist, b); });
     }
     nvalid += valid ? 1 : 0;
     rays[pk * 64 + l] = rec;
@@ -920,7 +939,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
   uint16_t* const ids = (uint16_t*)(row + 1);
   unsigned long long mine = 0;
   for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) {
-    const uint32_t n = hist[i];
+    const uint32_t n = H16 ? (hist[i >> 1] >> ((i & 1) << 4)) & 0xffffu : hist[i];
     if (n) {
       wg_base[(size_t)blockIdx.x * bg.nbricks + i] = atomicAdd(&pc[i], n);
       ids[atomicAdd(&nlist, 1u)] = (uint16_t)i;
@@ -941,7 +960,9 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
 __global__ __launch_bounds__(1024) void k_bk_batches(int P, const unsigned long long* __restrict__ pose_pairs,
                                                      unsigned long long cap, int max_poses,
                                                      uint32_t* __restrict__ bt) {
-  constexpr int kChunk = 4096;  // pose counts staged in LDS per round (32 KiB)
+  // pose counts staged in LDS per round (8 KiB: with pipelined calls this kernel runs beside
+  // phase F, whose box leaves ~25 KiB of the CU's LDS)
+  constexpr int kChunk = 1024;
   __shared__ unsigned long long spp[kChunk];
   uint32_t J = 0;
   unsigned long long sum = 0;
@@ -1007,6 +1028,10 @@ __global__ __launch_bounds__(256) void k_bk_batch_counts(int nbricks, int j, con
 // queue hands out the big parts first, so the parts left when the queue runs dry are the
 // small ones (the CUs finish together; counter sums do not depend on the order), and F
 // needs no search of part_pref for the brick of a part.
+// BIG (over 4096 bricks): the counts are staged in LDS (128 KiB); otherwise they are read
+// from memory (4 per lane at 512^3) and the kernel's ~12 KiB of LDS fit beside phase F's box
+// (pipelined calls).
+template <bool BIG>
 __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* __restrict__ cnt,
                                                   uint32_t* __restrict__ off,
                                                   uint32_t* __restrict__ part_pref,
@@ -1022,10 +1047,12 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
   __shared__ uint32_t s_cls[64];
   // the counts, loaded once with coalesced reads (the brick path has <= 32^3 bricks): the
   // per-thread brick ranges below then read LDS, not dependent HBM loads (1024^3: 0.18 ms)
-  __shared__ uint32_t s_cnt[kBkScanMax];
+  __shared__ uint32_t s_cnt_lds[BIG ? kBkScanMax : 1];
+  const uint32_t* const s_cnt = BIG ? s_cnt_lds : cnt;
   const int t = threadIdx.x;
   if (t < 64) s_cls[t] = 0;
-  for (int i = t; i < nbricks; i += 1024) s_cnt[i] = cnt[i];
+  if constexpr (BIG)
+    for (int i = t; i < nbricks; i += 1024) s_cnt_lds[i] = cnt[i];
   __syncthreads();
   const int per = (nbricks + 1023) / 1024;
   const int i0 = min(nbricks, t * per), i1 = min(nbricks, i0 + per);
@@ -1149,8 +1176,9 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
                                                          const uint32_t* __restrict__ wg_base,
                                                          const uint32_t* __restrict__ bt, int j,
                                                          const uint32_t* __restrict__ wg_list, int wgl_stride,
-                                                         uint4* __restrict__ pa, void* __restrict__ pbv) {
+                                                         uint4* __restrict__ pa, void* __restrict__ pbv, int prio) {
   static_assert(SLAB || !R20, "the 20-byte record carries the slab state");
+  wave_prio(prio);
   uint2* const pb = (uint2*)pbv;
   uint32_t* const pw = (uint32_t*)pbv;
   extern __shared__ uint32_t hist[];
@@ -2272,7 +2300,8 @@ static int bk_attributes() {
   static std::atomic<bool> attr_set{false};
   if (!attr_set.load()) {
     const int lds = (int)(sizeof(uint32_t) * 32768);
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -2376,6 +2405,16 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   // staged pass B (DMF_BK_STAGE=2): the batch cut, brick layout and pass B run on the staging
   // stream too, into the slot's own pair records; only phase F stays on the volume's stream
   const bool stage_b = staged && stage_level() >= 2;
+  // issue priority of the staged passes' waves (A/B: DMF_BK_PRIO 0-3)
+  const int prio = [&] {
+    const char* e = getenv("DMF_BK_PRIO");
+    return staged ? (e ? std::max(0, std::min(atoi(e), 3)) : 0) : 0;
+  }();
+  // pass A with 16-bit histogram counts (a workgroup's pairs per brick <= span * 64 rays)
+  const bool a16 = (int64_t)pl.span * 64 <= 65535 && [] {
+    const char* e = getenv("DMF_BK_A16");  // A/B: 0 = 32-bit counts
+    return !(e && atoi(e) == 0);
+  }();
   const unsigned nf = (unsigned)cu_count(v->device);
   const int fv = fuse_variant();
   const bool lpt_on = [] {  // A/B: DMF_BK_LPT=0 hands the parts out in brick order
@@ -2413,9 +2452,16 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     }
     DMF_HIP(hipMemsetAsync(b.pose_cnt, 0, pl.hist_bytes * (size_t)ps, sa));
     DMF_HIP(hipMemsetAsync(b.pose_pairs, 0, sizeof(unsigned long long) * (size_t)ps, sa));
-    hipLaunchKernelGGL(k_bk_rays, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, g, cp,
-                       d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
-                       pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st_a);
+    if (a16)
+      hipLaunchKernelGGL(k_bk_rays<true>, dim3(nwg), dim3(pl.ab_threads), sizeof(uint32_t) * ((bg.nbricks + 1) / 2), sa,
+                         g, cp, d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx,
+                         (int)pl.ppose, pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride,
+                         b.pose_pairs, st_a, prio);
+    else
+      hipLaunchKernelGGL(k_bk_rays<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, g, cp,
+                         d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
+                         pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st_a,
+                         prio);
     DMF_LAUNCH_CHECK();
     if (staged) {
       DMF_HIP(hipEventRecord(v->st_done[slot], sa));
@@ -2436,14 +2482,18 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sl, bg.nbricks,
                          (int)j, (const uint32_t*)b.bt, (const uint32_t*)b.pose_cnt, b.pose_base, b.cnt);
       DMF_LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(1024), 0, sl, bg.nbricks, (const uint32_t*)b.cnt, b.off, b.part_pref,
-                         b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
+      if (bg.nbricks > 4096)
+        hipLaunchKernelGGL(k_bk_scan<true>, dim3(1), dim3(1024), 0, sl, bg.nbricks, (const uint32_t*)b.cnt, b.off,
+                           b.part_pref, b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
+      else
+        hipLaunchKernelGGL(k_bk_scan<false>, dim3(1), dim3(1024), 0, sl, bg.nbricks, (const uint32_t*)b.cnt, b.off,
+                           b.part_pref, b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       DMF_LAUNCH_CHECK();
 #define DMF_BK_PAIRS(...)                                                                                          \
   hipLaunchKernelGGL((k_bk_pairs<__VA_ARGS__>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sl, (int)pl.ppose,  \
                      pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off,                   \
                      (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,             \
-                     tlist ? (const uint32_t*)b.wgl : nullptr, pl.wgl_stride, b.pra, b.prb)
+                     tlist ? (const uint32_t*)b.wgl : nullptr, pl.wgl_stride, b.pra, b.prb, prio)
       if (fv == 48)  // wave-aggregated slot atomics (the previous default)
         DMF_BK_PAIRS(true, true);
       else if (fv == 65)
