@@ -761,6 +761,7 @@ int dmf_volume_destroy(dmf_volume* v) {
   for (hipEvent_t e : {v->st_in, v->st_done[0], v->st_done[1], v->st_free[0], v->st_free[1], v->st_b[0], v->st_b[1]})
     if (e) (void)hipEventDestroy(e);
   if (v->stage) (void)hipStreamDestroy(v->stage);
+  if (v->stage1) (void)hipStreamDestroy(v->stage1);
   delete v;
   return DMF_OK;
   DMF_API_END

@@ -1693,7 +1693,11 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
 // POOL (20-B records, NSLOT 1): a wave takes pair indices from its own pool of 64, grabbed
 // from the part's LDS counter one refill AHEAD (the grab's latency, which waits for the
 // wave's queued walk adds, hides behind the next walk block instead of stalling the refill).
-template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, bool BL = false, bool R20 = false, bool POOL = false>
+// W0D (A/B, variant 67): a slab's first add (owned iff r > t, false only on a pair's last block
+// and on idle lanes) goes unmasked to the lane's dummy word when not owned: two SALU exec-mask
+// instructions fewer per slab for one LDS add per idle lane.
+template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, bool BL = false, bool R20 = false, bool POOL = false,
+          bool W0D = false>
 __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, const uint4* __restrict__ pa,
                                                           const void* __restrict__ pbv,
                                                           const uint32_t* __restrict__ off,
@@ -2018,7 +2022,8 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
             if (w2) atomicAdd((uint32_t*)(lds + dw), 1u);
           }
 #else
-          if (w0) atomicAdd((uint32_t*)(lds + cur[q]), 1u);
+          if constexpr (W0D) atomicAdd((uint32_t*)(lds + (w0 ? cur[q] : (uint32_t)(kBkBoxWords + 4 + l) * 4u)), 1u);
+          else if (w0) atomicAdd((uint32_t*)(lds + cur[q]), 1u);
           if (w1) atomicAdd((uint32_t*)(lds + p1), 1u);
           if (w2) atomicAdd((uint32_t*)(lds + p2), 1u);
 #endif
@@ -2154,7 +2159,7 @@ static int fuse_variant() {
 }
 constexpr int kVariantBrick = 40;
 constexpr int kVariantSlab = 44;  // 44..53: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
-constexpr int kVariantLast = 66;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
+constexpr int kVariantLast = 67;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
 constexpr int kVariantRec20 = 57;  // the default: 20-B pair records (beta state, dmf_brick.hpp pack20)
 // 57-63: 20-B records (57 = the default <24, 32, 4>; 58-63 refill / spread / unroll A/B)
 static bool is_rec20_variant(int v) { return v == 0 || (v >= kVariantRec20 && v <= kVariantLast); }
@@ -2380,9 +2385,15 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b, int slot = 0, 
 // stay ordered before the caller's next writes).  Pass A's statistics go to the slot's own
 // striped buffer, summed into d_user on the volume's stream.
 
+static int stage_streams() {
+  const char* e = getenv("DMF_BK_STAGE_STREAMS");
+  return e && atoi(e) == 2 ? 2 : 1;
+}
+
 static int stage_init(dmf_volume* v) {
   if (v->stage) return DMF_OK;
   DMF_HIP(hipStreamCreateWithFlags(&v->stage, hipStreamNonBlocking));
+  DMF_HIP(hipStreamCreateWithFlags(&v->stage1, hipStreamNonBlocking));
   DMF_HIP(hipEventCreateWithFlags(&v->st_in, hipEventDisableTiming));
   for (int k = 0; k < 2; ++k) {
     DMF_HIP(hipEventCreateWithFlags(&v->st_done[k], hipEventDisableTiming));
@@ -2431,7 +2442,9 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     const int slot = staged ? v->st_slot : 0;
     DMF_TRY(bk_scratch(v, pl, b, slot, stage_b));
     const uint2* lpt = lpt_on ? b.order : nullptr;  // (the tail split needs the order: bk_plan)
-    const hipStream_t sa = staged ? v->stage : v->stream;
+    // one staging stream, or one per slot (A/B DMF_BK_STAGE_STREAMS=2: a slot's pass A may
+    // then start as soon as the slot is free, beside the other slot's pass B)
+    const hipStream_t sa = staged ? (slot && stage_streams() == 2 ? v->stage1 : v->stage) : v->stream;
     const PoseX* tab_a = staged ? nullptr : tab + s0;
     unsigned long long* st_a = st;
     if (staged) {
@@ -2469,7 +2482,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       DMF_HIP(hipStreamWaitEvent(v->in_stream, v->st_done[slot], 0));
       if (st) DMF_TRY(stats_end(v, st_a, d_user, kStatWidth));
     }
-    const hipStream_t sl = stage_b ? v->stage : v->stream;  // batch cut, brick layout, pass B
+    const hipStream_t sl = stage_b ? sa : v->stream;  // batch cut, brick layout, pass B
     hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sl, (int)ps, (const unsigned long long*)b.pose_pairs,
                        (unsigned long long)pl.pair_cap, pl.max_poses, b.bt);
     DMF_LAUNCH_CHECK();
@@ -2557,6 +2570,12 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                              bg, (const uint4*)b.pra, (const void*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
                              (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st);
           break;
+        case 67:
+          hipLaunchKernelGGL((k_bk_fuse_s<24, 32, 4, 1, false, true, false, true>), dim3(nf), dim3(kBkThreads), 0,
+                             v->stream, g, bg, (const uint4*)b.pra, (const void*)b.prb, (const uint32_t*)b.off,
+                             (const uint32_t*)b.cnt, (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits,
+                             d_misses, st);
+          break;
         default: DMF_BK_FUSE_S20(24, 32, 4, 1); break;  // 0, 57
       }
 #undef DMF_BK_FUSE
@@ -2643,6 +2662,7 @@ static const char* variant_name(int v) {
     case 62: return "dmf::k_bk_fuse_s<24, 32, 3, 1, false, true>";
     case 63: return "dmf::k_bk_fuse_s<24, 32, 5, 1, false, true>";
     case 64: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true, true>";
+    case 67: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true, false, true>";
     case 53: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false>";
     default: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true>";  // 0, 57; grids over 1024 cells per axis: k_fuse_l<12, 1280>
   }

@@ -245,6 +245,7 @@ struct dmf_volume {
   bool pipelined = false;
   hipStream_t in_stream = nullptr;  // the caller's input stream
   hipStream_t stage = nullptr;      // staging stream (created on first use)
+  hipStream_t stage1 = nullptr;     // slot 1's own staging stream (DMF_BK_STAGE_STREAMS=2)
   hipEvent_t st_in = nullptr, st_done[2] = {nullptr, nullptr}, st_free[2] = {nullptr, nullptr};
   hipEvent_t st_b[2] = {nullptr, nullptr};  // pass B of the slot's batch enqueued (staged pass B)
   bool st_free_set[2] = {false, false};

@@ -580,7 +580,7 @@ def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
             L.dmf_device_free(h, p_)
 
 
-@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63, 64, 65, 66])
+@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63, 64, 65, 66, 67])
 def brick_variant(dmf, request):
     """Select a brick-owned fusion variant for one test: DMF_FUSE_VARIANT 40-43 = the
     per-cell walk (k_bk_fuse: refill threshold, pair order, interleaving), 44-51 = the
