@@ -96,9 +96,10 @@ def test_pipelined_equals_serial_256(monkeypatch, case, stage):
     hs, ms, ss = _run(256, poses, depth, 3, pipelined=False)
     hp, mp, sp = _run(256, poses, depth, 3, pipelined=True)
     assert ss[0] > 10 ** 7 and ss[3] == 0
-    # stats[6] (flushed cells) depends on which pairs share a part, i.e. on the order of the
-    # slot atomics of pass B: it varies run to run in either mode; the rest is exact
-    assert np.array_equal(ss[:6], sp[:6])
+    # stats[5] (parts) differs by design: serial calls cut the part queue's tail (k_bk_scan),
+    # pipelined ones do not; stats[6] (flushed cells) depends on which pairs share a part, i.e.
+    # on the order of pass B's slot atomics, and varies run to run in either mode
+    assert np.array_equal(ss[:5], sp[:5])
     assert np.array_equal(hs, hp) and np.array_equal(ms, mp)
 
 
