@@ -43,6 +43,11 @@ if kernels:
     # the PMC passes run their own (shorter) bench command: count its calls, not the trace's
     pmc_bench = json.load(open(sorted(glob.glob(os.path.join(src, "pmc*.json")))[0]))
     calls = int(pmc_bench["steps"]) + int(pmc_bench["warmup"])
+    # a pipelined bench also re-times the serial call after its timed region (roofline.
+    # serial_call_ms): count the phase-F dispatches instead (one per call and batch)
+    fk = [k for k in kernels if k.startswith(("dmf::k_bk_fuse", "dmf::k_fuse"))]
+    if fk and (pmc_bench.get("roofline") or {}).get("serial_call_ms"):
+        calls = max(len(ndisp[(fk[0], c)]) for (k, c) in tot if k == fk[0])
 
     def per(k, c):
         return tot.get((k, c), 0.0) / max(calls, 1)

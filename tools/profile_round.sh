@@ -15,7 +15,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 i=0
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" "SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 400 rocprofv3 --pmc $pmc --output-format csv -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-frames 0 --no-secondary --pmc off ${BENCHARGS} > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || exit 2
+  timeout -k 10 400 rocprofv3 --pmc $pmc --output-format csv -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-frames 0 --no-secondary --pmc off --serial-ref off ${BENCHARGS} > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || exit 2
 done
 # extra counter groups (";"-separated in $EXTRA_PMC); counters the box does not list are dropped
 if [ -n "$EXTRA_PMC" ]; then
@@ -29,7 +29,7 @@ if [ -n "$EXTRA_PMC" ]; then
     done
     [ -z "$keep" ] && continue
     i=$((i+1))
-    timeout -s KILL 120 rocprofv3 --pmc $keep --output-format csv -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-frames 0 --no-secondary --pmc off ${BENCHARGS} > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || exit 2
+    timeout -s KILL 120 rocprofv3 --pmc $keep --output-format csv -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-frames 0 --no-secondary --pmc off --serial-ref off ${BENCHARGS} > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || exit 2
   done
 fi
 python3 tools/pmc_summary.py "$OUT" "profiles/$TAG" || exit 3
