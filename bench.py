@@ -128,7 +128,8 @@ def pmc_measure(args, log_dir=None):
     tmp = tempfile.mkdtemp(prefix="dmf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.abspath(__file__), "--pmc", "off", "--steps", "1", "--warmup", "0",
              "--cpu-frames", "0", "--grid", str(args.grid), "--poses-per-gpu", str(args.poses_per_gpu),
-             "--image", args.image, "--serial-ref", "off"] + (["--no-secondary"] if args.no_secondary else [])
+             "--image", args.image, "--serial-ref", "off", "--cpu-reverse-poses", "0"] + (
+                 ["--no-secondary"] if args.no_secondary else [])
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     env.setdefault("TMPDIR", "/tmp")
     out = {}
@@ -151,6 +152,21 @@ def pmc_measure(args, log_dir=None):
                     e = out.setdefault(k, {}).setdefault(row["Counter_Name"], [0.0, set()])
                     e[0] += float(row["Counter_Value"])
                     e[1].add(row["Dispatch_Id"])
+        # kernel durations of the same workload in its timed mode (a short pipelined run): the
+        # per-kernel averages beside the step interval, F's among them
+        d = os.path.join(tmp, "kt")
+        kt_child = [c if c != "1" or child[i - 1] != "--steps" else "20" for i, c in enumerate(child)]
+        cmd = [prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "run", "--"] + kt_child
+        r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, timeout=300)
+        kt = {}
+        if r.returncode == 0:
+            for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
+                for row in csv.DictReader(open(f)):
+                    k = row["Name"].split("(")[0].replace("void ", "").strip()
+                    if k.startswith("dmf::"):
+                        kt[k] = {"avg_ms": float(row["AverageNs"]) * 1e-6, "calls": int(row["Calls"])}
+        else:
+            log(f"kernel-trace pass failed ({r.returncode}): {r.stderr.decode(errors='replace')[-400:]}")
         if log_dir:
             shutil.copytree(tmp, log_dir, dirs_exist_ok=True)
     except (OSError, subprocess.SubprocessError, ValueError, KeyError) as ex:
@@ -158,7 +174,9 @@ def pmc_measure(args, log_dir=None):
         return None
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    return {k: {c: (v[0], len(v[1])) for c, v in cs.items()} for k, cs in out.items()}
+    res = {k: {c: (v[0], len(v[1])) for c, v in cs.items()} for k, cs in out.items()}
+    res["__kernel_trace__"] = kt
+    return res
 
 
 def under_profiler():
@@ -206,6 +224,39 @@ def one_rccl_mapped():
         return False
     paths = {ln.split()[-1] for ln in maps if "librccl" in ln}
     return len(paths) == 1
+
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "fusion_digests.json")
+
+
+def expected_digest(grid, P_total):
+    """The oracle's log-odds digest of this run's GLOBAL pose set (fibonacci_poses(P_total,
+    seed=1234), bench make_inputs) at full size, committed by tests/golden/gen_fusion_digests.py,
+    or None when that workload was not generated."""
+    try:
+        table = json.load(open(GOLDEN))
+    except (OSError, ValueError):
+        return None
+    for key, e in table.items():
+        if (e["grid"], e["image"], e["global_poses"], e["seed"]) == (grid, f"{WIDTH}x{HEIGHT}", P_total, 1234):
+            return dict(e, key=key)
+    return None
+
+
+def host_cores():
+    """The GPU box host's CPUs as the OS reports them (nproc / lscpu), beside the threads the
+    CPU baselines used (the job's share, host_threads)."""
+    info = {"os_cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        out = subprocess.run(["lscpu"], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=10,
+                             text=True).stdout
+        for ln in out.splitlines():
+            k, _, v = ln.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)"):
+                info[k.strip()] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
 
 
 def host_threads():
@@ -309,12 +360,30 @@ def main():
     # or the plain finalize (N = 1: no collective).
     merge_mode = os.environ.get("DMF_BENCH_MERGE", "rs")
     comm_ptr = None
+    rccl = {"ranks": None, "merge": "finalize only (N = 1, no collective)" if world == 1 else None,
+            "fallback_reason": None}
     if world > 1:
         dist.barrier()  # connects the RCCL communicator
-        if backend == "nccl" and merge_mode == "rs" and one_rccl_mapped():
+        if backend != "nccl":
+            rccl["fallback_reason"] = f"DMF_BENCH_BACKEND={backend}"
+        elif merge_mode != "rs":
+            rccl["fallback_reason"] = f"DMF_BENCH_MERGE={merge_mode}"
+        elif not one_rccl_mapped():
+            rccl["fallback_reason"] = "more than one librccl mapped: libdmf cannot use torch's communicator"
+        if rccl["fallback_reason"] is None:
             comm_ptr = D.torch_comm_ptr(device=dev)
+            nr, rk = C.c_int32(), C.c_int32()
+            _lib.check(L.dmf_comm_shape(comm_ptr, C.addressof(nr), C.addressof(rk)))
+            rccl["ranks"] = nr.value
+            if nr.value != world or rk.value != rank:
+                raise RuntimeError(f"RCCL communicator spans {nr.value} ranks (rank {rk.value}), world {world} "
+                                   f"rank {rank}")
+            rccl["merge"] = ("libdmf dmf_fuse_merge_finalize_device: RCCL ncclReduceScatter(hits, misses) + slab "
+                             "finalize + ncclAllGather(int16) on torch's communicator")
         else:
             merge_mode = "torch"
+            rccl["merge"] = (f"fallback: torch.distributed all_reduce(sum) over {backend} + finalize of the "
+                             "world-padded grid")
     bufs = [torch.zeros(2 * npad, dtype=torch.int32, device=dev) for _ in range(2)]
     rt = S.TorchRuntime(dev)  # the volume stays on the compute stream; merges name theirs
     ev = {}
@@ -410,11 +479,12 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize(dev)
         serial_ms = e0.elapsed_time(e1) / nser
-    if pipe:
-        fuse_kernel_ms = ms
-    else:
-        fuse_kernel_ms = fuse_ms
-    achieved = bytes_launch / (fuse_kernel_ms * 1e-3) / 1e9
+    # the time the fusion's algorithmic bytes are priced over: the step interval when the calls
+    # are pipelined (they overlap: no per-call duration), the call's HIP-event span when serial
+    step_ms = ms if pipe else fuse_ms
+    achieved = bytes_launch / (step_ms * 1e-3) / 1e9
+    digest = hashlib.sha256(logodds[:ncell].cpu().numpy().tobytes()).hexdigest()[:16]
+    golden = expected_digest(grid, P * world)
 
     result = None
     if rank == 0:
@@ -434,9 +504,9 @@ def main():
             cpu_mt = {"value": ups_mt, "unit": "ray-voxel updates/s", "cores": nt, "kind": "port",
                       "sample": f"oracle fuse (OpenMP rows, atomic counters) of {nf} of the {P} frames, "
                                 f"{dt_mt:.1f}s on {nt} threads; Mrays/s {rps_mt / 1e6:.3f}"}
-        kname = L.dmf_fuse_kernel().decode()
+        kname = _lib.kernel_name(vol)
         if kname.startswith("dmf::k_bk_fuse"):
-            # brick-owned pipeline: kernel_ms spans every launch of the call
+            # brick-owned pipeline: step_ms spans every launch of the call
             # (A, the device-side batch cut, and per pose batch S, B, F)
             pipeline = ["dmf::k_bk_rays", "dmf::k_bk_batches", "dmf::k_bk_batch_counts", "dmf::k_bk_scan",
                         "dmf::k_bk_pairs", kname]
@@ -492,19 +562,33 @@ def main():
                                   + "; the brick pipeline accumulates in LDS, so these bytes are a price, not its "
                                     "HBM traffic",
                          "measured_frac": None, "traffic_source": None,
-                         "kernel": kname, "kernel_ms": fuse_kernel_ms, "pipeline": pipeline,
+                         "kernel": kname, "step_ms": step_ms,
+                         "step_ms_basis": ("elapsed / steps of the pipelined calls (each step also holds the "
+                                           "overlapped finalize)" if pipe else "HIP events around the serial fusion call"),
+                         "kernel_avg_ms": None,  # per-kernel averages from a rocprofv3 --kernel-trace child (attach_pmc)
+                         "f_kernel_ms": None,
+                         "companion": None,      # the valu-issue bound that binds the pipeline (attach_pmc)
+                         "pipeline": pipeline,
                          "pipelined": pipe, "serial_call_ms": serial_ms,
                          "serial_call_frac": (bytes_launch / (serial_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
                                               if serial_ms else None),
                          "updates_per_launch": upd_launch, "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,
+            "host_cores": host_cores(),
             "step_breakdown_ms": breakdown,
             "streaming": streaming,
             "secondary": secondary,
-            # the merged grid after the last step (the same poses every step): equal digests
-            # at N = 1 and N > 1 over the same global poses show the merge is exact
-            "logodds_digest": hashlib.sha256(logodds[:ncell].cpu().numpy().tobytes()).hexdigest()[:16],
+            # the merged grid after the last step (the same poses every step) against the oracle's
+            # digest of the same global poses (tests/golden/gen_fusion_digests.py): the line checks
+            # its own exactness at N = 1 and, over the merge, at N > 1
+            "logodds_digest": digest,
+            "digest_expected": golden["logodds_digest"] if golden else None,
+            "digest_match": (digest == golden["logodds_digest"]) if golden else None,
+            "digest_source": (f"oracle (CPU restatement) fusion of the {P * world} global poses, "
+                              f"tests/golden/fusion_digests.json[{golden['key']}]") if golden else
+                             "no committed oracle digest for this workload",
+            "rccl": rccl,
         }
     if dist.is_initialized():
         dist.barrier()
@@ -526,20 +610,39 @@ def attach_pmc(result, pmc):
     if not pmc:
         rf["traffic_source"] = "not measured (rocprofv3 unavailable or a PMC pass failed)"
         return
+    kt = pmc.pop("__kernel_trace__", {}) or {}
     fk = [k for k in pmc if k.startswith(("dmf::k_bk_", "dmf::k_fuse"))]
     calls = 1  # the child run makes one fusion call (steps 1, warmup 0)
     fetch, write = pmc_total(pmc, fk, "FETCH_SIZE"), pmc_total(pmc, fk, "WRITE_SIZE")
     traffic = 1024.0 * (2.0 * fetch + write) / calls
     valu = pmc_total(pmc, fk, "SQ_INSTS_VALU") / calls
     rf["traffic"] = traffic
-    rf["measured_frac"] = traffic / (rf["kernel_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+    rf["measured_frac"] = traffic / (rf["step_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+    if kt:
+        rf["kernel_avg_ms"] = {k: round(v["avg_ms"], 4) for k, v in sorted(kt.items())}
+        fkey = [k for k in kt if k.startswith("dmf::k_bk_fuse") or k.startswith("dmf::k_fuse_l")]
+        if fkey:
+            rf["f_kernel_ms"] = kt[fkey[0]]["avg_ms"]
+            rf["f_kernel"] = fkey[0]
+        rf["kernel_avg_source"] = ("rocprofv3 --kernel-trace --stats of the same workload, 20 steps in the timed "
+                                   "mode (child run): passes A and B run beside the previous call's F when "
+                                   "pipelined, so their averages include the stretch")
+    fvalu = pmc_per_dispatch(pmc, rf.get("f_kernel") or "", "SQ_INSTS_VALU") if rf.get("f_kernel") else None
+    rf["companion"] = {
+        "bound": "valu-issue", "achieved": valu / (rf["step_ms"] * 1e-3), "peak": VALU_PEAK_WIPS,
+        "unit": "wave-instr/s", "frac": valu / (rf["step_ms"] * 1e-3) / VALU_PEAK_WIPS,
+        "valu_per_call": valu, "lane_slots_per_update": valu * 64.0 / max(rf["updates_per_launch"], 1.0),
+        "f_valu_per_launch": fvalu,
+        "f_frac": (fvalu / (rf["f_kernel_ms"] * 1e-3) / VALU_PEAK_WIPS) if fvalu and rf.get("f_kernel_ms") else None,
+        "basis": "what binds the pipeline: SQ_INSTS_VALU of every fusion kernel per call (PMC child) over the step "
+                 "interval, vs 1024 SIMD-32 x one wave64 VALU instruction per 2 cycles at 2.4 GHz"}
     rf["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes of this configuration (child runs after "
                             "the timed region), (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per fusion call, summed over "
                             + ", ".join(sorted(fk)))
     rf["per_kernel_hbm_bytes"] = {k: 1024.0 * (2.0 * pmc_total(pmc, [k], "FETCH_SIZE") + pmc_total(pmc, [k], "WRITE_SIZE"))
                                   / calls for k in sorted(fk)}
     rf["valu_per_launch"] = valu
-    rf["valu_issue_frac"] = valu / (rf["kernel_ms"] * 1e-3) / VALU_PEAK_WIPS
+    rf["valu_issue_frac"] = rf["companion"]["frac"]
     rf["valu_lane_slots_per_update"] = valu * 64.0 / max(rf["updates_per_launch"], 1.0)
     sec = result.get("secondary") or {}
     for name, prefix in (("reverse_ray_trace_fast", "dmf::k_reverse_q"), ("forward_first_hits", "dmf::k_forward")):

@@ -132,6 +132,17 @@ int dmf_comm_init_rank(void** comm, int32_t nranks, const void* id, int32_t rank
   DMF_API_END
 }
 
+int dmf_comm_shape(void* comm, int32_t* nranks, int32_t* rank) {
+  DMF_API_BEGIN
+  if (!nranks || !rank) return fail(DMF_ERR_INVALID, "null argument");
+  int nr = 0, rk = 0;
+  DMF_TRY(comm_shape(comm, &nr, &rk));
+  *nranks = nr;
+  *rank = rk;
+  return DMF_OK;
+  DMF_API_END
+}
+
 int dmf_comm_destroy(void* comm) {
   DMF_API_BEGIN
   if (!comm) return DMF_OK;
@@ -240,9 +251,18 @@ int dmf_flags_allreduce(dmf_volume* v, void* comm, void* stream) {
   if (v->V == 0) return DMF_OK;
   const int64_t n = (int64_t)v->V;
   const unsigned nb = (unsigned)((n + 255) / 256);
-  // view: the smallest non-zero id (0 -> INT32_MAX, min, back); good: max (a flag)
+  // view: the smallest non-zero id (0 -> INT32_MAX, min, back); good: max (a flag).  The
+  // restore runs on every exit path once the rewrite is enqueued: a failed
+  // collective leaves the view ids as they were on this rank, never INT32_MAX.
   hipLaunchKernelGGL(k_view_zero_to_max, dim3(nb), dim3(256), 0, st, v->d_view, n);
   DMF_LAUNCH_CHECK();
+  struct Restore {
+    int32_t* view;
+    int64_t n;
+    unsigned nb;
+    hipStream_t st;
+    ~Restore() { hipLaunchKernelGGL(k_view_max_to_zero, dim3(nb), dim3(256), 0, st, view, n); }
+  } restore{v->d_view, n, nb, st};
   {
     NcclGroup grp;
     DMF_NCCL(grp.start());
@@ -250,8 +270,6 @@ int dmf_flags_allreduce(dmf_volume* v, void* comm, void* stream) {
     DMF_NCCL(ncclAllReduce(v->d_good, v->d_good, (size_t)n, ncclUint8, ncclMax, (ncclComm_t)comm, st));
     DMF_NCCL(grp.end());
   }
-  hipLaunchKernelGGL(k_view_max_to_zero, dim3(nb), dim3(256), 0, st, v->d_view, n);
-  DMF_LAUNCH_CHECK();
   return DMF_OK;
   DMF_API_END
 }

@@ -741,10 +741,11 @@ int dmf_volume_create(dmf_volume** out, int32_t device) {
   auto* v = new dmf_volume();
   v->device = device;
   v->dstar = angle_threshold();
-  // brick-fusion scratch budget: a third of the device's HBM (~96 GB of MI355X's 288 GB), at
-  // least 8 GiB -- every pose batch a smaller pair capacity forces costs its own passes and
-  // counter flushes (the device cuts the batches by the pairs a call really makes)
-  v->bk_budget = std::max<uint64_t>(8ull << 30, (uint64_t)prop.totalGlobalMem / 3);
+  // brick-fusion scratch budget: 45 % of the device's HBM (~130 GB of MI355X's 288 GB; the
+  // two staging slots of pipelined calls get half each), at least 8 GiB -- every pose batch a
+  // smaller pair capacity forces costs its own passes and counter flushes (the device cuts
+  // the batches by the pairs a call really makes)
+  v->bk_budget = std::max<uint64_t>(8ull << 30, (uint64_t)prop.totalGlobalMem / 20 * 9);
   *out = v;
   return DMF_OK;
   DMF_API_END
@@ -761,7 +762,6 @@ int dmf_volume_destroy(dmf_volume* v) {
   for (hipEvent_t e : {v->st_in, v->st_done[0], v->st_done[1], v->st_free[0], v->st_free[1], v->st_b[0], v->st_b[1]})
     if (e) (void)hipEventDestroy(e);
   if (v->stage) (void)hipStreamDestroy(v->stage);
-  if (v->stage1) (void)hipStreamDestroy(v->stage1);
   delete v;
   return DMF_OK;
   DMF_API_END
@@ -840,12 +840,8 @@ int dmf_volume_construct(dmf_volume* v) {
     return fail(DMF_ERR_RANGE, "occupancy bitmask over 2^32 bits (grid padded to 8-cell tiles)");
   DMF_HIP(hipMalloc((void**)&v->d_occ, sizeof(uint32_t) * (nocc + 1)));
   DMF_HIP(hipMemsetAsync(v->d_occ, 0, sizeof(uint32_t) * (nocc + 1), v->stream));
-  {
-    const char* e = getenv("DMF_BRICK_SHIFT");  // experiments only; default 8^3 bricks
-    v->brick_shift = e ? std::max(0, std::min(5, atoi(e))) : kBrickShiftDefault;
-    const char* c = getenv("DMF_BRICK_CAP");
-    v->brick_cap = c ? std::max(1, std::min(255, atoi(c))) : kBrickDistCapDefault;
-  }
+  v->brick_shift = kBrickShiftDefault;
+  v->brick_cap = kBrickDistCapDefault;
   const int bs = 1 << v->brick_shift;
   v->nb[0] = (v->xdim + bs - 1) / bs; v->nb[1] = (v->ydim + bs - 1) / bs; v->nb[2] = (v->zdim + bs - 1) / bs;
   const size_t bwords = ((size_t)v->nb[0] * v->nb[1] * v->nb[2] + 31) / 32 + 1;

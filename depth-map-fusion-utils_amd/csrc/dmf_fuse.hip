@@ -189,15 +189,6 @@ __device__ inline bool dda_setup(const Geom& g, const float O[3], const float E[
   return true;
 }
 
-// Advance one cell (earliest crossing; ties x before y before z).
-__device__ inline void dda_advance(Ray& R) {
-  bool s0, s1, s2;
-  dda_select(R.E01, R.E02, R.E12, R.K[0], R.K[1], R.K[2], s0, s1, s2);
-  R.c[0] += s0 ? R.st[0] : 0;
-  R.c[1] += s1 ? R.st[1] : 0;
-  R.c[2] += s2 ? R.st[2] : 0;
-}
-
 // The acceptance of integratePointCloud(cloud, normals) (Volume.hpp:199-228):
 // validPoints(E) && validCoords(getVoxel(E)).  validPoints as float compares (vlo / vhi,
 // dmf_geom.hpp; a NaN endpoint, from a non-finite pose, is outside: the reference's getVoxel
@@ -230,26 +221,8 @@ __device__ inline int pixel_ray(const Geom& g, const CamP& cam, const uint16_t* 
   return R.left;
 }
 
-// pixel_ray up to the quantised endpoints (the brick path's ray record).
-// As below with the pixel's depth already loaded (d < 0: outside the frame).
-__device__ inline bool pixel_quant_d(const Geom& g, const CamP& cam, int d, const PoseX* __restrict__ poses, int p,
-                                     int r, int c, int dmin, int dmax, int64_t qs[3], int64_t qe[3], bool& inside,
-                                     bool& valid) {
-  valid = false;
-  inside = false;
-  if (d < 0 || !(d >= dmin && d < dmax)) return false;
-  valid = true;
-  const PoseX& T = poses[p];
-  float pc[3], E[3];
-  project(cam, r, c, d, pc);
-  xform(T.f, pc[0], pc[1], pc[2], E);
-  inside = endpoint_inside(g, E);
-  const float O[3] = {T.f[3], T.f[7], T.f[11]};
-  return dda_quantize(g, O, E, inside, qs, qe);
-}
-
-// As pixel_quant_d with the pose's grid origin already computed (go = grid_origin of
-// poses[p]'s translation).
+// The brick path's ray record: pixel_ray up to the quantised endpoints, with the pose's grid
+// origin already computed (go = grid_origin of poses[p]'s translation; d < 0: outside the frame).
 __device__ inline bool pixel_quant_go(const Geom& g, const CamP& cam, int d, const PoseX& T, const double go[3], int r,
                                       int c, int dmin, int dmax, int64_t qs[3], int64_t qe[3], bool& inside,
                                       bool& valid) {
@@ -268,12 +241,6 @@ __device__ inline int pixel_depth(const CamP& cam, const uint16_t* __restrict__ 
   return (r >= cam.H || c >= cam.W) ? -1 : (int)depth[((int64_t)p * cam.H + r) * cam.W + c];
 }
 
-__device__ inline bool pixel_quant(const Geom& g, const CamP& cam, const uint16_t* __restrict__ depth,
-                                   const PoseX* __restrict__ poses, int p, int r, int c, int dmin, int dmax,
-                                   int64_t qs[3], int64_t qe[3], bool& inside, bool& valid) {
-  return pixel_quant_d(g, cam, pixel_depth(cam, depth, p, r, c), poses, p, r, c, dmin, dmax, qs, qe, inside, valid);
-}
-
 __device__ inline void wave_stats(unsigned long long* stats, unsigned long long upd, unsigned long long ray,
                                   unsigned long long hit) {
   for (int o = 32; o > 0; o >>= 1) {
@@ -288,39 +255,6 @@ __device__ inline void wave_stats(unsigned long long* stats, unsigned long long 
   }
 }
 
-
-// 16x16 tile of pixels per 256-lane workgroup; each wave an 8x8 packet.
-__device__ inline void tile_pixel(int tile, int tiles_x, int& r, int& c) {
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  c = (tile % tiles_x) * 16 + (w & 1) * 8 + (l & 7);
-  r = (tile / tiles_x) * 16 + (w >> 1) * 8 + (l >> 3);
-}
-
-// Baseline: one device-scope atomic per cell update (profiles/r01_baseline_atomic);
-// kept as the A/B reference (DMF_FUSE_VARIANT=1).
-__global__ __launch_bounds__(256) void k_fuse_direct(Geom g, CamP cam, const uint16_t* __restrict__ depth,
-                                                     const PoseX* __restrict__ poses, int dmin, int dmax, int tiles_x,
-                                                     int32_t* __restrict__ hits, int32_t* __restrict__ misses,
-                                                     unsigned long long* __restrict__ stats) {
-  stats = stat_slot(stats);
-  int r, c;
-  tile_pixel(blockIdx.x, tiles_x, r, c);
-  Ray R;
-  bool valid;
-  const int upd = pixel_ray(g, cam, depth, poses, blockIdx.y, r, c, dmin, dmax, R, valid);
-  const bool hit = R.left > 0 && R.end_inside;
-  const Tiles tl = tiles_of(g.n);
-  while (R.left > 1) {
-    atomic_add_dev(&misses[tiled_index(tl, R.c[0], R.c[1], R.c[2])], 1);
-    dda_advance(R);
-    --R.left;
-  }
-  if (R.left == 1) {
-    const uint32_t ti = tiled_index(tl, R.c[0], R.c[1], R.c[2]);
-    atomic_add_dev(R.end_inside ? &hits[ti] : &misses[ti], 1);
-  }
-  if (stats) wave_stats(stats, (unsigned long long)upd, valid ? 1ull : 0ull, hit ? 1ull : 0ull);
-}
 
 // Packed (hi | (0xffff - lo) << 16) extent reduction over the wave: one DPP max
 // chain of v_pk_max_u16 per axis gives both max(hi) and min(lo).  0 = no lane.
@@ -354,228 +288,6 @@ __device__ inline int small_div(int i, int b, float rb, int& rem) {
   return q;
 }
 
-// Previous production kernel (DMF_FUSE_VARIANT=24, A/B reference).
-// Same rounds as k_fuse_l below but the LDS box is widened to whole 2x2x4 counter
-// tiles and stored tile by tile like HBM (the replay tracks in-tile / tile-crossing
-// index deltas, odd lanes replay backwards), and the flush list is in tile order.
-// kR rays per lane share one box (the wave owns an 8 x (8 kR) pixel packet); kR = 1
-// measured fastest (2 and 3 lose to register pressure).
-template <int kS, int kBox, int kR>
-__global__ __launch_bounds__(64) void k_fuse_r(Geom g, CamP cam, const uint16_t* __restrict__ depth,
-                                               const PoseX* __restrict__ poses, int dmin, int dmax, int packets_x,
-                                               int32_t* __restrict__ hits, int32_t* __restrict__ misses,
-                                               unsigned long long* __restrict__ stats) {
-  static_assert(kS <= 15, "2-bit codes of up to 15 advances with a 32-bit field mask");
-  static_assert(kBox % 256 == 0 && kBox <= 65536, "box scanned 256 cells per iteration, 16-bit indices");
-  static_assert(kBox >= 64 * kS * kR, "the non-zero list lives in the box");
-  stats = stat_slot(stats);
-  __shared__ __attribute__((aligned(16))) int box[kBox];
-  uint32_t* nzl = (uint32_t*)box;  // non-zero list written behind the scan front
-  const int l = threadIdx.x;
-  for (int i = l; i < kBox; i += 64) box[i] = 0;
-  const Tiles tl = tiles_of(g.n);
-  int32_t E01[kR], E02[kR], E12[kR], K0[kR], K1[kR], K2[kR];
-  int st0[kR], st1[kR], st2[kR], c0[kR], c1[kR], c2[kR], left[kR];
-  bool end_inside[kR];
-  unsigned long long upd = 0, nvalid = 0, nhit = 0;
-#pragma unroll
-  for (int j = 0; j < kR; ++j) {
-    const int r = (blockIdx.x / packets_x) * (8 * kR) + 8 * j + (l >> 3), c = (blockIdx.x % packets_x) * 8 + (l & 7);
-    Ray R;
-    bool valid;
-    upd += (unsigned long long)pixel_ray(g, cam, depth, poses, blockIdx.y, r, c, dmin, dmax, R, valid);
-    nvalid += valid ? 1 : 0;
-    nhit += (R.left > 0 && R.end_inside) ? 1 : 0;
-    E01[j] = R.E01; E02[j] = R.E02; E12[j] = R.E12;
-    K0[j] = R.K[0]; K1[j] = R.K[1]; K2[j] = R.K[2];
-    st0[j] = R.st[0]; st1[j] = R.st[1]; st2[j] = R.st[2];
-    c0[j] = R.c[0]; c1[j] = R.c[1]; c2[j] = R.c[2];
-    left[j] = R.left;
-    end_inside[j] = R.end_inside;
-  }
-  unsigned long long nflush = 0, nround_lds = 0, nround_direct = 0;
-  while (true) {
-    bool any = false;
-#pragma unroll
-    for (int j = 0; j < kR; ++j) any = any || left[j] > 0;
-    if (__builtin_amdgcn_ballot_w64(any) == 0) break;
-    int rem[kR], nadv[kR], nm[kR], e0[kR], e1[kR], e2[kR], m0[kR], m1[kR], m2[kR];
-    bool fin[kR];
-    uint32_t codes[kR];
-    bool allfull = true;
-#pragma unroll
-    for (int j = 0; j < kR; ++j) {
-      rem[j] = left[j] < kS ? left[j] : kS;
-      fin[j] = rem[j] == left[j] && rem[j] > 0;
-      nadv[j] = fin[j] ? rem[j] - 1 : rem[j];
-      codes[j] = 0;
-      allfull = allfull && nadv[j] == kS;
-    }
-    if (__builtin_amdgcn_ballot_w64(!allfull) == 0) {
-#pragma unroll
-      for (int k = 0; k < kS; ++k)
-#pragma unroll
-        for (int j = 0; j < kR; ++j) {
-          bool s0, s1, s2;
-          dda_select(E01[j], E02[j], E12[j], K0[j], K1[j], K2[j], s0, s1, s2);
-          codes[j] |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
-        }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kS; ++k)
-#pragma unroll
-        for (int j = 0; j < kR; ++j)
-          if (k < nadv[j]) {
-            bool s0, s1, s2;
-            dda_select(E01[j], E02[j], E12[j], K0[j], K1[j], K2[j], s0, s1, s2);
-            codes[j] |= (s2 ? 2u : (s1 ? 1u : 0u)) << (2 * k);
-          }
-    }
-    uint32_t px = 0, py = 0, pz = 0;
-#pragma unroll
-    for (int j = 0; j < kR; ++j) {
-      const uint32_t fmask = (1u << (2 * nadv[j])) - 1u;
-      const int n2 = __builtin_popcount(codes[j] & fmask & 0xAAAAAAAAu);
-      const int n1 = __builtin_popcount(codes[j] & fmask & 0x55555555u);
-      const int n0 = nadv[j] - n1 - n2;
-      e0[j] = c0[j] + st0[j] * n0; e1[j] = c1[j] + st1[j] * n1; e2[j] = c2[j] + st2[j] * n2;
-      nm[j] = (fin[j] && end_inside[j]) ? rem[j] - 1 : rem[j];
-      m0[j] = e0[j]; m1[j] = e1[j]; m2[j] = e2[j];
-      if (nm[j] > 0 && nadv[j] > 0 && (!fin[j] || end_inside[j])) {
-        const uint32_t lc = (codes[j] >> (2 * (nadv[j] - 1))) & 3u;
-        m0[j] -= lc == 0u ? st0[j] : 0;
-        m1[j] -= lc == 1u ? st1[j] : 0;
-        m2[j] -= lc == 2u ? st2[j] : 0;
-      }
-      if (nm[j] > 0) {
-        px = pkmax(px, (uint32_t)max(c0[j], m0[j]) | ((0xffffu - (uint32_t)min(c0[j], m0[j])) << 16));
-        py = pkmax(py, (uint32_t)max(c1[j], m1[j]) | ((0xffffu - (uint32_t)min(c1[j], m1[j])) << 16));
-        pz = pkmax(pz, (uint32_t)max(c2[j], m2[j]) | ((0xffffu - (uint32_t)min(c2[j], m2[j])) << 16));
-      }
-    }
-    const uint32_t rx = wave_pkmax(px), ry = wave_pkmax(py), rz = wave_pkmax(pz);
-    if (rx != 0u) {
-      const int ax = (0xffff - (int)(rx >> 16)) & ~1, ay = (0xffff - (int)(ry >> 16)) & ~1,
-                az = (0xffff - (int)(rz >> 16)) & ~3;
-      const int tbx = (((int)(rx & 0xffffu) - ax) >> 1) + 1, tby = (((int)(ry & 0xffffu) - ay) >> 1) + 1,
-                tbz = (((int)(rz & 0xffffu) - az) >> 2) + 1;
-      const int tyz = tby * tbz;
-      const int64_t ncell_box = (int64_t)tbx * tyz * 16;
-      int x[kR], y[kR], z[kR], gx[kR], gy[kR], gz[kR];
-      uint32_t rc[kR];
-#pragma unroll
-      for (int j = 0; j < kR; ++j) {
-        const bool back = ((l + j) & 1) != 0;
-        const int sgn = back ? -1 : 1;
-        x[j] = back ? m0[j] : c0[j]; y[j] = back ? m1[j] : c1[j]; z[j] = back ? m2[j] : c2[j];
-        gx[j] = sgn * st0[j]; gy[j] = sgn * st1[j]; gz[j] = sgn * st2[j];
-        rc[j] = codes[j];
-        if (back) {
-          uint32_t t = __builtin_bitreverse32(codes[j]);
-          t = ((t & 0x55555555u) << 1) | ((t & 0xAAAAAAAAu) >> 1);
-          rc[j] = nm[j] >= 2 ? t >> (2 * (17 - nm[j])) : 0u;
-        }
-      }
-      if (ncell_box <= kBox) {
-        ++nround_lds;
-        int cur[kR], nx[kR], ny[kR], nzd[kR], qz[kR], ix[kR], iy[kR], jx[kR], jy[kR], jz[kR], fz[kR];
-        bool allm = true;
-#pragma unroll
-        for (int j = 0; j < kR; ++j) {
-          ix[j] = gx[j] * 8; iy[j] = gy[j] * 4;
-          jx[j] = gx[j] * (tyz * 16 - 8); jy[j] = gy[j] * (tbz * 16 - 4); jz[j] = gz[j] * 13;
-          fz[j] = gz[j] > 0 ? 3 : 0;
-          qz[j] = z[j] & 3;
-          nx[j] = ((x[j] & 1) == (gx[j] > 0 ? 1 : 0)) ? jx[j] : ix[j];
-          ny[j] = ((y[j] & 1) == (gy[j] > 0 ? 1 : 0)) ? jy[j] : iy[j];
-          nzd[j] = qz[j] == fz[j] ? jz[j] : gz[j];
-          cur[j] = ((((x[j] - ax) >> 1) * tby + ((y[j] - ay) >> 1)) * tbz + ((z[j] - az) >> 2)) * 16 +
-                   (((x[j] & 1) << 3) | ((y[j] & 1) << 2) | qz[j]);
-          allm = allm && nm[j] == kS;
-        }
-        const bool full = __builtin_amdgcn_ballot_w64(!allm) == 0;
-#pragma unroll
-        for (int k = 0; k < kS; ++k)
-#pragma unroll
-          for (int j = 0; j < kR; ++j) {
-            if (full || k < nm[j]) atomicAdd(&box[cur[j]], 1);
-            if (k + 1 < kS) {
-              const uint32_t cd = (rc[j] >> (2 * k)) & 3u;
-              const bool a0 = cd == 0u, a1 = cd == 1u, a2 = cd == 2u;
-              cur[j] += a2 ? nzd[j] : (a1 ? ny[j] : nx[j]);
-              nx[j] ^= a0 ? (ix[j] ^ jx[j]) : 0;
-              ny[j] ^= a1 ? (iy[j] ^ jy[j]) : 0;
-              qz[j] = a2 ? ((qz[j] + gz[j]) & 3) : qz[j];
-              nzd[j] = qz[j] == fz[j] ? jz[j] : gz[j];
-            }
-          }
-        __syncthreads();  // single-wave workgroup: orders the LDS adds before the flush
-        const int nb = (int)ncell_box;
-        int nnz = 0;
-        for (int i0 = 0; i0 < nb; i0 += 256) {
-          int v[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int i = i0 + 64 * u + l;
-            v[u] = i < nb ? box[i] : 0;
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int i = i0 + 64 * u + l;
-            const uint64_t b = __builtin_amdgcn_ballot_w64(v[u] != 0);
-            if (i < nb) box[i] = 0;
-            if (v[u]) nzl[nnz + lane_prefix(b)] = (uint32_t)i | ((uint32_t)v[u] << 16);
-            nnz += __builtin_popcountll(b);
-          }
-        }
-        __syncthreads();
-        const float rtyz = __builtin_amdgcn_rcpf((float)tyz), rtz = __builtin_amdgcn_rcpf((float)tbz);
-        const int tax = ax >> 1, tay = ay >> 1, taz = az >> 2;
-        for (int e = l; e < nnz; e += 64) {
-          const uint32_t en = nzl[e];
-          const int i = (int)(en & 0xffffu);
-          int rr, tc;
-          const int t = i >> 4;
-          const int ta = small_div(t, tyz, rtyz, rr);
-          const int tb = small_div(rr, tbz, rtz, tc);
-          ++nflush;
-          atomic_add_dev(&misses[tile_base(tl, tax + ta, tay + tb, taz + tc) + (i & 15)], (int)(en >> 16));
-        }
-        __syncthreads();
-        for (int e = l; e < nnz; e += 64) box[e] = 0;
-        __syncthreads();
-      } else {
-        ++nround_direct;
-#pragma unroll
-        for (int j = 0; j < kR; ++j)
-#pragma unroll
-          for (int k = 0; k < kS; ++k) {
-            if (k < nm[j]) atomic_add_dev(&misses[tiled_index(tl, x[j], y[j], z[j])], 1);
-            const uint32_t cd = (rc[j] >> (2 * k)) & 3u;
-            x[j] += cd == 0u ? gx[j] : 0;
-            y[j] += cd == 1u ? gy[j] : 0;
-            z[j] += cd == 2u ? gz[j] : 0;
-          }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kR; ++j) {
-      if (fin[j] && end_inside[j]) atomic_add_dev(&hits[tiled_index(tl, e0[j], e1[j], e2[j])], 1);
-      c0[j] = e0[j]; c1[j] = e1[j]; c2[j] = e2[j];
-      left[j] -= rem[j];
-    }
-  }
-  if (stats) {
-    wave_stats(stats, upd, nvalid, nhit);
-    for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
-    if (l == 0) {
-      if (nflush) atomicAdd(&stats[6], nflush);
-      if (nround_lds) atomicAdd(&stats[4], nround_lds);
-      if (nround_direct) atomicAdd(&stats[5], nround_direct);
-    }
-  }
-}
-
 __device__ inline int popc(uint32_t v) { return __builtin_popcount(v); }
 __device__ inline int popc(uint64_t v) { return __builtin_popcountll(v); }
 
@@ -601,8 +313,7 @@ __device__ inline int popc(uint64_t v) { return __builtin_popcountll(v); }
 //     ~4.4 cells of one 64-B tiled counter line into each wave instruction
 //     (tools/sim_fusion_flush_order.py; tile order: 4.85), which is one memory-side request.
 // A round whose box exceeds kBox cells adds its misses to HBM directly.  Hits (one per
-// ray) go straight to HBM.  Counts are exact integers: bit-identical to k_fuse_direct
-// and to the oracle.
+// ray) go straight to HBM.  Counts are exact integers: bit-identical to the oracle.
 template <int kS, int kBox>
 __global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t* __restrict__ depth,
                                                const PoseX* __restrict__ poses, int dmin, int dmax, int packets_x,
@@ -777,14 +488,6 @@ __global__ __launch_bounds__(64) void k_fuse_l(Geom g, CamP cam, const uint16_t*
 //                   counter).  No device atomic per update.
 namespace bk = dmf::brick;
 
-// Wave issue priority (s_setprio) of a staged pass-A / pass-B wave that shares its CU with
-// phase F (pipelined calls): the SIMD arbiter prefers higher-priority waves.
-__device__ inline void wave_prio(int p) {
-  if (p == 1) __builtin_amdgcn_s_setprio(1);
-  else if (p == 2) __builtin_amdgcn_s_setprio(2);
-  else if (p >= 3) __builtin_amdgcn_s_setprio(3);
-}
-
 struct BkGeom {
   int nb[3];    // bricks per axis
   int nbricks;
@@ -850,25 +553,6 @@ __device__ inline void hist_add_agg(uint32_t* hist, int b) {
   }
 }
 
-// As hist_add_agg, returning this lane's slot (the old count plus its rank among the
-// lanes naming the same brick).
-__device__ inline uint32_t hist_take_agg(uint32_t* hist, int b) {
-  uint64_t rem = __builtin_amdgcn_ballot_w64(true);
-  const int l = (int)(threadIdx.x & 63);
-  uint32_t slot = 0;
-  while (rem) {
-    const int leader = __builtin_ctzll(rem);
-    const int bl = __builtin_amdgcn_readlane(b, leader);
-    const uint64_t same = __builtin_amdgcn_ballot_w64(b == bl) & rem;
-    uint32_t old = 0;
-    if (l == leader) old = atomicAdd(&hist[bl], (uint32_t)__builtin_popcountll(same));
-    old = (uint32_t)__builtin_amdgcn_readlane((int)old, leader);
-    if ((same >> l) & 1ull) slot = old + (uint32_t)lane_prefix(same);
-    rem &= ~same;
-  }
-  return slot;
-}
-
 // Pass A.  Workgroup = 4 (or 16) waves over a span of 8x8 packets of ONE pose (wg_pose
 // workgroups per pose, the last one of a pose shorter); ray index = packet * 64 + lane.
 // Counts are kept per (pose, brick): pose_cnt[p][b] (the workgroup's base inside that
@@ -888,10 +572,9 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
                                                         uint32_t* __restrict__ wg_base,
                                                         uint32_t* __restrict__ wg_list, int wgl_stride,
                                                         unsigned long long* __restrict__ pose_pairs,
-                                                        unsigned long long* __restrict__ stats, int prio) {
+                                                        unsigned long long* __restrict__ stats) {
   extern __shared__ uint32_t hist[];
   __shared__ uint32_t nlist;
-  wave_prio(prio);
   stats = stat_slot(stats);
   if (threadIdx.x == 0) nlist = 0;
   const int nwords = H16 ? (bg.nbricks + 1) >> 1 : bg.nbricks;
@@ -1127,58 +810,39 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
   }
 }
 
-// Pass B.  Same spans as pass A; the workgroup counts its pairs per brick, reserves one
-// contiguous range per brick, then writes one self-contained 24-B record per pair (the
-// fine walk's state at the brick entry, so phase F makes ONE coalesced load per pair
-// and never touches the ray records).  Record (s = steps inside the brick = cells - 1,
-// 0..93; word offsets into phase F's skewed box, < 33824):
+// Pass B.  Same spans as pass A; the workgroup's range in each brick was laid out by pass A
+// and k_bk_batch_counts / k_bk_scan; every lane writes one self-contained record per (ray,
+// brick) pair (the fine walk's state at the brick entry, so phase F makes ONE coalesced
+// load per pair and never touches the ray records).
+// Entry crossing counts at a brick boundary event (axis a, fine crossing k) come from
+// bk::counts_at; E = E(0) + c_a K_b - c_b K_a (exact mod 2^32).
+// SLAB (the default, phase F k_bk_fuse_s): the 20-byte record of
+// dmf_brick.hpp pack20 (slab state on beta = b >> 9, |dq| in (major, minor1, minor2) order,
+// the slab ownership code as the walk bound), pa = words 0-3, pb = word 4 (uint32).
+// !SLAB (the per-cell walk of k_bk_fuse, kept as an independent exact check): a 24-B record
+// (s = steps inside the brick = cells - 1, 0..93; word offsets into phase F's skewed box)
 //   pa = {E01 | s[0:2) << 30, E02 | s[2:4) << 30, E12 | s[4:6) << 30, entry word | last word << 16}
 //   pb = {adq0 | adq2[0:14) << 18, adq1 | adq2[14:18) << 18 | neg x,y,z << 22 | s[6] << 25 | ends << 26}
-// with each E as a 30-bit two's-complement field: |E| < 2^28 for a moving pair of a grid
-// <= 1024 cells/axis, and a pair with a non-moving axis keeps a constant E of which only
-// the sign is used (stored as +-(2^29 - 1)).
-// Entry crossing counts at a brick boundary event (axis a, fine crossing k) come from
-// bk::counts_at; E = E(0) + c_a K_b - c_b K_a (exact mod 2^32); a pair's steps are the
-// next entry's crossing index minus its own, minus one (the ray's last brick: up to and
-// including the end cell).
+// with each E as a 30-bit two's-complement field (|E| < 2^28 for a moving pair of a grid
+// <= 1024 cells/axis; a pair with a non-moving axis keeps a constant E of which only the
+// sign is used, stored as +-(2^29 - 1)).
+// Slots: one LDS atomic per lane, whose return is consumed only by the pair's store at the
+// next brick boundary (its latency hides behind that boundary's count_at; B 1.92 -> 1.88 ms;
+// wave-aggregated and run-aggregated takes measured slower).
 __device__ inline uint32_t bk_e30(int32_t e) {
   const int32_t lim = (1 << 29) - 1;
   return (uint32_t)(e > lim ? lim : (e < -lim ? -lim : e)) & 0x3fffffffu;
 }
 
-// SLAB (phase F's major-axis walk, k_bk_fuse_s): the E fields hold the
-// slab state (b1, b2, b12) of dmf_brick.hpp instead of (E01, E02, E12), the |dq| fields are
-// in (major, minor1, minor2) order, and pb.y bits 27-28 name the major axis.
-// AGG: slots from wave-aggregated LDS atomics (hist_take_agg: one atomic per distinct brick
-// among the wave's lanes, its return broadcast by readlane at once) or, AGG = false (the
-// slab pipeline's default), one LDS atomic per lane whose return is only consumed by the
-// pair's store at the next brick boundary (its latency hides behind that boundary's
-// count_at; B 1.92 -> 1.88 ms).
-#if defined(DMF_BK_PAIRS_WAVES)  // A/B: cap pass B's VGPRs for more waves per SIMD (spills)
-#define DMF_BK_PAIRS_ATTR __attribute__((amdgpu_waves_per_eu(DMF_BK_PAIRS_WAVES)))
-#else
-#define DMF_BK_PAIRS_ATTR
-#endif
-// R20 (SLAB only; the default): the 20-byte record of dmf_brick.hpp pack20 (beta state,
-// pa = words 0-3, pb = word 4 as uint32) instead of the 24-byte one.
-// SEL: boundary-event counts by bk::counts_at_sel (one code path for every crossing axis;
-// counts_at's per-axis branches run once per distinct axis among a wave's lanes).
-// RUN (with SEL): slots by runs of adjacent lanes entering the same brick -- one LDS atomic
-// per run, by its first lane (same-address atomics of one instruction serialise: pass B's
-// LDS bank-conflict cycles were ~26 % of its time).  The coarse loop runs wave-uniform with
-// per-lane liveness so that every lane is active where the run's base is fetched from its
-// first lane (DPP wave_shr for the neighbour's brick, ds_bpermute for the base).
-template <bool SLAB, bool AGG = true, bool R20 = false, bool SEL = false, bool RUN = false>
-__global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pairs(int packets_pose, int wg_pose, int span,
-                                                         BkGeom bg, const ulonglong2* __restrict__ rays,
+template <bool SLAB>
+__global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose, int wg_pose, int span, BkGeom bg,
+                                                         const ulonglong2* __restrict__ rays,
                                                          const uint32_t* __restrict__ off,
                                                          const uint32_t* __restrict__ pose_base,
                                                          const uint32_t* __restrict__ wg_base,
                                                          const uint32_t* __restrict__ bt, int j,
                                                          const uint32_t* __restrict__ wg_list, int wgl_stride,
-                                                         uint4* __restrict__ pa, void* __restrict__ pbv, int prio) {
-  static_assert(SLAB || !R20, "the 20-byte record carries the slab state");
-  wave_prio(prio);
+                                                         uint4* __restrict__ pa, void* __restrict__ pbv) {
   uint2* const pb = (uint2*)pbv;
   uint32_t* const pw = (uint32_t*)pbv;
   extern __shared__ uint32_t hist[];
@@ -1186,11 +850,11 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
   const int pz = (int)(blockIdx.x / (unsigned)wg_pose);
   if ((uint32_t)j >= bt[0] || (uint32_t)pz < bt[1 + j] || (uint32_t)pz >= bt[2 + j]) return;
   // this workgroup's range in brick i starts at off[i] + pose_base[p][i] + wg_base[wg][i]
-  // (k_bk_scan, k_bk_batch_counts, pass A); entries of bricks pass A did not count for
-  // this workgroup are never used
+  // (k_bk_scan, k_bk_batch_counts, pass A); only the bricks pass A counted for this
+  // workgroup are initialised (1024^3: 32768 bricks, ~300 touched)
   const uint32_t* wb = wg_base + (size_t)blockIdx.x * bg.nbricks;
   const uint32_t* pbz = pose_base + (size_t)pz * bg.nbricks;
-  if (wg_list) {  // only the bricks pass A counted for this workgroup (1024^3: 32768 bricks, ~300 touched)
+  {
     const uint32_t* row = wg_list + (size_t)blockIdx.x * (size_t)wgl_stride;
     const uint32_t nl = row[0];
     const uint16_t* ids = (const uint16_t*)(row + 1);
@@ -1198,8 +862,6 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
       const int i = ids[k];
       hist[i] = off[i] + pbz[i] + wb[i];
     }
-  } else {
-    for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = off[i] + pbz[i] + wb[i];
   }
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
@@ -1213,8 +875,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
     const ulonglong2 rec = rnext;
     if (pk + nw < pk1) rnext = rays[(pk + nw) * 64 + l];
-    const bool valid = (rec.y >> 63) != 0;
-    if (!RUN && !valid) continue;
+    if ((rec.y >> 63) == 0) continue;  // no ray
     bk::QRay R;
     bk::decode_ray(rec.x, rec.y, R);
     const uint32_t K0 = (uint32_t)(2 * bk::kQ) * (uint32_t)R.adq[0], K1 = (uint32_t)(2 * bk::kQ) * (uint32_t)R.adq[1],
@@ -1231,11 +892,9 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
     const uint32_t KM = (uint32_t)(2 * bk::kQ) * aM, Km1 = (uint32_t)(2 * bk::kQ) * a1, Km2 = (uint32_t)(2 * bk::kQ) * a2;
     int32_t sb1 = 0, sb2 = 0, sb12 = 0;
     if (SLAB) bk::slab_from_pairwise(M, (int32_t)e01, (int32_t)e02, (int32_t)e12, sb1, sb2, sb12);
-    const uint2 wb0 = SLAB ? make_uint2(aM | ((a2 & 0x3fffu) << 18), a1 | ((a2 >> 14) << 18) | signs | ((uint32_t)M << 27))
-                           : make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
-                                        (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18) | signs);
-    // entry state of the pair being built (E fields without the step bits)
-    // (the exact int32 state; put() formats it)
+    const uint2 wb0 = make_uint2((uint32_t)R.adq[0] | (((uint32_t)R.adq[2] & 0x3fffu) << 18),
+                                 (uint32_t)R.adq[1] | (((uint32_t)R.adq[2] >> 14) << 18) | signs);
+    // entry state of the pair being built (the exact int32 state; put() formats it)
     auto entry = [&](const int32_t c[3]) {
       uint4 e;
       if (SLAB) {  // b = b(0) + c_M K_m - c_m K_M;  b12 = b12(0) + c_1 K_2 - c_2 K_1
@@ -1262,16 +921,12 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
       return bk_lds_word(x, y, z);
     };
     auto put = [&](uint32_t slot, uint4 e, uint32_t last, uint32_t steps, bool ends) {
-      if constexpr (R20) {
+      if constexpr (SLAB) {
         uint32_t w[5];
         bk::pack20((int32_t)e.x, (int32_t)e.y, (int32_t)e.z, aM, a1, a2, e.w, last, steps, signs >> 22, (uint32_t)M,
                    ends, w);
-#if defined(DMF_DIAG_B_NOSTORE)  // diagnostic build (wrong results): pass B without its record stores
-        if ((w[0] ^ w[1] ^ w[2] ^ w[3] ^ w[4] ^ slot) == 0x9e3779b9u) pw[0] = 0;  // keep the record live
-#else
         pa[slot] = make_uint4(w[0], w[1], w[2], w[3]);
         pw[slot] = w[4];
-#endif
       } else {
         e.x = bk_e30((int32_t)e.x) | (steps & 3u) << 30;
         e.y = bk_e30((int32_t)e.y) | ((steps >> 2) & 3u) << 30;
@@ -1292,8 +947,8 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
     };
     const int32_t c00[3] = {0, 0, 0};
     uint4 cur = entry(c00);
-    int32_t idx = 0;                      // crossings before the current pair's first cell
-    int32_t ci0 = 0, ci1 = 0, ci2 = 0;    // SLAB: their counts per axis
+    int32_t idx = 0;                    // crossings before the current pair's first cell
+    int32_t ci0 = 0, ci1 = 0, ci2 = 0;  // SLAB: their counts per axis
     // count field: SLAB = the slab ownership code of dmf_brick.hpp slab_rcode (F's walk
     // bound), else the pair's cells - 1; cL = crossing counts at the pair's last cell
     auto count_field = [&](int32_t L0, int32_t L1, int32_t L2) -> uint32_t {
@@ -1301,80 +956,14 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
       const int32_t cin[3] = {ci0, ci1, ci2}, cL[3] = {L0, L1, L2};
       return bk::slab_rcode(M, sb1, sb2, KM, Km1, Km2, cin, cL);
     };
-    if constexpr (RUN) {
-      // run-aggregated slot take (wave-uniform): the run of live lanes starting at this
-      // lane's run leader adds its length once; this lane's slot = the leader's old + rank
-      uint32_t old = 0;
-      int start = 0, rank = 0;
-      auto take = [&](bool live, int b) {
-        const uint64_t act = __builtin_amdgcn_ballot_w64(live);
-        const int pb = __builtin_amdgcn_update_dpp(b, b, 0x138, 0xf, 0xf, false);  // wave_shr:1
-        const bool lead = live && (l == 0 || !((act >> (l - 1)) & 1ull) || pb != b);
-        const uint64_t leaders = __builtin_amdgcn_ballot_w64(lead);
-        const uint64_t stops = leaders | ~act;
-        const uint64_t above = l == 63 ? 0ull : (stops >> (l + 1)) << (l + 1);
-        const int end = above ? __builtin_ctzll(above) : 64;
-        if (lead) old = atomicAdd(&hist[b], (uint32_t)(end - l));
-        const uint64_t upto = leaders & (~0ull >> (63 - l));
-        start = upto ? 63 - __builtin_clzll(upto) : l;
-        rank = l - start;
-      };
-      auto slot_of = [&]() {
-        return (uint32_t)__builtin_amdgcn_ds_bpermute(start << 2, (int)old) + (uint32_t)rank;
-      };
-      int bx = R.cs[0] >> bk::kLog, by = R.cs[1] >> bk::kLog, bz = R.cs[2] >> bk::kLog;
-      bk::Coarse cw;
-      bk::coarse_init(R, cw);
-      const int total = valid ? cw.total : -1;
-      take(valid, bk_index(bg, bx, by, bz));
-      // iteration t: boundary t for live lanes (t < total); at t == total the lane stores its
-      // last pair, with the slot of its last take (every take overwrites the run bases, so
-      // each slot is fetched in the iteration right after its take)
-      for (int t = 0;; ++t) {
-        const bool live = t < total, fin = t == total;
-        if (__builtin_amdgcn_ballot_w64(live || fin) == 0) break;
-        int a = 0;
-        int32_t c[3] = {0, 0, 0};
-        if (live) {
-          a = bk::coarse_next(cw);
-          bx += a == 0 ? R.st[0] : 0;
-          by += a == 1 ? R.st[1] : 0;
-          bz += a == 2 ? R.st[2] : 0;
-          const int32_t sa = bk::sel3(a == 0, a == 1, R.st[0], R.st[1], R.st[2]);
-          const int32_t ca = bk::sel3(a == 0, a == 1, R.cs[0], R.cs[1], R.cs[2]);
-          const int32_t nb = (a == 0 ? bx : (a == 1 ? by : bz)) << bk::kLog;
-          bk::counts_at_sel(R, a, sa > 0 ? nb - ca - 1 : ca - nb - bk::kB, c);
-        }
-        const uint32_t slot = slot_of();  // every lane active: the leaders' bases are readable
-        if (live) {
-          put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
-          cur = entry(c);
-          idx = c[0] + c[1] + c[2];
-          ci0 = c[0];
-          ci1 = c[1];
-          ci2 = c[2];
-        } else if (fin) {
-          put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
-        }
-        take(live, bk_index(bg, bx, by, bz));
-      }
-      continue;
-    }
     uint32_t slot = 0;
     bk_coarse(bg, R, [&](int b, int a, int bx, int by, int bz) {
       if (a >= 0) {
         int32_t c[3];
-        if constexpr (SEL) {
-          const int32_t sa = bk::sel3(a == 0, a == 1, R.st[0], R.st[1], R.st[2]);
-          const int32_t ca = bk::sel3(a == 0, a == 1, R.cs[0], R.cs[1], R.cs[2]);
-          const int32_t nb = (a == 0 ? bx : (a == 1 ? by : bz)) << bk::kLog;
-          bk::counts_at_sel(R, a, sa > 0 ? nb - ca - 1 : ca - nb - bk::kB, c);
-        } else {
-          // constant axis in each call: no dynamically indexed (scratch) arrays
-          if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
-          else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
-          else bk::counts_at(R, 2, boundary_k(2, bz), c);
-        }
+        // constant axis in each call: no dynamically indexed (scratch) arrays
+        if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
+        else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
+        else bk::counts_at(R, 2, boundary_k(2, bz), c);
         put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
         cur = entry(c);
         idx = c[0] + c[1] + c[2];
@@ -1382,11 +971,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_BK_PAIRS_ATTR void k_bk_pair
         ci1 = c[1];
         ci2 = c[2];
       }
-#if defined(DMF_DIAG_B_NOATOMIC)  // diagnostic build (wrong results): no slot atomics
-      slot = hist[b];  // (every lane of the workgroup writes the range start: no out-of-range store)
-#else
-      slot = AGG ? hist_take_agg(hist, b) : atomicAdd(&hist[b], 1u);
-#endif
+      slot = atomicAdd(&hist[b], 1u);
     });
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }
@@ -1403,20 +988,13 @@ __device__ inline uint32_t bk_order(uint32_t k, uint32_t n) {
   return k < n1 ? (k % S_ORDER) * per + k / S_ORDER : k;
 }
 
-// Bit select with an all-ones / all-zero mask: m ? a : b (one v_bfi_b32, no SGPR mask).
-__device__ inline int32_t bsel(int32_t m, int32_t a, int32_t b) { return (a & m) | (b & ~m); }
-
-// Phase F (persistent; a work queue of parts, every workgroup exits when it is empty).
-// Each lane walks one pair at a time; a wave refills its idle lanes when >= REFILL are
-// idle, from per-lane records prefetched one refill ahead (their load latency is hidden
-// behind the walk of the current pairs).
-//
-// The walk runs in blocks of UNROLL steps with no branch and no scalar mask work inside:
-// a lane with `rem` steps left adds to its cell while u < rem and to a private dummy word
-// past the box otherwise (its state keeps moving, harmlessly: 8 extra steps change |E|
-// by < 2^30).  The DDA selection works on VGPR masks: the E fields are kept biased by -1
-// so that (E' >> 31) is all-ones exactly when E <= 0, and every select is a bit select.
-template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, int CHUNK, bool BR>
+// Phase F, per-cell walk (variant DMF_FUSE_CELL_WALK = 40: an independent exact walk kept for
+// cross-checks; the default is k_bk_fuse_s below).  Persistent: a work queue of parts, every
+// workgroup exits when it is empty.  Each lane walks one pair at a time, one DDA selection
+// per cell; a wave refills its idle lanes when >= REFILL are idle, from per-lane records
+// prefetched one refill ahead (their load latency is hidden behind the walk of the current
+// pairs).  The E fields are kept biased by -1 so that E >= 0 tests E > 0.
+template <int REFILL, int S_ORDER, int UNROLL>
 __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const uint4* __restrict__ pa,
                                                         const uint2* __restrict__ pb,
                                                         const uint32_t* __restrict__ off,
@@ -1425,25 +1003,15 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
                                                         unsigned long long* __restrict__ ctl,
                                                         int32_t* __restrict__ hits, int32_t* __restrict__ misses,
                                                         unsigned long long* __restrict__ stats) {
-  // counters (skewed), 4 control words, then one dummy word per lane
-  __shared__ uint32_t box[kBkBoxWords + 4 + 64];
+  // counters (skewed), then 4 control words
+  __shared__ uint32_t box[kBkBoxWords + 4];
   uint32_t* sh = box + kBkBoxWords;
   stats = stat_slot(stats);
   const int tid = threadIdx.x, l = tid & 63;
-  const int dummy = (kBkBoxWords + 4 + l) * 4;
   for (int i = tid; i < kBkBoxWords; i += blockDim.x) box[i] = 0;
   const uint32_t nparts = (uint32_t)ctl[1];
   const Tiles tl = tiles_of(g.n);
   unsigned long long npairs = 0, nparts_done = 0, nflush = 0;
-#if defined(DMF_EXP_STATS)
-  unsigned long long nblocks = 0, nlanes = 0, nrefill = 0, t_refill = 0, t_walk = 0, t_flush = 0;
-  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-#define DMF_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
-#define DMF_TACC(acc, x) acc += __builtin_amdgcn_s_memtime() - (x)
-#else
-#define DMF_T(x)
-#define DMF_TACC(acc, x)
-#endif
   for (;;) {
     if (tid == 0) {
       sh[0] = (uint32_t)atomicAdd(&ctl[2], 1ull);
@@ -1468,173 +1036,83 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       npairs += n;
       ++nparts_done;
     }
-    // walk state per slot (biased E, K negated once per pair: the step is adds and bit
-    // selects).  NSLOT pairs per lane walk interleaved: independent dependency chains in
-    // one basic block, so a wave keeps issuing while one chain waits on its last result.
-    int32_t E01[NSLOT], E02[NSLOT], E12[NSLOT], K1[NSLOT], K2[NSLOT], nK0[NSLOT], nK1[NSLOT];
-    // BR (branchy walk): a slot is active while cur != cend (its last cell); otherwise while
-    // rem > 0, with the steps past the end sent to the lane's dummy word
-    int cur[NSLOT], rem[NSLOT], cend[NSLOT], dX[NSLOT], dY[NSLOT], dZ[NSLOT];
-    uint4 ca[NSLOT];
-    uint2 cb[NSLOT];
-    bool fok[NSLOT];
-#pragma unroll
-    for (int q = 0; q < NSLOT; ++q) {
-      E01[q] = E02[q] = E12[q] = K1[q] = K2[q] = nK0[q] = nK1[q] = 0;
-      cur[q] = rem[q] = cend[q] = dX[q] = dY[q] = dZ[q] = 0;
-      ca[q] = make_uint4(0, 0, 0, 0);
-      cb[q] = make_uint2(0, 0);
-      fok[q] = false;
-    }
-    auto decode = [&](int q) {
-      const uint4 ra = ca[q];
-      const uint2 rb = cb[q];
-      E01[q] = __builtin_amdgcn_sbfe((int32_t)ra.x, 0, 30) - 1;
-      E02[q] = __builtin_amdgcn_sbfe((int32_t)ra.y, 0, 30) - 1;
-      E12[q] = __builtin_amdgcn_sbfe((int32_t)ra.z, 0, 30) - 1;
-      const uint32_t a0 = rb.x & 0x3ffffu, a1 = rb.y & 0x3ffffu, a2 = (rb.x >> 18) | (((rb.y >> 18) & 15u) << 14);
-      nK0[q] = -(int32_t)(a0 << 9);
-      K1[q] = (int32_t)(a1 << 9);
-      K2[q] = (int32_t)(a2 << 9);
-      nK1[q] = -K1[q];
-      cur[q] = (int)(ra.w & 0xffffu) * 4;
-      cend[q] = (int)(ra.w >> 16) * 4;
-      rem[q] = (int)((ra.x >> 30) | ((ra.y >> 30) << 2) | ((ra.z >> 30) << 4) | (((rb.y >> 25) & 1u) << 6));
-      dX[q] = (rb.y >> 22) & 1u ? -(4 * kBkSx) : 4 * kBkSx;
-      dY[q] = (rb.y >> 23) & 1u ? -(4 * kBkSy) : 4 * kBkSy;
-      dZ[q] = (rb.y >> 24) & 1u ? -4 : 4;
+    // walk state (biased E, K negated once per pair: the step is adds and bit selects); a
+    // lane is active while cur != cend (its last cell, added at adoption)
+    int32_t E01 = 0, E02 = 0, E12 = 0, K1 = 0, K2 = 0, nK0 = 0, nK1 = 0;
+    int cur = 0, cend = 0, dX = 0, dY = 0, dZ = 0;
+    uint4 ca = make_uint4(0, 0, 0, 0);
+    uint2 cb = make_uint2(0, 0);
+    bool fok = false;
+    auto decode = [&]() {
+      E01 = __builtin_amdgcn_sbfe((int32_t)ca.x, 0, 30) - 1;
+      E02 = __builtin_amdgcn_sbfe((int32_t)ca.y, 0, 30) - 1;
+      E12 = __builtin_amdgcn_sbfe((int32_t)ca.z, 0, 30) - 1;
+      const uint32_t a0 = cb.x & 0x3ffffu, a1 = cb.y & 0x3ffffu, a2 = (cb.x >> 18) | (((cb.y >> 18) & 15u) << 14);
+      nK0 = -(int32_t)(a0 << 9);
+      K1 = (int32_t)(a1 << 9);
+      K2 = (int32_t)(a2 << 9);
+      nK1 = -K1;
+      cur = (int)(ca.w & 0xffffu) * 4;
+      cend = (int)(ca.w >> 16) * 4;
+      dX = (cb.y >> 22) & 1u ? -(4 * kBkSx) : 4 * kBkSx;
+      dY = (cb.y >> 23) & 1u ? -(4 * kBkSy) : 4 * kBkSy;
+      dZ = (cb.y >> 24) & 1u ? -4 : 4;
       // the pair's last cell: a hit when the ray ends there inside the grid, else a miss
-      atomicAdd(&box[ra.w >> 16], (rb.y >> 26) & 1u ? 0x10000u : 1u);
+      atomicAdd(&box[ca.w >> 16], (cb.y >> 26) & 1u ? 0x10000u : 1u);
     };
-    bool more = true, last_chunk = false;
-    uint32_t wcur = 0, wend = 0;  // CHUNK > 0: the wave's current index range
-    // lanes in need[q] allocate and load the next record of slot q (one LDS allocation
-    // for all slots)
-    auto prefetch = [&](const uint64_t* need) {
-      int nn = 0;
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) nn += __builtin_popcountll(need[q]);
-      uint32_t base, avail = (uint32_t)nn, nbase = 0, roff = 0;
-      if (CHUNK == 0) {  // one LDS allocation per refill
-        uint32_t base0 = 0;
-        if (l == 0) base0 = atomicAdd(&sh[1], (uint32_t)nn);
-        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
-        if (base + (uint32_t)nn >= n) more = false;
-      } else {  // wave-private chunks of CHUNK indices: an LDS allocation (and its
-                // lgkmcnt drain behind the wave's queued adds) only every CHUNK pairs
-        base = wcur;
-        avail = wend - wcur;
-        if (avail < (uint32_t)nn) {
-          uint32_t c0 = 0;
-          if (l == 0) c0 = atomicAdd(&sh[1], (uint32_t)CHUNK);
-          nbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)c0);
-          wcur = nbase + ((uint32_t)nn - avail);
-          wend = nbase + CHUNK;
-          if (nbase + CHUNK >= n) last_chunk = true;
-        } else {
-          wcur += (uint32_t)nn;
+    bool more = true;
+    // lanes in `need` take the next pair indices (one LDS allocation) and load their records
+    auto prefetch = [&](uint64_t need) {
+      const uint32_t nn = (uint32_t)__builtin_popcountll(need);
+      uint32_t base0 = 0;
+      if (l == 0) base0 = atomicAdd(&sh[1], nn);
+      const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
+      if (base + nn >= n) more = false;
+      if ((need >> l) & 1ull) {
+        const uint32_t k = base + (uint32_t)lane_prefix(need);
+        fok = k < n;
+        if (fok) {
+          const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
+          ca = pa[i];
+          cb = pb[i];
         }
-        if (last_chunk && wcur >= n) more = false;
-      }
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) {
-        if ((need[q] >> l) & 1ull) {
-          const uint32_t rk = roff + (uint32_t)lane_prefix(need[q]);  // rank among this refill's takers
-          const uint32_t k = CHUNK == 0 ? base + (uint32_t)lane_prefix(need[q])
-                                        : (rk < avail ? base + rk : nbase + (rk - avail));
-          fok[q] = k < n;
-          if (fok[q]) {
-            const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
-            ca[q] = pa[i];
-            cb[q] = pb[i];
-          }
-        }
-        base += (uint32_t)__builtin_popcountll(need[q]);
-        roff += (uint32_t)__builtin_popcountll(need[q]);
       }
     };
-    {
-      uint64_t all[NSLOT];
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) all[q] = ~0ull;
-      prefetch(all);
-    }
+    prefetch(~0ull);
     for (;;) {
-      int nact = 0;
-      bool any_act = false;
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) {
-        const uint64_t a = __builtin_amdgcn_ballot_w64(BR ? cur[q] != cend[q] : rem[q] > 0);
-        nact += __builtin_popcountll(a);
-        any_act |= a != 0;
-      }
-      DMF_T(tr0);
-      if (nact <= 64 * NSLOT - REFILL) {
-        uint64_t take[NSLOT];
-        bool any = false;
-#pragma unroll
-        for (int q = 0; q < NSLOT; ++q) {
-          take[q] = __builtin_amdgcn_ballot_w64((BR ? cur[q] == cend[q] : rem[q] <= 0) && fok[q]);
-          any |= take[q] != 0;
-        }
-        if (any) {
-#if defined(DMF_EXP_STATS)
-          if (l == 0) ++nrefill;
-#endif
-#pragma unroll
-          for (int q = 0; q < NSLOT; ++q) {
-            if ((BR ? cur[q] == cend[q] : rem[q] <= 0) && fok[q]) {
-              decode(q);
-              fok[q] = false;
-            }
+      const uint64_t act = __builtin_amdgcn_ballot_w64(cur != cend);
+      bool any_act = act != 0;
+      if (__builtin_popcountll(act) <= 64 - REFILL) {
+        const uint64_t take = __builtin_amdgcn_ballot_w64(cur == cend && fok);
+        if (take) {
+          if (cur == cend && fok) {
+            decode();
+            fok = false;
           }
           if (more) prefetch(take);
-          any_act = false;
-#pragma unroll
-          for (int q = 0; q < NSLOT; ++q)
-            any_act |= __builtin_amdgcn_ballot_w64(BR ? cur[q] != cend[q] : rem[q] > 0) != 0;
+          any_act = __builtin_amdgcn_ballot_w64(cur != cend) != 0;
         }
       }
-      DMF_TACC(t_refill, tr0);
       if (!any_act) {
-        bool pending = false;
-#pragma unroll
-        for (int q = 0; q < NSLOT; ++q) pending |= __builtin_amdgcn_ballot_w64(fok[q]) != 0;
-        if (!pending) break;
+        if (__builtin_amdgcn_ballot_w64(fok) == 0) break;
         continue;
       }
-      DMF_T(tw0);
-#if defined(DMF_EXP_STATS)
-      if (l == 0) ++nblocks;
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q)
-        nlanes += (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(BR ? cur[q] != cend[q] : rem[q] > 0));
-#endif
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-#pragma unroll
-        for (int q = 0; q < NSLOT; ++q) {
-          if (BR && cur[q] == cend[q]) continue;
-          atomicAdd((uint32_t*)((char*)box + (BR || u < rem[q] ? cur[q] : dummy)), 1u);
-          const bool b10 = E01[q] >= 0;              // E01 > 0 (biased): T1 < T0
-          const bool s2 = (b10 ? E12[q] : E02[q]) >= 0;  // T2 first
-          const bool s1 = !s2 && b10, s0 = !s2 && !b10;
-          E01[q] += s0 ? K1[q] : (s1 ? nK0[q] : 0);
-          E02[q] += s0 ? K2[q] : (s2 ? nK0[q] : 0);
-          E12[q] += s1 ? K2[q] : (s2 ? nK1[q] : 0);
-          cur[q] += s2 ? dZ[q] : (s1 ? dY[q] : dX[q]);
-        }
+        if (cur == cend) continue;
+        atomicAdd((uint32_t*)((char*)box + cur), 1u);
+        const bool b10 = E01 >= 0;              // E01 > 0 (biased): T1 < T0
+        const bool s2 = (b10 ? E12 : E02) >= 0;  // T2 first
+        const bool s1 = !s2 && b10, s0 = !s2 && !b10;
+        E01 += s0 ? K1 : (s1 ? nK0 : 0);
+        E02 += s0 ? K2 : (s2 ? nK0 : 0);
+        E12 += s1 ? K2 : (s2 ? nK1 : 0);
+        cur += s2 ? dZ : (s1 ? dY : dX);
       }
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) rem[q] -= UNROLL;
-      DMF_TACC(t_walk, tw0);
     }
-    DMF_T(tf0);
     __syncthreads();
     // flush: e -> 2x2x4 tile (e >> 4) of the brick, cell (e & 15) as in the tiled layout,
-    // so 16 lanes cover one 64-B counter line
-    // device atomics for every part (fire-and-forget; a plain read-modify-write of a
-    // single-part brick waits one HBM latency per cell: measured 4 % slower)
+    // so 16 lanes cover one 64-B counter line; device atomics for every part
     for (int e = tid; e < bk::kCells; e += blockDim.x) {
       const int tile = e >> 4, w16 = e & 15;
       const int tx = tile >> (2 * bk::kLog - 3), ty = (tile >> (bk::kLog - 2)) & ((bk::kB >> 1) - 1),
@@ -1652,24 +1130,10 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       }
     }
     __syncthreads();
-    DMF_TACC(t_flush, tf0);
   }
   if (stats) {
     for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
     if (l == 0 && nflush) atomicAdd(&stats[6], nflush);
-#if defined(DMF_EXP_STATS)
-    if (l == 0) {  // diagnostic: wave blocks, active lanes at block start, refills
-      atomicAdd(&stats[7], nblocks);
-      atomicAdd(&stats[8], nlanes);
-      atomicAdd(&stats[9], nrefill);
-      atomicAdd(&stats[10], t_refill);
-      atomicAdd(&stats[11], t_walk);
-      atomicAdd(&stats[12], t_flush);
-      const unsigned long long t_end = __builtin_amdgcn_s_memtime();
-      atomicMax(&stats[13], t_end - t_start);  // longest workgroup lifetime
-      atomicAdd(&stats[14], t_end - t_start);  // sum over waves of lifetimes
-    }
-#endif
     if (tid == 0) {
       if (npairs) atomicAdd(&stats[4], npairs);
       if (nparts_done) atomicAdd(&stats[5], nparts_done);
@@ -1677,48 +1141,42 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
   }
 }
 
-// Phase F, slab walk (default).  Same part queue, LDS box, refill and
-// flush as k_bk_fuse, but a lane advances one SLAB per step (dmf_brick.hpp slab_walk):
-// the cells between two major-axis crossings, 1 + c1 + c2 of them, with one compare per
-// minor axis instead of a three-way DDA selection per cell.  Branch-free: the three LDS
-// adds of a slab are predicated on the cells the pair still owns (v = min(1 + c1 + c2,
-// r)); the state keeps moving harmlessly past the pair's end (unsigned arithmetic;
-// refilled or ignored).  The pair's last cell is added at adoption (hit or miss), so the
-// walk covers r = cells - 1.  NSLOT pairs per lane walk interleaved (independent
-// dependency chains: at 4 waves per SIMD a single chain leaves the SIMD idle between
-// its dependent instructions).  A wave refills when >= REFILL of its 64 * NSLOT slots
-// are idle, from per-slot records prefetched one refill ahead.
-// R20: 20-byte records (dmf_brick.hpp pack20): the walk runs on the beta state with
-// increments |dq| (exactly the same decisions as b with K = 512 |dq|).
-// POOL (20-B records, NSLOT 1): a wave takes pair indices from its own pool of 64, grabbed
-// from the part's LDS counter one refill AHEAD (the grab's latency, which waits for the
-// wave's queued walk adds, hides behind the next walk block instead of stalling the refill).
-// W0D (A/B, variant 67): a slab's first add (owned iff r > t, false only on a pair's last block
-// and on idle lanes) goes unmasked to the lane's dummy word when not owned: two SALU exec-mask
-// instructions fewer per slab for one LDS add per idle lane.
-template <int REFILL, int S_ORDER, int UNROLL, int NSLOT, bool BL = false, bool R20 = false, bool POOL = false,
-          bool W0D = false>
+// Phase F, slab walk (the default).  Same part queue, LDS box and
+// flush as k_bk_fuse, but a lane advances one SLAB per step (dmf_brick.hpp slab_walk): the
+// cells between two major-axis crossings, 1 + c1 + c2 of them, with one compare per minor
+// axis instead of a three-way DDA selection per cell, on the 20-byte record's scaled state
+// beta = b >> 9 with increments |dq| (exactly the decisions of b with K = 512 |dq|).  The
+// three LDS adds of a slab are predicated on the pair's slab ownership code r (cell j of the
+// k-th slab from here is owned iff r - 3k > j); the state keeps moving harmlessly past the
+// pair's end (unsigned arithmetic; refilled or ignored).  The pair's last cell is added at
+// adoption (hit or miss).  A wave refills when >= REFILL of its lanes are idle, from
+// per-lane records prefetched one refill ahead through buffer resources over the part.
+// Parts are taken from k_bk_scan's largest-first order (entries (brick, part index); bit 31
+// of the index marks a quarter of a part from the scan's tail split).
+#if defined(DMF_EXP_STATS)
+#define DMF_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
+#define DMF_TACC(acc, x) acc += __builtin_amdgcn_s_memtime() - (x)
+#else
+#define DMF_T(x)
+#define DMF_TACC(acc, x)
+#endif
+template <int REFILL, int S_ORDER, int UNROLL>
 __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, const uint4* __restrict__ pa,
-                                                          const void* __restrict__ pbv,
+                                                          const uint32_t* __restrict__ pw,
                                                           const uint32_t* __restrict__ off,
                                                           const uint32_t* __restrict__ cnt,
-                                                          const uint32_t* __restrict__ part_pref,
                                                           const uint2* __restrict__ order, uint32_t part_max,
                                                           unsigned long long* __restrict__ ctl,
                                                           int32_t* __restrict__ hits, int32_t* __restrict__ misses,
                                                           unsigned long long* __restrict__ stats) {
-  __shared__ uint32_t box[kBkBoxWords + 4 + 64];  // counters (skewed), control words, diagnostic words
+  __shared__ uint32_t box[kBkBoxWords + 4];  // counters (skewed), control words
   uint32_t* sh = box + kBkBoxWords;
-  // (dM, d1, d2) LDS byte strides of a pair, looked up by its record bits 22-28 (step signs,
-  // a step-count bit, hit, major axis): one ds_read instead of ~17 selects per refill
-  // (F -1.3 %); written before the first part's barrier
+  // (dM, d1, d2) LDS byte strides of a pair, looked up by its record bits w4 >> 24 (bits 1-3
+  // step signs, 4-5 the major axis): one ds_read instead of ~17 selects per refill (F -1.3 %);
+  // written before the first part's barrier
   __shared__ uint4 slut[128];
-  const uint2* const pb = (const uint2*)pbv;
-  const uint32_t* const pw = (const uint32_t*)pbv;
   if (threadIdx.x < 128) {
-    // 24-B record: index bits 0-2 = step signs, 5-6 = M; 20-B record (w4 >> 24): 1-3 = step
-    // signs, 4-5 = M
-    const uint32_t c = threadIdx.x, sg = R20 ? c >> 1 : c, M = R20 ? (c >> 4) & 3u : (c >> 5) & 3u;
+    const uint32_t c = threadIdx.x, sg = c >> 1, M = (c >> 4) & 3u;
     const uint32_t sx = sg & 1u ? 0u - 4u * kBkSx : 4u * kBkSx, sy = sg & 2u ? 0u - 4u * kBkSy : 4u * kBkSy,
                    sz = sg & 4u ? 0u - 4u : 4u;
     slut[c] = make_uint4(M == 0 ? sx : (M == 1 ? sy : sz), M == 0 ? sy : sx, M == 2 ? sy : sz, 0u);
@@ -1730,10 +1188,11 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
   const Tiles tl = tiles_of(g.n);
   unsigned long long npairs = 0, nparts_done = 0, nflush = 0;
 #if defined(DMF_EXP_STATS)
-  // diagnostic build: wave blocks, slots active at block start, refills, and s_memtime
-  // cycles per phase (refill, walk, flush incl. its barriers, wait at the part-start barrier)
+  // diagnostic build: wave blocks, lanes active at block start, refills, and s_memtime
+  // cycles per phase (refill = decode + index allocation / prefetch, walk, flush incl. its
+  // barriers, wait at the part-start barrier)
   unsigned long long nblocks = 0, nlanes = 0, nrefill = 0, t_refill = 0, t_walk = 0, t_flush = 0, t_bar = 0;
-  unsigned long long t_dec = 0, t_pf = 0;  // refill split: decode (incl. the record wait), index allocation + prefetch
+  unsigned long long t_dec = 0, t_pf = 0;
   const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
   char* const lds = (char*)box;
@@ -1746,30 +1205,14 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     __syncthreads();
     DMF_TACC(t_bar, tb0);
     if (sh[0] >= nparts) break;
-    int b;
-    uint32_t j;
-    uint32_t q4 = 1;  // quarters of the tail split (k_bk_scan)
-    if (order) {  // largest parts first, (brick, index) from k_bk_scan
-      const uint2 o = order[sh[0]];
-      b = (int)o.x;
-      j = o.y & 0x7fffffffu;
-      q4 = o.y >> 31 ? 4u : 1u;
-    } else {  // brick order: the last brick b with part_pref[b] <= t
-      const uint32_t t = sh[0];
-      int lo = 0, hi = bg.nbricks - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (part_pref[mid] <= t) lo = mid;
-        else hi = mid - 1;
-      }
-      b = lo;
-      j = t - part_pref[b];
-    }
+    const uint2 o = order[sh[0]];
+    const int b = (int)o.x;
+    const uint32_t j = o.y & 0x7fffffffu, q4 = o.y >> 31 ? 4u : 1u;  // quarters of the tail split
     const uint32_t nb_pairs = cnt[b], np = q4 * ((nb_pairs + part_max - 1) / part_max);
     const uint32_t p0 = off[b] + (uint32_t)(((uint64_t)nb_pairs * j) / np);
     const uint32_t n = (uint32_t)(((uint64_t)nb_pairs * (j + 1)) / np) - (uint32_t)(((uint64_t)nb_pairs * j) / np);
-    // 20-B records: buffer resources over the part's records (32-bit offsets < 2^21, no
-    // 64-bit address math per load; a load past the part returns zeros)
+    // buffer resources over the part's records (32-bit offsets < 2^21, no 64-bit address
+    // math per load; a load past the part returns zeros)
     const __amdgpu_buffer_rsrc_t rs_a = __builtin_amdgcn_make_buffer_rsrc((void*)(pa + p0), (short)0, (int)(n * 16u),
                                                                          0x00020000);
     const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)(pw + p0), (short)0, (int)(n * 4u),
@@ -1780,174 +1223,67 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       npairs += n;
       ++nparts_done;
     }
-    // per slot: slab state (unsigned: it may run past the pair's end), LDS byte offset
-    // and strides, cells left (r), the prefetched record (ca, cb) and whether it is valid
-    uint32_t b1[NSLOT], b2[NSLOT], b12[NSLOT], K1[NSLOT], K2[NSLOT], K1mM[NSLOT], K2mM[NSLOT], nK1[NSLOT];
-    uint32_t cur[NSLOT], dM[NSLOT], d1[NSLOT], d2[NSLOT];
-    int r[NSLOT];
-    uint4 ca[NSLOT];
-    uint2 cb[NSLOT];
-    bool fok[NSLOT];
-#pragma unroll
-    for (int q = 0; q < NSLOT; ++q) {
-      b1[q] = b2[q] = b12[q] = K1[q] = K2[q] = K1mM[q] = K2mM[q] = nK1[q] = 0;
-      cur[q] = dM[q] = d1[q] = d2[q] = 0;
-      r[q] = 0;
-      ca[q] = make_uint4(0, 0, 0, 0);
-      cb[q] = make_uint2(0, 0);
-      fok[q] = false;
-    }
-    auto decode = [&](int q) {
-      const uint4 ra = ca[q];
-      const uint2 rb = cb[q];
-      if constexpr (R20) {
-        const uint32_t w[5] = {ra.x, ra.y, ra.z, ra.w, rb.x};
-        bk::Slab20 sd;
-        bk::unpack20(w, sd);
-        b1[q] = (uint32_t)sd.b1;
-        b2[q] = (uint32_t)sd.b2;
-        b12[q] = (uint32_t)sd.b12;
-        K1[q] = sd.a1;
-        K2[q] = sd.a2;
-        K1mM[q] = sd.a1 - sd.aM;
-        K2mM[q] = sd.a2 - sd.aM;
-        nK1[q] = 0u - sd.a1;
-        cur[q] = sd.entry * 4u;
-        r[q] = (int)sd.R;
-        const uint4 st3 = slut[rb.x >> 24 & 127u];
-        dM[q] = st3.x;
-        d1[q] = st3.y;
-        d2[q] = st3.z;
-        atomicAdd(&box[sd.last], sd.ends ? 0x10000u : 1u);
-        return;
-      }
-      b1[q] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ra.x, 0, 30);
-      b2[q] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ra.y, 0, 30);
-      b12[q] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ra.z, 0, 30);
-      const uint32_t aM = rb.x & 0x3ffffu, a1 = rb.y & 0x3ffffu, a2 = (rb.x >> 18) | (((rb.y >> 18) & 15u) << 14);
-      const uint32_t KM = aM << 9;
-      K1[q] = a1 << 9;
-      K2[q] = a2 << 9;
-      K1mM[q] = K1[q] - KM;
-      K2mM[q] = K2[q] - KM;
-      nK1[q] = 0u - K1[q];
-      cur[q] = (ra.w & 0xffffu) * 4u;
-      r[q] = (int)((ra.x >> 30) | ((ra.y >> 30) << 2) | ((ra.z >> 30) << 4) | (((rb.y >> 25) & 1u) << 6));
-      const uint4 st3 = slut[(rb.y >> 22) & 127u];
-      dM[q] = st3.x;
-      d1[q] = st3.y;
-      d2[q] = st3.z;
+    // slab state (unsigned: it may run past the pair's end), LDS byte offset and strides,
+    // ownership code (r), the prefetched record (ca, cw) and whether it is valid
+    uint32_t b1 = 0, b2 = 0, b12 = 0, K1 = 0, K2 = 0, K1mM = 0, K2mM = 0, nK1 = 0;
+    uint32_t cur = 0, dM = 0, d1 = 0, d2 = 0;
+    int r = 0;
+    uint4 ca = make_uint4(0, 0, 0, 0);
+    uint32_t cw = 0;
+    bool fok = false;
+    auto decode = [&]() {
+      const uint32_t w[5] = {ca.x, ca.y, ca.z, ca.w, cw};
+      bk::Slab20 sd;
+      bk::unpack20(w, sd);
+      b1 = (uint32_t)sd.b1;
+      b2 = (uint32_t)sd.b2;
+      b12 = (uint32_t)sd.b12;
+      K1 = sd.a1;
+      K2 = sd.a2;
+      K1mM = sd.a1 - sd.aM;
+      K2mM = sd.a2 - sd.aM;
+      nK1 = 0u - sd.a1;
+      cur = sd.entry * 4u;
+      r = (int)sd.R;
+      const uint4 st3 = slut[cw >> 24 & 127u];
+      dM = st3.x;
+      d1 = st3.y;
+      d2 = st3.z;
       // the pair's last cell: a hit when the ray ends there inside the grid, else a miss
-      atomicAdd(&box[ra.w >> 16], (rb.y >> 26) & 1u ? 0x10000u : 1u);
+      atomicAdd(&box[sd.last], sd.ends ? 0x10000u : 1u);
     };
     bool more = true;
-    // POOL: this wave's index pool [pl_lo, pl_hi) and the grab in flight (lane 0's return)
-    constexpr uint32_t kGrab = 64;
-    static_assert(!POOL || (NSLOT == 1 && R20), "index pool: one slot, 20-B records");
-    uint32_t pl_lo = 0, pl_hi = 0, pend = 0;
-    bool in_flight = false;
-    auto grab = [&]() {
-      uint32_t b0 = 0;
-      if (l == 0) b0 = atomicAdd(&sh[1], kGrab);
-      pend = b0;
-      in_flight = true;
-    };
-    if constexpr (POOL) grab();
-    auto prefetch_pool = [&](uint64_t need) {
-      const uint32_t nn = (uint32_t)__builtin_popcountll(need), left = pl_hi - pl_lo;
-      uint32_t nbase = 0, nb = 0;
-      if (left < nn && in_flight) {  // the grab issued one refill ago
-        nbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-        nb = kGrab;
-        in_flight = false;
-      }
-      if ((need >> l) & 1ull) {
-        const uint32_t i = (uint32_t)lane_prefix(need);
-        const uint32_t k = i < left ? pl_lo + i : (i - left < nb ? nbase + (i - left) : 0xffffffffu);
-        fok[0] = k < n;
-        const uint32_t o = bk_order<S_ORDER>(k, n);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_a, o * 16u, 0, 0);
-        ca[0] = make_uint4(v[0], v[1], v[2], v[3]);
-        cb[0].x = __builtin_amdgcn_raw_buffer_load_b32(rs_w, o * 4u, 0, 0);
-      }
-      if (nn <= left) {
-        pl_lo += nn;
-      } else {
-        pl_lo = nbase + (nn - left);
-        pl_hi = nbase + nb;
-        if (nb == 0) pl_lo = pl_hi = n;  // nothing left to hand out
-      }
-      if (pl_lo >= n) more = false;  // every later grab lies past n too
-      else if (!in_flight) grab();     // keep one grab in flight
-    };
-    // lanes in need[q] take the next pair indices (one LDS counter atomic for all slots)
-    // and load their records into slot q
-    auto prefetch = [&](const uint64_t* need) {
-      if constexpr (POOL) {
-        prefetch_pool(need[0]);
-        return;
-      }
-      uint32_t nn = 0;
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) nn += (uint32_t)__builtin_popcountll(need[q]);
+    // lanes in `need` take the next pair indices (one LDS counter atomic) and load their records
+    auto prefetch = [&](uint64_t need) {
+      const uint32_t nn = (uint32_t)__builtin_popcountll(need);
       uint32_t base0 = 0;
       if (l == 0) base0 = atomicAdd(&sh[1], nn);
-      uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
+      const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
       if (base + nn >= n) more = false;
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) {
-        if ((need[q] >> l) & 1ull) {
-          const uint32_t k = base + (uint32_t)lane_prefix(need[q]);
-          fok[q] = k < n;
-          if constexpr (R20) {
-            const uint32_t o = bk_order<S_ORDER>(k, n);
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_a, o * 16u, 0, 0);
-            ca[q] = make_uint4(v[0], v[1], v[2], v[3]);
-            cb[q].x = __builtin_amdgcn_raw_buffer_load_b32(rs_w, o * 4u, 0, 0);
-          } else if (fok[q]) {
-            const uint32_t i = p0 + bk_order<S_ORDER>(k, n);
-            ca[q] = pa[i];
-            cb[q] = pb[i];
-          }
-        }
-        base += (uint32_t)__builtin_popcountll(need[q]);
+      if ((need >> l) & 1ull) {
+        const uint32_t k = base + (uint32_t)lane_prefix(need);
+        fok = k < n;
+        const uint32_t ob = bk_order<S_ORDER>(k, n);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_a, ob * 16u, 0, 0);
+        ca = make_uint4(v[0], v[1], v[2], v[3]);
+        cw = __builtin_amdgcn_raw_buffer_load_b32(rs_w, ob * 4u, 0, 0);
       }
     };
-    {
-      uint64_t all[NSLOT];
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) all[q] = ~0ull;
-      prefetch(all);
-    }
+    prefetch(~0ull);
     for (;;) {
-      int nact = 0;
-      bool any_act = false;
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) {
-        const uint64_t a = __builtin_amdgcn_ballot_w64(r[q] > 0);
-        nact += __builtin_popcountll(a);
-        any_act |= a != 0;
-      }
+      const uint64_t act = __builtin_amdgcn_ballot_w64(r > 0);
+      bool any_act = act != 0;
       DMF_T(tr0);
-      if (nact <= 64 * NSLOT - REFILL) {
-        uint64_t take[NSLOT];
-        bool any = false;
-#pragma unroll
-        for (int q = 0; q < NSLOT; ++q) {
-          take[q] = __builtin_amdgcn_ballot_w64(r[q] <= 0 && fok[q]);
-          any |= take[q] != 0;
-        }
-        if (any) {
+      if (__builtin_popcountll(act) <= 64 - REFILL) {
+        const uint64_t take = __builtin_amdgcn_ballot_w64(r <= 0 && fok);
+        if (take) {
 #if defined(DMF_EXP_STATS)
           if (l == 0) ++nrefill;
 #endif
           DMF_T(td0);
-#pragma unroll
-          for (int q = 0; q < NSLOT; ++q) {
-            if (r[q] <= 0 && fok[q]) {
-              decode(q);
-              fok[q] = false;
-            }
+          if (r <= 0 && fok) {
+            decode();
+            fok = false;
           }
 #if defined(DMF_EXP_STATS)
           __builtin_amdgcn_s_waitcnt(0);  // close the decode interval on its loads and LDS adds
@@ -1956,85 +1292,38 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
           DMF_T(tp0);
           if (more) prefetch(take);
           DMF_TACC(t_pf, tp0);
-          any_act = false;
-#pragma unroll
-          for (int q = 0; q < NSLOT; ++q) any_act |= __builtin_amdgcn_ballot_w64(r[q] > 0) != 0;
+          any_act = __builtin_amdgcn_ballot_w64(r > 0) != 0;
         }
       }
       DMF_TACC(t_refill, tr0);
       if (!any_act) {
-        bool pending = false;
-#pragma unroll
-        for (int q = 0; q < NSLOT; ++q) pending |= __builtin_amdgcn_ballot_w64(fok[q]) != 0;
-        if (!pending) break;
+        if (__builtin_amdgcn_ballot_w64(fok) == 0) break;
         continue;
       }
       DMF_T(tw0);
 #if defined(DMF_EXP_STATS)
       if (l == 0) ++nblocks;
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) nlanes += (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(r[q] > 0));
+      nlanes += (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(r > 0));
 #endif
-      // r is the pair's slab ownership code (dmf_brick.hpp slab_rcode): cell j of the
-      // k-th slab from here is owned iff r - 3k > j.  Inside the block the thresholds move
-      // (3u + j) and r drops by 3 UNROLL once at its end: no per-slab count arithmetic.
+      // cell j of the k-th slab from here is owned iff r - 3k > j: inside the block the
+      // thresholds move (3u + j) and r drops by 3 UNROLL once at its end
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
         const int t = 3 * u;
-#pragma unroll
-        for (int q = 0; q < NSLOT; ++q) {
-          if constexpr (BL) {
-            // branch-free slab: sign masks instead of compares, and the adds a lane does not
-            // own go to its private dummy word (no exec-mask regions, so the slots' chains
-            // interleave)
-            const uint32_t n1 = (uint32_t)((int32_t)b1[q] >> 31), n2 = (uint32_t)((int32_t)b2[q] >> 31);  // ~c1, ~c2
-            const uint32_t mo = (uint32_t)((int32_t)~b12[q] >> 31);                                        // o
-            const uint32_t x1 = d1[q] & ~n1, x2 = d2[q] & ~n2;
-            // the first extra cell is on m2 iff o (also when only one minor crosses:
-            // dmf_brick.hpp slab_walk_owned)
-            const uint32_t p1 = cur[q] + ((mo & x2) | (~mo & x1)), p2 = cur[q] + x1 + x2;
-            const uint32_t dw = (uint32_t)(kBkBoxWords + 4 + l) * 4u;
-            const uint32_t a0 = r[q] > t ? cur[q] : dw, a1 = (r[q] > t + 1 && (n1 & n2) == 0u) ? p1 : dw,
-                           a2 = (r[q] > t + 2 && (n1 | n2) == 0u) ? p2 : dw;
-            atomicAdd((uint32_t*)(lds + a0), 1u);
-            atomicAdd((uint32_t*)(lds + a1), 1u);
-            atomicAdd((uint32_t*)(lds + a2), 1u);
-            cur[q] = p2 + dM[q];
-            b1[q] += (n1 & K1[q]) | (~n1 & K1mM[q]);
-            b2[q] += (n2 & K2[q]) | (~n2 & K2mM[q]);
-            b12[q] += (K2[q] & ~n1) + (nK1[q] & ~n2);
-            continue;
-          }
-          const bool c1 = (int32_t)b1[q] >= 0, c2 = (int32_t)b2[q] >= 0, o = (int32_t)b12[q] >= 0;
-          const uint32_t x1 = c1 ? d1[q] : 0u, x2 = c2 ? d2[q] : 0u;
-          // the slab's cells: cur, then p1 if a minor crosses (on m2 iff o, also when only
-          // one does: dmf_brick.hpp slab_walk_owned), then p2 if both do
-          const uint32_t p1 = cur[q] + (o ? x2 : x1), p2 = cur[q] + x1 + x2;
-          const bool w0 = r[q] > t, w1 = (c1 || c2) && r[q] > t + 1, w2 = c1 && c2 && r[q] > t + 2;
-#if defined(DMF_EXP_NOLDS)  // timing diagnostics only (wrong counts): no walk adds
-          asm volatile("" ::"v"(p1), "v"(p2), "v"((int)w0 + (int)w1 + (int)w2));
-#elif defined(DMF_EXP_LDSLANE)  // timing diagnostics only: conflict-free per-lane words
-          {
-            const uint32_t dw = (uint32_t)(kBkBoxWords + 4 + l) * 4u;
-            asm volatile("" ::"v"(p1), "v"(p2));
-            if (w0) atomicAdd((uint32_t*)(lds + dw), 1u);
-            if (w1) atomicAdd((uint32_t*)(lds + dw), 1u);
-            if (w2) atomicAdd((uint32_t*)(lds + dw), 1u);
-          }
-#else
-          if constexpr (W0D) atomicAdd((uint32_t*)(lds + (w0 ? cur[q] : (uint32_t)(kBkBoxWords + 4 + l) * 4u)), 1u);
-          else if (w0) atomicAdd((uint32_t*)(lds + cur[q]), 1u);
-          if (w1) atomicAdd((uint32_t*)(lds + p1), 1u);
-          if (w2) atomicAdd((uint32_t*)(lds + p2), 1u);
-#endif
-          cur[q] = p2 + dM[q];
-          b1[q] += c1 ? K1mM[q] : K1[q];
-          b2[q] += c2 ? K2mM[q] : K2[q];
-          b12[q] += (c1 ? K2[q] : 0u) + (c2 ? nK1[q] : 0u);
-        }
+        const bool c1 = (int32_t)b1 >= 0, c2 = (int32_t)b2 >= 0, o2 = (int32_t)b12 >= 0;
+        const uint32_t x1 = c1 ? d1 : 0u, x2 = c2 ? d2 : 0u;
+        // the slab's cells: cur, then p1 if a minor crosses (on m2 iff o2, also when only
+        // one does: dmf_brick.hpp slab_walk_owned), then p2 if both do
+        const uint32_t p1 = cur + (o2 ? x2 : x1), p2 = cur + x1 + x2;
+        if (r > t) atomicAdd((uint32_t*)(lds + cur), 1u);
+        if ((c1 || c2) && r > t + 1) atomicAdd((uint32_t*)(lds + p1), 1u);
+        if (c1 && c2 && r > t + 2) atomicAdd((uint32_t*)(lds + p2), 1u);
+        cur = p2 + dM;
+        b1 += c1 ? K1mM : K1;
+        b2 += c2 ? K2mM : K2;
+        b12 += (c1 ? K2 : 0u) + (c2 ? nK1 : 0u);
       }
-#pragma unroll
-      for (int q = 0; q < NSLOT; ++q) r[q] -= 3 * UNROLL;
+      r -= 3 * UNROLL;
       DMF_TACC(t_walk, tw0);
     }
     DMF_T(tf0);
@@ -2093,6 +1382,8 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     }
   }
 }
+#undef DMF_T
+#undef DMF_TACC
 
 // Tiled counters -> clamped int16 log-odds in the reference's x-major voxel order.
 // Four lanes per 2x2x4 tile: lane q of the tile reads int4 q of each counter line (the
@@ -2145,27 +1436,10 @@ __global__ __launch_bounds__(256) void k_counter_layout(Geom g, const int32_t* _
   else dst[ti] = src[i];
 }
 
-// Kernel variant: DMF_FUSE_VARIANT=<n> (or dmf_fuse_set_variant) selects an
-// implementation for A/B measurements; 0 = the default.
-static std::atomic<int> g_fuse_variant{-1};
-static int fuse_variant() {
-  int v = g_fuse_variant.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("DMF_FUSE_VARIANT");
-    v = e ? atoi(e) : 0;
-    g_fuse_variant.store(v, std::memory_order_relaxed);
-  }
-  return v;
+// Fusion implementation of a volume (dmf_diag.h dmf_fuse_set_variant; 0 = by grid size).
+static bool is_known_variant(int v) {
+  return v == DMF_FUSE_DEFAULT || v == DMF_FUSE_LDS_BOX || v == DMF_FUSE_CELL_WALK || v == DMF_FUSE_SLAB;
 }
-constexpr int kVariantBrick = 40;
-constexpr int kVariantSlab = 44;  // 44..53: slab walk (k_bk_pairs<true, *> + k_bk_fuse_s); 40..43: per-cell walk
-constexpr int kVariantLast = 67;  // 50, 51: branch-free slab body (measured slower); 53 = the 24-B record
-constexpr int kVariantRec20 = 57;  // the default: 20-B pair records (beta state, dmf_brick.hpp pack20)
-// 57-63: 20-B records (57 = the default <24, 32, 4>; 58-63 refill / spread / unroll A/B)
-static bool is_rec20_variant(int v) { return v == 0 || (v >= kVariantRec20 && v <= kVariantLast); }
-static bool is_brick_variant(int v) { return v >= kVariantBrick && v <= kVariantLast; }
-static bool is_slab_variant(int v) { return v == 0 || (v >= kVariantSlab && v <= kVariantLast); }
-static bool is_known_variant(int v) { return v == 0 || v == 1 || v == 24 || (v >= 30 && v <= 33) || is_brick_variant(v); }
 
 static BkGeom brick_geom(const Geom& g) {
   BkGeom bg;
@@ -2181,15 +1455,23 @@ static bool brick_path_ok(const Geom& g) {
   return g.n[0] <= 1024 && g.n[1] <= 1024 && g.n[2] <= 1024 && bg.nbricks <= kBkScanMax;
 }
 
-// Default choice (variant 0): the brick pipeline pays a per-ray cost (passes A/B) that
-// the shorter rays of small grids do not amortise.  Measured on MI355X (640x480 frames,
-// slab walk): 256^3 (64 frames) brick 2.43 ms vs k_fuse_l 2.50; 320^3 2.91 vs 3.08; 384^3
-// 3.30 vs 3.62; 512^3 (128 frames) 7.6 vs 10.2; 1024^3 (32 frames) brick ahead by 2x.
+// Default choice: the brick pipeline pays a per-ray cost (passes A/B) that the shorter rays
+// of small grids do not amortise.  Measured on MI355X (640x480 frames, slab walk): 256^3 (64
+// frames) brick 2.43 ms vs k_fuse_l 2.50; 320^3 2.91 vs 3.08; 384^3 3.30 vs 3.62; 512^3 (128
+// frames) 7.6 vs 10.2; 1024^3 (32 frames) brick ahead by 2x.
 static bool brick_preferred(const Geom& g) {
   return std::max(g.n[0], std::max(g.n[1], g.n[2])) >= 256;
 }
 
-static std::atomic<const char*> g_last_kernel{nullptr};
+static bool use_bricks(const dmf_volume* v, const Geom& g) {
+  if (!brick_path_ok(g)) return false;
+  const int fv = v->fuse_variant;
+  return fv == DMF_FUSE_SLAB || fv == DMF_FUSE_CELL_WALK || (fv == DMF_FUSE_DEFAULT && brick_preferred(g));
+}
+
+constexpr const char* kNameSlab = "dmf::k_bk_fuse_s<24, 32, 4>";
+constexpr const char* kNameCell = "dmf::k_bk_fuse<16, 8, 8>";
+constexpr const char* kNameLds = "dmf::k_fuse_l<12, 1280>";
 
 static int cu_count(int device) {
   static std::atomic<int> cached{0};
@@ -2205,13 +1487,14 @@ static int cu_count(int device) {
 // the device (pass A), and the fusion call never reads anything back (no host sync, no
 // allocation once reserved: dmf_fuse_reserve).  So the host plans by bounds and the device
 // decides: pass A runs once over a super-batch of poses (all P when their ray records fit
-// half the budget), counting pairs per (pose, brick); k_bk_batches cuts the poses into
-// batches by the pairs they really make against the pair capacity (the rest of the budget,
-// at most the geometric bound of the super-batch); the host launches jmax = the batches the
-// geometric bound rays x (1 + brick boundaries) would need, and the launches past the
-// device's batch count exit at once.  Budget: a third of the device's HBM by default
-// (~96 GB of MI355X's 288 GB): the 1024-pose 512^3 anchor and the 256-pose 1024^3 shard
-// each run as one batch.
+// half the slot's budget), counting pairs per (pose, brick); k_bk_batches cuts the poses
+// into batches by the pairs they really make against the pair capacity (the rest of the
+// slot's budget, at most the geometric bound of the super-batch); the host launches jmax =
+// the batches the geometric bound rays x (1 + brick boundaries) would need, and the launches
+// past the device's batch count exit at once.  Budget (dmf_fuse_reserve): 45 % of the
+// device's HBM by default (~130 GB of MI355X's 288 GB), all of it for the one slot of serial
+// calls, half of it for each of the two staging slots of pipelined calls: the 1024-pose
+// 512^3 anchor and the 256-pose 1024^3 shard each run as one batch either way.
 
 struct BkPlan {
   BkGeom bg;
@@ -2220,34 +1503,29 @@ struct BkPlan {
   int64_t max_pairs_ray = 0;  // geometric bound of (ray, brick) pairs per ray
   int64_t PS = 0;             // poses per super-batch (one pass A over all of them)
   int64_t PBg = 0;            // poses per batch under the geometric bound (>= 1)
-  int max_poses = 0;          // cap of poses per batch (DMF_BK_BATCH_POSES test hook; else PS)
+  int max_poses = 0;          // cap of poses per batch (DMF_KNOB_BATCH_POSES test hook; else PS)
   int ab_threads = 0, span = 0, wg_pose = 0, wgl_stride = 0;
-  uint32_t part_max = kBkPartMax;  // pairs per part of phase F (DMF_BK_PART_MAX: A/B)
-  size_t rec_bytes = 24;           // bytes per pair record: 16 (pa) + 8 (pb) or, 20-B records, 16 + 4
+  uint32_t part_max = kBkPartMax;  // pairs per part of phase F (DMF_KNOB_PART_MAX)
+  size_t rec_bytes = 20;           // bytes per pair record: 16 (pa) + 4 (slab walk) or 16 + 8 (per-cell walk)
   size_t hist_bytes = 0;
-  uint64_t pair_cap = 0;      // pair records reserved (shared by the batches of a call)
+  uint64_t pair_cap = 0;  // pair records reserved per slot (shared by the batches of a call)
   uint64_t per_pose_bytes = 0;
+  uint64_t slot_bytes = 0;  // device scratch of one slot
+  int slots = 1;            // 2 when the calls are pipelined
   int64_t jmax(int64_t ps) const { return (ps + PBg - 1) / PBg; }
   int64_t max_batches(int64_t P) const { return (P / PS) * jmax(PS) + (P % PS ? jmax(P % PS) : 0); }
   int split_cu = 0;  // k_bk_scan's tail split: F's workgroups | entries split per CU << 16 (0 = off)
   size_t max_parts() const { return (size_t)bg.nbricks + pair_cap / part_max + 1 + 3 * 1024; }
 };
 
-// Pipelined fusion: 2 = pass A, the batch layout and pass B of a call run
-// on the staging stream (the default: 512^3 x 128 frames 6.50 -> 6.16 ms per call); 1 = pass A
-// only (6.46 ms; A/B via DMF_BK_STAGE=1)
-static int stage_level() {
-  const char* e = getenv("DMF_BK_STAGE");
-  return e ? std::max(1, std::min(atoi(e), 2)) : 2;
-}
-
 static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, BkPlan& pl) {
+  const int64_t* kn = v->knob;
   pl.bg = brick_geom(g);
   pl.pkx = (cp.W + 7) / 8;
   pl.pky = (cp.H + 7) / 8;
   pl.ppose = (int64_t)pl.pkx * pl.pky;
   pl.max_pairs_ray = 1 + (pl.bg.nb[0] - 1) + (pl.bg.nb[1] - 1) + (pl.bg.nb[2] - 1);
-  pl.rec_bytes = is_rec20_variant(fuse_variant()) ? 20 : 24;
+  pl.rec_bytes = v->fuse_variant == DMF_FUSE_CELL_WALK ? 24 : 20;
   const int64_t rays_pose = pl.ppose * 64;
   const uint64_t one_pose = (uint64_t)rays_pose * (uint64_t)pl.max_pairs_ray;  // pairs of one pose, at most
   if (one_pose > (uint64_t)UINT32_MAX) return fail(DMF_ERR_RANGE, "one frame exceeds the 32-bit pair offsets");
@@ -2257,9 +1535,9 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   // histogram is small enough for 8 per wave: config 2 fusion 2.05 -> 2.02 ms, while 384^3
   // and 512^3 measured slower at 32 packets than at 64
   pl.span = std::max((pl.bg.nbricks <= 512 ? 8 : 16) * (pl.ab_threads / 64), (pl.bg.nbricks + 63) / 64);
-  if (const char* e = getenv("DMF_BK_SPAN")) pl.span = std::max(4, std::min(atoi(e), 4096));  // A/B
-  if (const char* e = getenv("DMF_BK_PART_MAX"))
-    pl.part_max = (uint32_t)std::max(1024, std::min(atoi(e), (int)kBkPartMax));
+  if (kn[DMF_KNOB_SPAN] > 0) pl.span = (int)std::max<int64_t>(4, std::min<int64_t>(kn[DMF_KNOB_SPAN], 4096));
+  if (kn[DMF_KNOB_PART_MAX] > 0)
+    pl.part_max = (uint32_t)std::max<int64_t>(1024, std::min<int64_t>(kn[DMF_KNOB_PART_MAX], kBkPartMax));
   pl.wg_pose = (int)((pl.ppose + pl.span - 1) / pl.span);
   pl.hist_bytes = sizeof(uint32_t) * (size_t)pl.bg.nbricks;
   // per pose: ray records, per-workgroup brick bases, pose counts and bases, pose pairs + batch table
@@ -2267,38 +1545,31 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   pl.per_pose_bytes = (uint64_t)rays_pose * sizeof(ulonglong2) + (uint64_t)pl.wg_pose * pl.hist_bytes +
                       (uint64_t)pl.wg_pose * sizeof(uint32_t) * (uint64_t)pl.wgl_stride + 2 * (uint64_t)pl.hist_bytes +
                       sizeof(unsigned long long) + sizeof(uint32_t);
-  // with pass B staged the two slots each hold pair records: each gets three quarters of the
-  // budget (1.5x in all, ~144 GB of MI355X's 288 GB by default), so that the 1024^3 shard
-  // (2.85G pairs) and the 1024-pose 512^3 anchor (2.0G) still run as one batch per slot
-  const uint64_t budget = v->pipelined && stage_level() >= 2 ? v->bk_budget / 4 * 3 : v->bk_budget;
+  // pipelined calls: two staging slots, each with its own pair records, share the budget
+  pl.slots = v->pipelined ? 2 : 1;
+  const uint64_t budget = v->bk_budget / (uint64_t)pl.slots;
   pl.PS = std::min<int64_t>(P, (int64_t)(budget / 2 / pl.per_pose_bytes));
-  if (const char* e = getenv("DMF_BK_SUPER_POSES")) {  // test hook: cap the poses per super-batch
-    const int64_t c = (int64_t)atoll(e);
-    if (c > 0) pl.PS = std::min<int64_t>(pl.PS, c);
-  }
+  if (kn[DMF_KNOB_SUPER_POSES] > 0) pl.PS = std::min<int64_t>(pl.PS, kn[DMF_KNOB_SUPER_POSES]);
   if (pl.PS < 1) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion budget (dmf_fuse_reserve)");
   pl.pair_cap = std::min<uint64_t>({(budget - (uint64_t)pl.PS * pl.per_pose_bytes) / pl.rec_bytes,
                                     (uint64_t)pl.PS * one_pose, (uint64_t)UINT32_MAX});
   if (pl.pair_cap < one_pose) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion pair budget (dmf_fuse_reserve)");
-  if (const char* e = getenv("DMF_BK_PAIR_CAP")) {  // test hook: a pair capacity below one pose's bound
-    const int64_t c = (int64_t)atoll(e);             // (the caller guarantees it holds any one pose's pairs)
-    if (c > 0) pl.pair_cap = std::min<uint64_t>(pl.pair_cap, (uint64_t)c);
-  }
+  if (kn[DMF_KNOB_PAIR_CAP] > 0)  // test hook: the caller guarantees it holds any one pose's pairs
+    pl.pair_cap = std::min<uint64_t>(pl.pair_cap, (uint64_t)kn[DMF_KNOB_PAIR_CAP]);
   pl.max_poses = (int)pl.PS;
-  if (const char* e = getenv("DMF_BK_BATCH_POSES")) {  // test hook: cap the poses per batch
-    const int64_t c = (int64_t)atoll(e);
-    if (c > 0) pl.max_poses = (int)std::min<int64_t>(pl.PS, c);
-  }
+  if (kn[DMF_KNOB_BATCH_POSES] > 0) pl.max_poses = (int)std::min<int64_t>(pl.PS, kn[DMF_KNOB_BATCH_POSES]);
   pl.PBg = std::max<int64_t>(1, std::min<int64_t>(pl.max_poses, (int64_t)(pl.pair_cap / one_pose)));
-  // tail split of the part queue (k_bk_scan): the largest-first order of k_bk_fuse_s only
-  const char* lpt = getenv("DMF_BK_LPT");
-  const char* ts = getenv("DMF_BK_TAILSPLIT");  // A/B: 0 = off
-  // (pipelined calls: off unless asked for; the next call's pass A fills the queue's last round
-  // there: config 2 1.78 -> 1.74 ms per call without the split)
-  if (is_slab_variant(fuse_variant()) && !(lpt && atoi(lpt) == 0) && !(ts && atoi(ts) == 0) && (ts || !v->pipelined)) {
-    const int k = ts ? std::max(1, std::min(atoi(ts), 8)) : 2;  // entries split: k per CU
+  // tail split of the part queue (k_bk_scan, slab walk only): on for serial calls; pipelined
+  // calls skip it (the next call's pass A fills the queue's last round there: config 2 1.78
+  // -> 1.74 ms per call without the split)
+  const int64_t ts = kn[DMF_KNOB_TAIL_SPLIT];
+  if (v->fuse_variant != DMF_FUSE_CELL_WALK && ts >= 0 && (ts > 0 || !v->pipelined)) {
+    const int k = ts > 0 ? (int)std::min<int64_t>(ts, 8) : 2;  // entries split: k per CU
     pl.split_cu = std::min(512, cu_count(v->device)) | (k << 16);
   }
+  pl.slot_bytes = pl.pair_cap * pl.rec_bytes + (uint64_t)pl.PS * pl.per_pose_bytes +
+                  sizeof(uint32_t) * (3 * (uint64_t)pl.bg.nbricks + 6 + 2 * pl.max_parts()) +
+                  sizeof(unsigned long long) * 4;
   return DMF_OK;
 }
 
@@ -2310,14 +1581,7 @@ static int bk_attributes() {
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                lds));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false, true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true, false, true, true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set.store(true);
   }
   return DMF_OK;
@@ -2334,28 +1598,25 @@ struct BkBufs {
   uint2* order = nullptr;
   unsigned long long* ctl = nullptr;
   uint4* pra = nullptr;
-  void* prb = nullptr;  // uint2 per pair (24-B records) or uint32 (20-B records)
+  void* prb = nullptr;  // uint32 per pair (20-B records) or uint2 (24-B records)
 };
 
-// Allocates only when a slot is too small.  `slot` picks the buffers pass A writes (ray
-// records, workgroup bases and touched-brick lists, pose counts and pair totals + batch
-// table): 0 or 1, the two staging slots of pipelined fusion (slot 0 serially).
-// slot_all: the brick layout, part queue and pair records are per slot too (pass B staged).
-static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b, int slot = 0, bool slot_all = false) {
+// Allocates only when a slot is too small.  `slot` = 0 or 1: the two staging slots of
+// pipelined fusion (serial calls use slot 0).
+static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b, int slot) {
   const size_t PS = (size_t)pl.PS, nb = (size_t)pl.bg.nbricks;
-  const bool s2 = slot && slot_all;
   void *rays, *bricks, *ctl, *wgb, *wgl, *pra, *prb, *pcnt, *pbase, *batch;
   DMF_TRY(scratch(v, slot ? kScBkRays1 : kScBkRays, sizeof(ulonglong2) * (size_t)(pl.PS * pl.ppose * 64), &rays));
   // cnt | off | part_pref (nbricks + 1) | order (uint2 per part)
-  DMF_TRY(scratch(v, s2 ? kScBkBricks1 : kScBkBricks, sizeof(uint32_t) * (3 * nb + 6 + 2 * pl.max_parts()), &bricks));
-  DMF_TRY(scratch(v, s2 ? kScBkCtl1 : kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
+  DMF_TRY(scratch(v, slot ? kScBkBricks1 : kScBkBricks, sizeof(uint32_t) * (3 * nb + 6 + 2 * pl.max_parts()), &bricks));
+  DMF_TRY(scratch(v, slot ? kScBkCtl1 : kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
   DMF_TRY(scratch(v, slot ? kScBkWgBase1 : kScBkWgBase, pl.hist_bytes * (size_t)pl.wg_pose * PS, &wgb));
   DMF_TRY(scratch(v, slot ? kScBkWgList1 : kScBkWgList,
                   sizeof(uint32_t) * (size_t)pl.wgl_stride * (size_t)pl.wg_pose * PS, &wgl));
-  DMF_TRY(scratch(v, s2 ? kScBkPairs1 : kScBkPairs, sizeof(uint4) * (size_t)pl.pair_cap, &pra));
-  DMF_TRY(scratch(v, s2 ? kScBkPairsB1 : kScBkPairsB, (pl.rec_bytes - sizeof(uint4)) * (size_t)pl.pair_cap, &prb));
+  DMF_TRY(scratch(v, slot ? kScBkPairs1 : kScBkPairs, sizeof(uint4) * (size_t)pl.pair_cap, &pra));
+  DMF_TRY(scratch(v, slot ? kScBkPairsB1 : kScBkPairsB, (pl.rec_bytes - sizeof(uint4)) * (size_t)pl.pair_cap, &prb));
   DMF_TRY(scratch(v, slot ? kScBkPoseCnt1 : kScBkPoseCnt, pl.hist_bytes * PS, &pcnt));
-  DMF_TRY(scratch(v, s2 ? kScBkPoseBase1 : kScBkPoseBase, pl.hist_bytes * PS, &pbase));
+  DMF_TRY(scratch(v, slot ? kScBkPoseBase1 : kScBkPoseBase, pl.hist_bytes * PS, &pbase));
   DMF_TRY(scratch(v, slot ? kScBkBatch1 : kScBkBatch, sizeof(unsigned long long) * PS + sizeof(uint32_t) * (PS + 4),
                   &batch));
   b.rays = (ulonglong2*)rays;
@@ -2375,27 +1636,42 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b, int slot = 0, 
   return DMF_OK;
 }
 
-// Brick-owned fusion of P frames (kernels above).  Only enqueues work: per super-batch,
-// pass A over all its poses, the device's batch cut, then per batch launch the brick
-// layout (k_bk_batch_counts, k_bk_scan), pass B and phase F; a launch past the device's
-// batch count exits at once.  Phase F reads its part count itself (its persistent
-// workgroups exit when the queue is empty).
-// Pipelined (staged): the pose table and pass A of each super-batch run on
-// the volume's staging stream into staging slot s (alternating), after the caller's input
-// stream and after the slot's previous reader (the super-batch two back); the volume's stream
-// waits for them before its batch cut, and the input stream waits for them too (the inputs
-// stay ordered before the caller's next writes).  Pass A's statistics go to the slot's own
-// striped buffer, summed into d_user on the volume's stream.
-
-static int stage_streams() {
-  const char* e = getenv("DMF_BK_STAGE_STREAMS");
-  return e && atoi(e) == 2 ? 2 : 1;
+// Frees the brick pipeline's scratch (both slots), after the work in flight that may read
+// it: a volume switching between serial and pipelined calls re-plans its slots against the
+// budget (one slot of the whole budget, or two of half).
+static int bk_release(dmf_volume* v) {
+  static const int kSlots[] = {kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkWgBase, kScBkCtl, kScBkPoseCnt,
+                               kScBkPoseBase, kScBkBatch, kScBkWgList, kScBkRays1, kScBkWgBase1, kScBkWgList1,
+                               kScBkPoseCnt1, kScBkBatch1, kScBkBricks1, kScBkCtl1, kScBkPairs1, kScBkPairsB1,
+                               kScBkPoseBase1};
+  if (v->stream) DMF_HIP(hipStreamSynchronize(v->stream));
+  if (v->stage) DMF_HIP(hipStreamSynchronize(v->stage));
+  for (int k : kSlots) {
+    if (k < (int)v->scratch.size() && v->scratch[k].first) {
+      DMF_HIP(hipFree(v->scratch[k].first));
+      v->scratch[k] = {nullptr, 0};
+    }
+  }
+  v->bk_last_bt = nullptr;
+  return DMF_OK;
 }
 
+// Brick-owned fusion of P frames (kernels above).  Only enqueues work: per super-batch,
+// pass A over all its poses, the device's batch cut, then per batch the brick layout
+// (k_bk_batch_counts, k_bk_scan), pass B and phase F; a launch past the device's batch
+// count exits at once.  Phase F reads its part count itself (its persistent workgroups exit
+// when the queue is empty).
+// Pipelined (staged): the pose table, pass A, the batch cut, the brick
+// layout and pass B of each super-batch run on the volume's staging stream into staging slot
+// s (alternating), after the caller's input stream and after the slot's previous reader
+// (event st_free[s]); phase F runs on the volume's stream after pass B's event; the input
+// stream waits for pass A (the inputs stay ordered before the caller's next writes).  Pass
+// A's statistics go to the slot's own striped buffer, summed into d_user on the volume's
+// stream.  Serial calls use slot 0 on the volume's stream; once the staging stream exists
+// they record st_free[0] too, so that a later pipelined call on slot 0 waits for them.
 static int stage_init(dmf_volume* v) {
   if (v->stage) return DMF_OK;
   DMF_HIP(hipStreamCreateWithFlags(&v->stage, hipStreamNonBlocking));
-  DMF_HIP(hipStreamCreateWithFlags(&v->stage1, hipStreamNonBlocking));
   DMF_HIP(hipEventCreateWithFlags(&v->st_in, hipEventDisableTiming));
   for (int k = 0; k < 2; ++k) {
     DMF_HIP(hipEventCreateWithFlags(&v->st_done[k], hipEventDisableTiming));
@@ -2403,50 +1679,33 @@ static int stage_init(dmf_volume* v) {
     DMF_HIP(hipEventCreateWithFlags(&v->st_b[k], hipEventDisableTiming));
     v->st_free_set[k] = false;
   }
+  // work already enqueued on the volume's stream (a serial call's slot 0 readers) precedes
+  // the first staged use of slot 0
+  DMF_HIP(hipEventRecord(v->st_free[0], v->stream));
+  v->st_free_set[0] = true;
   return DMF_OK;
 }
 
 static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint16_t* d_depth, const PoseX* tab,
                        const float* d_poses, int P, const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses,
-                       unsigned long long* st, uint64_t* d_user, bool staged) {
+                       unsigned long long* st, uint64_t* d_user, bool staged, bool capturing) {
   BkPlan pl;
   DMF_TRY(bk_plan(v, cp, g, P, pl));
   const BkGeom& bg = pl.bg;
   DMF_TRY(bk_attributes());
   BkBufs b;
   if (staged) DMF_TRY(stage_init(v));
-  // staged pass B (DMF_BK_STAGE=2): the batch cut, brick layout and pass B run on the staging
-  // stream too, into the slot's own pair records; only phase F stays on the volume's stream
-  const bool stage_b = staged && stage_level() >= 2;
-  // issue priority of the staged passes' waves (A/B: DMF_BK_PRIO 0-3)
-  const int prio = [&] {
-    const char* e = getenv("DMF_BK_PRIO");
-    return staged ? (e ? std::max(0, std::min(atoi(e), 3)) : 0) : 0;
-  }();
+  const bool slab = v->fuse_variant != DMF_FUSE_CELL_WALK;
   // pass A with 16-bit histogram counts (a workgroup's pairs per brick <= span * 64 rays)
-  const bool a16 = (int64_t)pl.span * 64 <= 65535 && [] {
-    const char* e = getenv("DMF_BK_A16");  // A/B: 0 = 32-bit counts
-    return !(e && atoi(e) == 0);
-  }();
+  const bool a16 = (int64_t)pl.span * 64 <= 65535;
   const unsigned nf = (unsigned)cu_count(v->device);
-  const int fv = fuse_variant();
-  const bool lpt_on = [] {  // A/B: DMF_BK_LPT=0 hands the parts out in brick order
-    const char* e = getenv("DMF_BK_LPT");
-    return !(e && atoi(e) == 0);
-  }();
-  const bool tlist = [] {  // A/B: DMF_BK_TLIST=0 makes pass B initialise its whole brick histogram
-    const char* e = getenv("DMF_BK_TLIST");
-    return !(e && atoi(e) == 0);
-  }();
   for (int64_t s0 = 0; s0 < P; s0 += pl.PS) {
     const int64_t ps = std::min<int64_t>(pl.PS, P - s0);
     const unsigned nwg = (unsigned)(ps * pl.wg_pose);
     const int slot = staged ? v->st_slot : 0;
-    DMF_TRY(bk_scratch(v, pl, b, slot, stage_b));
-    const uint2* lpt = lpt_on ? b.order : nullptr;  // (the tail split needs the order: bk_plan)
-    // one staging stream, or one per slot (A/B DMF_BK_STAGE_STREAMS=2: a slot's pass A may
-    // then start as soon as the slot is free, beside the other slot's pass B)
-    const hipStream_t sa = staged ? (slot && stage_streams() == 2 ? v->stage1 : v->stage) : v->stream;
+    DMF_TRY(bk_scratch(v, pl, b, slot));
+    // everything but phase F: the staging stream (pipelined) or the volume's stream
+    const hipStream_t sa = staged ? v->stage : v->stream;
     const PoseX* tab_a = staged ? nullptr : tab + s0;
     unsigned long long* st_a = st;
     if (staged) {
@@ -2471,123 +1730,66 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       hipLaunchKernelGGL(k_bk_rays<true>, dim3(nwg), dim3(pl.ab_threads), sizeof(uint32_t) * ((bg.nbricks + 1) / 2), sa,
                          g, cp, d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx,
                          (int)pl.ppose, pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride,
-                         b.pose_pairs, st_a, prio);
+                         b.pose_pairs, st_a);
     else
       hipLaunchKernelGGL(k_bk_rays<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, g, cp,
                          d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
-                         pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st_a,
-                         prio);
+                         pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st_a);
     DMF_LAUNCH_CHECK();
     if (staged) {
       DMF_HIP(hipEventRecord(v->st_done[slot], sa));
-      DMF_HIP(hipStreamWaitEvent(v->stream, v->st_done[slot], 0));
       DMF_HIP(hipStreamWaitEvent(v->in_stream, v->st_done[slot], 0));
-      if (st) DMF_TRY(stats_end(v, st_a, d_user, kStatWidth));
+      if (st) {  // pass A's statistics, summed on the volume's stream after pass A
+        DMF_HIP(hipStreamWaitEvent(v->stream, v->st_done[slot], 0));
+        DMF_TRY(stats_end(v, st_a, d_user, kStatWidth));
+      }
     }
-    const hipStream_t sl = stage_b ? sa : v->stream;  // batch cut, brick layout, pass B
-    hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sl, (int)ps, (const unsigned long long*)b.pose_pairs,
+    hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sa, (int)ps, (const unsigned long long*)b.pose_pairs,
                        (unsigned long long)pl.pair_cap, pl.max_poses, b.bt);
     DMF_LAUNCH_CHECK();
     v->bk_last_bt = b.bt;
     const int64_t jm = pl.jmax(ps);
     for (int64_t j = 0; j < jm; ++j) {
       // batch j reuses the slot's pair records and part queue: after batch j-1's phase F
-      if (stage_b && j > 0) DMF_HIP(hipStreamWaitEvent(sl, v->st_free[slot], 0));
-      DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sl));
-      hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sl, bg.nbricks,
+      if (staged && j > 0) DMF_HIP(hipStreamWaitEvent(sa, v->st_free[slot], 0));
+      DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sa));
+      hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sa, bg.nbricks,
                          (int)j, (const uint32_t*)b.bt, (const uint32_t*)b.pose_cnt, b.pose_base, b.cnt);
       DMF_LAUNCH_CHECK();
       if (bg.nbricks > 4096)
-        hipLaunchKernelGGL(k_bk_scan<true>, dim3(1), dim3(1024), 0, sl, bg.nbricks, (const uint32_t*)b.cnt, b.off,
+        hipLaunchKernelGGL(k_bk_scan<true>, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off,
                            b.part_pref, b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       else
-        hipLaunchKernelGGL(k_bk_scan<false>, dim3(1), dim3(1024), 0, sl, bg.nbricks, (const uint32_t*)b.cnt, b.off,
+        hipLaunchKernelGGL(k_bk_scan<false>, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off,
                            b.part_pref, b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       DMF_LAUNCH_CHECK();
-#define DMF_BK_PAIRS(...)                                                                                          \
-  hipLaunchKernelGGL((k_bk_pairs<__VA_ARGS__>), dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sl, (int)pl.ppose,  \
-                     pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off,                   \
-                     (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,             \
-                     tlist ? (const uint32_t*)b.wgl : nullptr, pl.wgl_stride, b.pra, b.prb, prio)
-      if (fv == 48)  // wave-aggregated slot atomics (the previous default)
-        DMF_BK_PAIRS(true, true);
-      else if (fv == 65)
-        DMF_BK_PAIRS(true, false, true, true);
-      else if (fv == 66)
-        DMF_BK_PAIRS(true, false, true, true, true);
-      else if (is_rec20_variant(fv))
-        DMF_BK_PAIRS(true, false, true);
-      else if (is_slab_variant(fv))
-        DMF_BK_PAIRS(true, false);
+      if (slab)
+        hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,
+                           pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off,
+                           (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
+                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb);
       else
-        DMF_BK_PAIRS(false);
-#undef DMF_BK_PAIRS
+        hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,
+                           pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off,
+                           (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
+                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb);
       DMF_LAUNCH_CHECK();
-      if (stage_b) {
-        DMF_HIP(hipEventRecord(v->st_b[slot], sl));
+      if (staged) {
+        DMF_HIP(hipEventRecord(v->st_b[slot], sa));
         DMF_HIP(hipStreamWaitEvent(v->stream, v->st_b[slot], 0));
       }
-#define DMF_BK_FUSE(R, S, U, N, C, B)                                                                           \
-  hipLaunchKernelGGL((k_bk_fuse<R, S, U, N, C, B>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,            \
-                     (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
-                     (const uint32_t*)b.part_pref, b.ctl, d_hits, d_misses, st)
-#define DMF_BK_FUSE_S(R, S, U, N)                                                                              \
-  hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,                \
-                     (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
-                     (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st)
-#define DMF_BK_FUSE_S20(R, S, U, N)                                                                            \
-  hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N, false, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,   \
-                     (const uint4*)b.pra, (const void*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,    \
-                     (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st)
-#define DMF_BK_FUSE_SB(R, S, U, N)                                                                             \
-  hipLaunchKernelGGL((k_bk_fuse_s<R, S, U, N, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,          \
-                     (const uint4*)b.pra, (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,   \
-                     (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st)
-      switch (fv) {
-        case 40: DMF_BK_FUSE(16, 8, 8, 1, 0, true); break;
-        case 41: DMF_BK_FUSE(16, 8, 8, 1, 0, false); break;
-        case 42: DMF_BK_FUSE(32, 8, 8, 2, 0, false); break;
-        case 43: DMF_BK_FUSE(16, 8, 8, 1, 256, true); break;
-        case 45: DMF_BK_FUSE_S(24, 8, 4, 1); break;
-        case 46: DMF_BK_FUSE_S(32, 8, 4, 1); break;
-        case 47: DMF_BK_FUSE_S(40, 8, 4, 1); break;
-        case 48: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // with k_bk_pairs<true, true>
-        case 49: DMF_BK_FUSE_S(32, 8, 4, 2); break;
-        case 50: DMF_BK_FUSE_SB(16, 8, 4, 1); break;
-        case 51: DMF_BK_FUSE_SB(32, 8, 4, 2); break;
-        case 44: DMF_BK_FUSE_S(16, 8, 4, 1); break;  // the round-1 default
-        case 52: DMF_BK_FUSE_S(24, 16, 4, 1); break;  // the default until the ownership-code walk
-        case 53: DMF_BK_FUSE_S(24, 32, 4, 1); break;  // 24-B records (the round-2 default)
-        case 54: DMF_BK_FUSE_S(24, 64, 4, 1); break;
-        case 55: DMF_BK_FUSE_S(20, 32, 4, 1); break;
-        case 56: DMF_BK_FUSE_S(28, 32, 4, 1); break;
-        case 58: DMF_BK_FUSE_S20(20, 32, 4, 1); break;
-        case 59: DMF_BK_FUSE_S20(28, 32, 4, 1); break;
-        case 60: DMF_BK_FUSE_S20(32, 32, 4, 1); break;
-        case 61: DMF_BK_FUSE_S20(24, 16, 4, 1); break;
-        case 62: DMF_BK_FUSE_S20(24, 32, 3, 1); break;
-        case 63: DMF_BK_FUSE_S20(24, 32, 5, 1); break;
-        case 64:
-          hipLaunchKernelGGL((k_bk_fuse_s<24, 32, 4, 1, false, true, true>), dim3(nf), dim3(kBkThreads), 0, v->stream, g,
-                             bg, (const uint4*)b.pra, (const void*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
-                             (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits, d_misses, st);
-          break;
-        case 67:
-          hipLaunchKernelGGL((k_bk_fuse_s<24, 32, 4, 1, false, true, false, true>), dim3(nf), dim3(kBkThreads), 0,
-                             v->stream, g, bg, (const uint4*)b.pra, (const void*)b.prb, (const uint32_t*)b.off,
-                             (const uint32_t*)b.cnt, (const uint32_t*)b.part_pref, lpt, pl.part_max, b.ctl, d_hits,
-                             d_misses, st);
-          break;
-        default: DMF_BK_FUSE_S20(24, 32, 4, 1); break;  // 0, 57
-      }
-#undef DMF_BK_FUSE
-#undef DMF_BK_FUSE_S
-#undef DMF_BK_FUSE_S20
-#undef DMF_BK_FUSE_SB
+      if (slab)
+        hipLaunchKernelGGL((k_bk_fuse_s<24, 32, 4>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,
+                           (const uint4*)b.pra, (const uint32_t*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
+                           (const uint2*)b.order, pl.part_max, b.ctl, d_hits, d_misses, st);
+      else
+        hipLaunchKernelGGL((k_bk_fuse<16, 8, 8>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg, (const uint4*)b.pra,
+                           (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
+                           (const uint32_t*)b.part_pref, b.ctl, d_hits, d_misses, st);
       DMF_LAUNCH_CHECK();
-      if (stage_b) DMF_HIP(hipEventRecord(v->st_free[slot], v->stream));  // batch j's phase F
+      if (staged) DMF_HIP(hipEventRecord(v->st_free[slot], v->stream));  // batch j's phase F
     }
-    if (staged) {  // the slot's last readers (pass B and the batch layout, or phase F) are enqueued
+    if (staged || (v->stage && !capturing)) {  // the slot's last reader (phase F) is enqueued
       DMF_HIP(hipEventRecord(v->st_free[slot], v->stream));
       v->st_free_set[slot] = true;
     }
@@ -2627,79 +1829,72 @@ static int check_fuse(const dmf_volume* v, const dmf_camera* cam, int P, const d
   return DMF_OK;
 }
 
+static const char* variant_kernel(int fv) {
+  return fv == DMF_FUSE_LDS_BOX ? kNameLds : (fv == DMF_FUSE_CELL_WALK ? kNameCell : kNameSlab);
+}
+
 }  // namespace dmf
 
 using namespace dmf;
 
 extern "C" {
 
-static const char* variant_name(int v) {
-  switch (v) {
-    case 1: return "dmf::k_fuse_direct";
-    case 24: return "dmf::k_fuse_r<10, 1280, 1>";
-    case 30: return "dmf::k_fuse_l<10, 1280>";
-    case 31: return "dmf::k_fuse_l<12, 1280>";
-    case 32: return "dmf::k_fuse_l<14, 1536>";
-    case 33: return "dmf::k_fuse_l<12, 1536>";
-    case 40: return "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>";
-    case 41: return "dmf::k_bk_fuse<16, 8, 8, 1, 0, false>";
-    case 42: return "dmf::k_bk_fuse<32, 8, 8, 2, 0, false>";
-    case 43: return "dmf::k_bk_fuse<16, 8, 8, 1, 256, true>";
-    case 45: return "dmf::k_bk_fuse_s<24, 8, 4, 1, false>";
-    case 46: return "dmf::k_bk_fuse_s<32, 8, 4, 1, false>";
-    case 47: return "dmf::k_bk_fuse_s<40, 8, 4, 1, false>";
-    case 48: return "dmf::k_bk_fuse_s<16, 8, 4, 1, false> (pairs: wave-aggregated slots)";
-    case 49: return "dmf::k_bk_fuse_s<32, 8, 4, 2, false>";
-    case 50: return "dmf::k_bk_fuse_s<16, 8, 4, 1, true>";
-    case 51: return "dmf::k_bk_fuse_s<32, 8, 4, 2, true>";
-    case 44: return "dmf::k_bk_fuse_s<16, 8, 4, 1, false>";
-    case 52: return "dmf::k_bk_fuse_s<24, 16, 4, 1, false>";
-    case 54: return "dmf::k_bk_fuse_s<24, 64, 4, 1, false>";
-    case 55: return "dmf::k_bk_fuse_s<20, 32, 4, 1, false>";
-    case 56: return "dmf::k_bk_fuse_s<28, 32, 4, 1, false>";
-    case 58: return "dmf::k_bk_fuse_s<20, 32, 4, 1, false, true>";
-    case 59: return "dmf::k_bk_fuse_s<28, 32, 4, 1, false, true>";
-    case 60: return "dmf::k_bk_fuse_s<32, 32, 4, 1, false, true>";
-    case 61: return "dmf::k_bk_fuse_s<24, 16, 4, 1, false, true>";
-    case 62: return "dmf::k_bk_fuse_s<24, 32, 3, 1, false, true>";
-    case 63: return "dmf::k_bk_fuse_s<24, 32, 5, 1, false, true>";
-    case 64: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true, true>";
-    case 67: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true, false, true>";
-    case 53: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false>";
-    default: return "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true>";  // 0, 57; grids over 1024 cells per axis: k_fuse_l<12, 1280>
-  }
+const char* dmf_fuse_kernel_name(const dmf_volume* v) {
+  if (!v) return "";
+  return v->last_kernel ? v->last_kernel : variant_kernel(v->fuse_variant);
 }
 
-const char* dmf_fuse_kernel(void) {
-  const char* k = g_last_kernel.load();
-  return k ? k : variant_name(fuse_variant());
-}
-
-int dmf_fuse_set_variant(int32_t variant) {
+int dmf_fuse_set_variant(dmf_volume* v, int32_t variant) {
+  DMF_API_BEGIN
+  if (!v) return fail(DMF_ERR_INVALID, "null volume");
   if (!is_known_variant(variant)) return fail(DMF_ERR_INVALID, "unknown fusion variant %d", variant);
-  g_fuse_variant.store(variant, std::memory_order_relaxed);
-  g_last_kernel.store(nullptr);
+  v->fuse_variant = variant;
+  v->last_kernel = nullptr;
+  return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_fuse_get_variant(const dmf_volume* v, int32_t* variant) {
+  if (!v || !variant) return fail(DMF_ERR_INVALID, "null argument");
+  *variant = v->fuse_variant;
+  return DMF_OK;
+}
+
+int dmf_volume_set_knob(dmf_volume* v, int32_t knob, int64_t value) {
+  if (!v) return fail(DMF_ERR_INVALID, "null volume");
+  if (knob < 1 || knob >= DMF_KNOB_COUNT) return fail(DMF_ERR_INVALID, "unknown knob %d", knob);
+  v->knob[knob] = value;
+  return DMF_OK;
+}
+
+int dmf_volume_get_knob(const dmf_volume* v, int32_t knob, int64_t* value) {
+  if (!v || !value) return fail(DMF_ERR_INVALID, "null argument");
+  if (knob < 1 || knob >= DMF_KNOB_COUNT) return fail(DMF_ERR_INVALID, "unknown knob %d", knob);
+  *value = v->knob[knob];
   return DMF_OK;
 }
 
 int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t max_scratch_bytes) {
   DMF_API_BEGIN
   DMF_TRY(check_fuse(v, cam, P, &kDefaultParamsForCheck));
-  if (max_scratch_bytes) v->bk_budget = max_scratch_bytes;
+  if (max_scratch_bytes && max_scratch_bytes != v->bk_budget) {
+    DMF_TRY(bk_release(v));  // the slots are re-planned against the new budget
+    v->bk_budget = max_scratch_bytes;
+  }
   const CamP cp = cam_params(cam);
   const Geom g = v->geom();
   void* tab;
   DMF_TRY(scratch(v, kScPoses, sizeof(PoseX) * (size_t)P, &tab));
   unsigned long long* st;
   DMF_TRY(stats_begin(v, &st));
-  if (brick_path_ok(g)) {
+  if (use_bricks(v, g)) {
     BkPlan pl;
     DMF_TRY(bk_plan(v, cp, g, P, pl));
     DMF_TRY(bk_attributes());
     BkBufs set;
-    DMF_TRY(bk_scratch(v, pl, set));
+    DMF_TRY(bk_scratch(v, pl, set, 0));
     if (v->pipelined) {  // the second staging slot, the staging stream, slot pose tables and statistics
-      DMF_TRY(bk_scratch(v, pl, set, 1, stage_level() >= 2));
+      DMF_TRY(bk_scratch(v, pl, set, 1));
       DMF_TRY(stage_init(v));
       void* t;
       for (int k = 0; k < 2; ++k) {
@@ -2719,10 +1914,9 @@ int dmf_fuse_plan(const dmf_volume* v, const dmf_camera* cam, int32_t P, dmf_fus
   DMF_TRY(check_fuse(v, cam, P, &kDefaultParamsForCheck));
   *out = dmf_fuse_plan_info{};
   const Geom g = v->geom();
-  const int fv = fuse_variant();
   out->max_batches = 1;
   out->poses_per_batch = P;
-  if (brick_path_ok(g) && (is_brick_variant(fv) || (fv == 0 && brick_preferred(g)))) {
+  if (use_bricks(v, g)) {
     BkPlan pl;
     DMF_TRY(bk_plan(v, cam_params(cam), g, P, pl));
     out->brick = 1;
@@ -2730,9 +1924,9 @@ int dmf_fuse_plan(const dmf_volume* v, const dmf_camera* cam, int32_t P, dmf_fus
     out->max_batches = (int32_t)pl.max_batches(P);
     out->record_bytes = (int32_t)pl.rec_bytes;
     out->pair_capacity = (uint64_t)pl.pair_cap;
-    out->scratch_bytes = pl.pair_cap * pl.rec_bytes + (uint64_t)pl.PS * pl.per_pose_bytes +
-                         sizeof(uint32_t) * (3 * (uint64_t)pl.bg.nbricks + 2 * pl.max_parts());
+    out->scratch_bytes = pl.slot_bytes * (uint64_t)pl.slots;  // both staging slots when pipelined
     out->super_batch_poses = (int32_t)pl.PS;
+    out->slots = pl.slots;
   }
   return DMF_OK;
   DMF_API_END
@@ -2745,6 +1939,7 @@ int dmf_fuse_batches_used(dmf_volume* v, int32_t* batches) {
   *batches = 0;
   if (!v->bk_last_bt) return DMF_OK;
   uint32_t J = 0;
+  if (v->stage) DMF_HIP(hipStreamSynchronize(v->stage));  // the table of a staged call
   DMF_HIP(hipMemcpyAsync(&J, v->bk_last_bt, sizeof(J), hipMemcpyDeviceToHost, v->stream));
   DMF_HIP(hipStreamSynchronize(v->stream));
   *batches = (int32_t)J;
@@ -2777,8 +1972,10 @@ int dmf_fuse_set_input_stream(dmf_volume* v, void* stream) {
   DMF_API_BEGIN
   if (!v) return fail(DMF_ERR_INVALID, "null volume");
   DMF_TRY(activate(v));
+  const bool pipelined = stream != nullptr;
+  if (pipelined != v->pipelined) DMF_TRY(bk_release(v));  // one slot of the budget, or two of half
   v->in_stream = (hipStream_t)stream;
-  v->pipelined = stream != nullptr;
+  v->pipelined = pipelined;
   return DMF_OK;
   DMF_API_END
 }
@@ -2795,48 +1992,25 @@ static int fuse_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_d
   if (!d_depth || !d_poses || !d_hits || !d_misses) return fail(DMF_ERR_INVALID, "null device buffer");
   const CamP cp = cam_params(cam);
   const Geom g = v->geom();
-  // default (variant 0): the brick-owned pipeline where it applies (longest axis 256-1024
-  // cells), the LDS-box kernel k_fuse_l<12, 1280> otherwise
-  const int fv = fuse_variant();
-  const bool brick = brick_path_ok(g) && (is_brick_variant(fv) || (fv == 0 && brick_preferred(g)));
-  bool staged = false;
-  if (brick && allow_stage && v->pipelined) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    DMF_HIP(hipStreamIsCapturing(v->stream, &cs));
-    staged = cs == hipStreamCaptureStatusNone;
-  }
+  const bool brick = use_bricks(v, g);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  DMF_HIP(hipStreamIsCapturing(v->stream, &cs));
+  const bool capturing = cs != hipStreamCaptureStatusNone;
+  const bool staged = brick && allow_stage && v->pipelined && !capturing;
   PoseX* tab = nullptr;
   if (!staged) DMF_TRY(pose_table(v, d_poses, P, true, &tab));
   unsigned long long* st = nullptr;
   if (d_stats) DMF_TRY(stats_begin(v, &st));
-  const int pkx = (cp.W + 7) / 8;
   if (brick) {
-    g_last_kernel.store(variant_name(fv));
-    DMF_TRY(fuse_bricks(v, cp, g, d_depth, tab, d_poses, P, prm, d_hits, d_misses, st, d_stats, staged));
-    if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
+    v->last_kernel = variant_kernel(v->fuse_variant);
+    DMF_TRY(fuse_bricks(v, cp, g, d_depth, tab, d_poses, P, prm, d_hits, d_misses, st, d_stats, staged, capturing));
+  } else {
+    const int pkx = (cp.W + 7) / 8;
+    hipLaunchKernelGGL((k_fuse_l<12, 1280>), dim3((unsigned)(pkx * ((cp.H + 7) / 8)), (unsigned)P), dim3(64), 0,
+                       v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, d_misses, st);
     DMF_LAUNCH_CHECK();
-    return DMF_OK;
+    v->last_kernel = kNameLds;
   }
-#define DMF_FUSE_LAUNCH_R(K, NR)                                                                               \
-  hipLaunchKernelGGL(K, dim3((unsigned)(pkx * ((cp.H + 8 * (NR) - 1) / (8 * (NR)))), (unsigned)P), dim3(64), 0,        \
-                     v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, d_misses, st)
-  switch (fuse_variant()) {
-    case 1: {
-      const int tx = (cp.W + 15) / 16, ty = (cp.H + 15) / 16;
-      hipLaunchKernelGGL(k_fuse_direct, dim3((unsigned)(tx * ty), (unsigned)P), dim3(256), 0, v->stream, g, cp,
-                         d_depth, tab, prm->dmin_mm, prm->dmax_mm, tx, d_hits, d_misses, st);
-      break;
-    }
-    case 24: DMF_FUSE_LAUNCH_R((k_fuse_r<10, 1280, 1>), 1); break;
-    case 30: DMF_FUSE_LAUNCH_R((k_fuse_l<10, 1280>), 1); break;
-    case 31: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1280>), 1); break;
-    case 32: DMF_FUSE_LAUNCH_R((k_fuse_l<14, 1536>), 1); break;
-    case 33: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1536>), 1); break;
-    default: DMF_FUSE_LAUNCH_R((k_fuse_l<12, 1280>), 1); break;
-  }
-  g_last_kernel.store(is_brick_variant(fv) || fv == 0 ? "dmf::k_fuse_l<12, 1280>" : variant_name(fv));
-#undef DMF_FUSE_LAUNCH_R
-  DMF_LAUNCH_CHECK();
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
   DMF_LAUNCH_CHECK();
   return DMF_OK;

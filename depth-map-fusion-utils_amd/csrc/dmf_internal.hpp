@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "dmf.h"
+#include "dmf_diag.h"
 #include "dmf_geom.hpp"
 
 namespace dmf {
@@ -245,11 +246,14 @@ struct dmf_volume {
   bool pipelined = false;
   hipStream_t in_stream = nullptr;  // the caller's input stream
   hipStream_t stage = nullptr;      // staging stream (created on first use)
-  hipStream_t stage1 = nullptr;     // slot 1's own staging stream (DMF_BK_STAGE_STREAMS=2)
   hipEvent_t st_in = nullptr, st_done[2] = {nullptr, nullptr}, st_free[2] = {nullptr, nullptr};
   hipEvent_t st_b[2] = {nullptr, nullptr};  // pass B of the slot's batch enqueued (staged pass B)
   bool st_free_set[2] = {false, false};
   int st_slot = 0;
+  // diagnostic / A-B controls (include/dmf_diag.h): fusion implementation and knobs
+  int fuse_variant = 0;
+  const char* last_kernel = nullptr;  // the fusion kernel of the latest call
+  int64_t knob[DMF_KNOB_COUNT] = {};
   // scratch arena
   std::vector<std::pair<void*, size_t>> scratch;
 

@@ -1,5 +1,8 @@
 // dmf_io.hip — persistent form of the fused log-odds grid (optional
-// checkpoint/resume).  Host code only (no GPU needed).
+// checkpoint/resume).  Host code only (no GPU needed).  The file holds the FINAL clamped
+// int16 grid (what the reference's consumers read), not the int32 hit/miss counters: it is a
+// dump of a finished fusion, from which a new fusion cannot resume exactly (clamped log-odds
+// do not accumulate; keep the counters for that).
 //
 // The reference's only persistent outputs are text files (writeCameraLocations,
 // FileRoutines.hpp:98-112, and a PCD); the fusion grid it never had.  The file is a
@@ -11,6 +14,10 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <string>
+
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "dmf_host.hpp"
 
@@ -95,20 +102,28 @@ int dmf_grid_save(const char* path, const dmf_grid_header* h, const int16_t* log
     if (h->dims[a] < 1 || h->dims[a] > (1 << 20)) return fail(DMF_ERR_INVALID, "bad dims");
   uint8_t head[kHeaderBytes];
   put_header(h, head);
+  // written to path.tmp, flushed to disk, then renamed over path: a crash or a full disk
+  // mid-write leaves the previous file intact
+  const std::string tmp = std::string(path) + ".tmp";
   File out;
-  out.f = fopen(path, "wb");
-  if (!out.f) return fail(DMF_ERR_INVALID, "cannot open %s for writing", path);
+  out.f = fopen(tmp.c_str(), "wb");
+  if (!out.f) return fail(DMF_ERR_INVALID, "cannot open %s for writing", tmp.c_str());
   const size_t n = (size_t)cells_of(h->dims);
   uint32_t crc = crc32().update(0, head, sizeof(head));
   crc = crc32().update(crc, logodds, n * sizeof(int16_t));
-  if (fwrite(head, 1, sizeof(head), out.f) != sizeof(head) ||
-      fwrite(logodds, sizeof(int16_t), n, out.f) != n || fwrite(&crc, 4, 1, out.f) != 1)
-    return fail(DMF_ERR_INVALID, "short write to %s", path);
-  if (fclose(out.f) != 0) {
-    out.f = nullptr;
-    return fail(DMF_ERR_INVALID, "close of %s failed", path);
-  }
+  const bool ok = fwrite(head, 1, sizeof(head), out.f) == sizeof(head) &&
+                  fwrite(logodds, sizeof(int16_t), n, out.f) == n && fwrite(&crc, 4, 1, out.f) == 1 &&
+                  fflush(out.f) == 0 && fsync(fileno(out.f)) == 0;
+  const bool closed = fclose(out.f) == 0;
   out.f = nullptr;
+  if (!ok || !closed) {
+    unlink(tmp.c_str());
+    return fail(DMF_ERR_INVALID, "short write to %s", tmp.c_str());
+  }
+  if (rename(tmp.c_str(), path) != 0) {
+    unlink(tmp.c_str());
+    return fail(DMF_ERR_INVALID, "cannot rename %s to %s", tmp.c_str(), path);
+  }
   return DMF_OK;
   DMF_API_END
 }
@@ -122,6 +137,11 @@ int dmf_grid_load(const char* path, dmf_grid_header* h, int16_t* logodds, int64_
   uint32_t crc = 0;
   DMF_TRY(read_header(in.f, h, &crc));
   const int64_t n = cells_of(h->dims);
+  // the file's size must be exactly header + grid + checksum BEFORE a caller sizes a buffer
+  // from the (not yet checksummed) dims
+  struct stat sb;
+  if (fstat(fileno(in.f), &sb) != 0 || (int64_t)sb.st_size != (int64_t)kHeaderBytes + 2 * n + 4)
+    return fail(DMF_ERR_INVALID, "grid file: size does not match its dims");
   if (!logodds) return DMF_OK;  // header only
   if (cap < n) return fail(DMF_ERR_CAPACITY, "grid of %lld cells, buffer of %lld", (long long)n, (long long)cap);
   if (fread(logodds, sizeof(int16_t), (size_t)n, in.f) != (size_t)n) return fail(DMF_ERR_INVALID, "grid file: short grid");

@@ -688,10 +688,10 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
     EnumList el{v->d_axes, {v->nax[0], v->nax[1], v->nax[2]}, v->d_enum};
     const dim3 grid((unsigned)((nelem + 255) / 256), (unsigned)P);
     const int depth0 = enumerate ? 1 : 50;  // :81 vs :172
-    static const int rev_kernel = [] {
-      const char* e = getenv("DMF_REVERSE_KERNEL");  // 0 plain, 1 plain + brick skip, >= 2 queue + distance field (2 = default)
-      return e ? atoi(e) : 2;
-    }();
+    // DMF_KNOB_REVERSE_KERNEL (dmf_diag.h): 0 = the queue + distance field (internal mode 2),
+    // 1 = the plain march, 2 = plain + brick skip (internal 0, 1); >= 3 measured alternatives
+    const int64_t kr = v->knob[DMF_KNOB_REVERSE_KERNEL];
+    const int rev_kernel = kr == 0 ? 2 : (kr == 1 ? 0 : (kr == 2 ? 1 : (int)kr));
 #define DMF_REV(E, S, NT)                                                                                        \
   hipLaunchKernelGGL((k_reverse<E, S>), grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab, \
                      nelem, el, depth0, max_march_steps(v), v->dstar, viz, NT, vis, good, words, st, found, hz)
@@ -935,18 +935,12 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, co
   if (stats) wave_add_u64(&stats[0], (unsigned long long)samples);
 }
 
-// DMF_FWD_SKIP=0 disables the forward march's empty-space skipping (A/B, diagnostics)
-static bool fwd_skip() {
-  static const bool on = [] {
-    const char* e = getenv("DMF_FWD_SKIP");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// DMF_KNOB_FWD_SKIP = -1 (dmf_diag.h) disables the forward march's empty-space skipping (A/B)
+static bool fwd_skip(const dmf_volume* v) { return v->knob[DMF_KNOB_FWD_SKIP] >= 0; }
 
 #define DMF_LAUNCH_FORWARD(GRID, ...)                                                                          \
   do {                                                                                                        \
-    if (fwd_skip()) {                                                                                         \
+    if (fwd_skip(v)) {                                                                                         \
       DMF_TRY(ensure_brick_dist(v));                                                                          \
       hipLaunchKernelGGL(k_forward<true>, GRID, dim3(256), 0, v->stream, __VA_ARGS__);                         \
     } else {                                                                                                  \

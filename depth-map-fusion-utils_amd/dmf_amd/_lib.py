@@ -18,6 +18,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("DMF_LIB", os.path.join(PKG_ROOT, "build", "libdmf.so"))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "dmf.h")
+DIAG_HEADER_PATH = os.path.join(REPO_ROOT, "include", "dmf_diag.h")
 
 DMF_OK = 0
 DMF_ERR_INVALID = 1
@@ -49,7 +50,7 @@ class dmf_volume_info(C.Structure):
 class dmf_fuse_plan_info(C.Structure):
     _fields_ = [("brick", C.c_int32), ("max_batches", C.c_int32), ("poses_per_batch", C.c_int32),
                 ("record_bytes", C.c_int32), ("pair_capacity", C.c_uint64), ("scratch_bytes", C.c_uint64),
-                ("super_batch_poses", C.c_int32), ("reserved", C.c_int32)]
+                ("super_batch_poses", C.c_int32), ("slots", C.c_int32)]
 
 
 class dmf_merge_plan(C.Structure):
@@ -79,8 +80,11 @@ SIGNATURES = {
     "dmf_device_count": (C.c_int, [_p]),
     "dmf_fuse_params_default": (None, [_p]),
     "dmf_angle_threshold": (C.c_int, [_p]),
-    "dmf_fuse_kernel": (C.c_char_p, []),
-    "dmf_fuse_set_variant": (C.c_int, [_i32]),
+    "dmf_fuse_kernel_name": (C.c_char_p, [_vp]),
+    "dmf_fuse_set_variant": (C.c_int, [_vp, _i32]),
+    "dmf_fuse_get_variant": (C.c_int, [_vp, _p]),
+    "dmf_volume_set_knob": (C.c_int, [_vp, _i32, _i64]),
+    "dmf_volume_get_knob": (C.c_int, [_vp, _i32, _p]),
     "dmf_volume_create": (C.c_int, [_p, _i32]),
     "dmf_volume_destroy": (C.c_int, [_vp]),
     "dmf_volume_set_stream": (C.c_int, [_vp, _vp]),
@@ -133,6 +137,7 @@ SIGNATURES = {
     "dmf_comm_unique_id": (C.c_int, [_p]),
     "dmf_comm_init_rank": (C.c_int, [_p, _i32, _p, _i32, _i32]),
     "dmf_comm_destroy": (C.c_int, [_vp]),
+    "dmf_comm_shape": (C.c_int, [_vp, _p, _p]),
     "dmf_fuse_counter_cells_padded": (C.c_int, [_vp, _i32, _p]),
     "dmf_fuse_logodds_cells_padded": (C.c_int, [_vp, _i32, _p]),
     "dmf_fuse_allreduce_device": (C.c_int, [_vp, _p, _i64, _vp, _vp]),
@@ -200,10 +205,32 @@ def device_count():
 
 
 def declared_symbols():
-    """Function names declared in include/dmf.h (parsed from the header text)."""
+    """Function names declared in include/dmf.h and include/dmf_diag.h (parsed from the
+    header text)."""
     import re
-    txt = open(HEADER_PATH).read()
+    txt = open(HEADER_PATH).read() + open(DIAG_HEADER_PATH).read()
     return sorted(set(re.findall(r"\b(dmf_[a-z0-9_]+)\s*\(", txt)))
+
+
+# include/dmf_diag.h: fusion implementations and per-volume knobs (diagnostics, A/B, tests)
+FUSE_DEFAULT, FUSE_LDS_BOX, FUSE_CELL_WALK, FUSE_SLAB = 0, 31, 40, 57
+KNOBS = {"super_poses": 1, "pair_cap": 2, "batch_poses": 3, "part_max": 4, "span": 5, "tail_split": 6,
+         "reverse_kernel": 7, "fwd_skip": 8}
+
+
+def set_variant(vol, variant):
+    """dmf_fuse_set_variant on a dmf_amd.VoxelVolume (or a raw handle)."""
+    check(load().dmf_fuse_set_variant(getattr(vol, "_h", vol), int(variant)))
+
+
+def kernel_name(vol):
+    """dmf_fuse_kernel_name: the fusion kernel of the volume's latest call."""
+    return load().dmf_fuse_kernel_name(getattr(vol, "_h", vol)).decode()
+
+
+def set_knob(vol, name, value):
+    """dmf_volume_set_knob by name (KNOBS); 0 = the default."""
+    check(load().dmf_volume_set_knob(getattr(vol, "_h", vol), KNOBS[name], int(value)))
 
 
 def make_camera(K, height=480, width=640):

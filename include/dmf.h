@@ -91,18 +91,8 @@ void dmf_fuse_params_default(dmf_fuse_params* p);
  * dstar the smallest float whose host-libm acosf passes (the function the reference
  * binary calls).  Host-only; no GPU needed. */
 int dmf_angle_threshold(float* dstar);
-/* Diagnostic: name of the (dominant) fusion kernel the most recent dmf_fuse_depth* call
- * of this process launched; before any call (or after dmf_fuse_set_variant), the kernel
- * the selected variant uses on a 512^3 grid. */
-const char* dmf_fuse_kernel(void);
-/* Diagnostic / A-B: select the fusion implementation for this process.  0 = default:
- * the brick-owned pipeline (k_bk_rays, k_bk_scan, k_bk_pairs, k_bk_fuse)
- * when the longest grid axis has 384..1024 cells, k_fuse_l<12, 1280> otherwise; 40 = the
- * brick pipeline whenever it applies (<= 1024 cells per axis); 41-43 = its refill
- * variants; 1 = one device atomic per update; 24, 30-33 = LDS-box kernels (k_fuse_r /
- * k_fuse_l).  Grids over 1024 cells per axis always use k_fuse_l<12, 1280>.  Results are
- * identical for every variant. */
-int dmf_fuse_set_variant(int32_t variant);
+/* The fusion implementation, its kernel name and the tuning / test knobs of a volume are
+ * diagnostics, declared in include/dmf_diag.h (results never depend on them). */
 
 /* ---- VoxelVolume  (Volume.hpp:50-255) ------------------------------------ */
 /* VoxelVolume::VoxelVolume()  Volume.hpp:63 — device = HIP device ordinal. */
@@ -238,9 +228,11 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
 /* Pre-allocate the fusion scratch for calls of up to P frames of `cam`'s size on this
  * volume, so that dmf_fuse_depth_device then neither allocates nor synchronises (e.g. for
  * hipGraph capture).  The brick pipeline fits its ray records, brick tables and (ray,
- * brick) pair records into max_scratch_bytes (0 = keep the current budget; default a third
- * of the device's memory, ~96 GB on MI355X): a call whose pairs exceed the pair capacity
- * is cut into pose batches on the device (dmf_fuse_plan).  Synchronises the stream once. */
+ * brick) pair records into max_scratch_bytes (0 = keep the current budget; default 45 % of
+ * the device's memory, ~130 GB on MI355X): serial calls use one slot of the whole budget,
+ * pipelined calls (dmf_fuse_set_input_stream) two staging slots of half each.  A call whose
+ * pairs exceed a slot's pair capacity is cut into pose batches on the device
+ * (dmf_fuse_plan).  A new budget frees and re-plans the slots.  Synchronises the stream. */
 int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t max_scratch_bytes);
 /* Pipelined fusion (an extension, the reference fuses one frame at a time,
  * tests/Raytracing.cpp:70-76).  Declares that the device inputs (d_depth, d_poses) of later
@@ -251,11 +243,15 @@ int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t m
  * staging stream of the volume that waits only for `stream` and for its staging slot's
  * previous reader, so that they overlap the previous call's phase F; only phase F stays on
  * the volume's stream.  Two staging slots alternate between super-batches, each with its
- * own pair records and three quarters of the fusion budget (dmf_fuse_reserve).  `stream` is made to
+ * own pair records and half of the fusion budget (dmf_fuse_reserve).  `stream` is made to
  * wait until the call's pass A has read the inputs, so inputs rewritten there afterwards
- * stay ordered.  Results are identical to the serial order.  stream = NULL restores the serial order (the
- * default); a volume stream that is capturing a graph always runs serially, and so does the
- * host form dmf_fuse_depth. */
+ * stay ordered.  Results are identical to the serial order, and serial and pipelined calls
+ * may be mixed on one volume without synchronising (a pipelined call waits for the serial
+ * calls before it that used its slot).  Switching the mode frees the fusion scratch (after
+ * synchronising the volume's streams) so that it is re-planned.  stream = NULL restores
+ * the serial order (the default); a volume stream that is capturing a graph always runs
+ * serially, and so does the host form dmf_fuse_depth (a captured graph must not be launched
+ * while pipelined calls of the same volume are in flight: it reads the serial slot). */
 int dmf_fuse_set_input_stream(dmf_volume* v, void* stream);
 /* How a fusion call of P frames of `cam`'s size on this volume is executed (no GPU work,
  * no allocation): brick = 1 for the brick-owned pipeline (k_bk_*), 0 for k_fuse_l.  The
@@ -263,7 +259,8 @@ int dmf_fuse_set_input_stream(dmf_volume* v, void* stream);
  * each into pose batches by the (ray, brick) pairs they really make against pair_capacity
  * records of record_bytes (no host synchronisation); at most max_batches batches, each of at
  * least poses_per_batch frames (the geometric bound rays x (1 + brick boundaries));
- * scratch_bytes = the pipeline's device scratch. */
+ * scratch_bytes = the pipeline's device scratch over its `slots` staging slots (2 when the
+ * calls are pipelined). */
 typedef struct dmf_fuse_plan_info {
   int32_t brick;
   int32_t max_batches;
@@ -272,7 +269,7 @@ typedef struct dmf_fuse_plan_info {
   uint64_t pair_capacity;
   uint64_t scratch_bytes;
   int32_t super_batch_poses;
-  int32_t reserved;
+  int32_t slots;
 } dmf_fuse_plan_info;
 int dmf_fuse_plan(const dmf_volume* v, const dmf_camera* cam, int32_t P, dmf_fuse_plan_info* out);
 /* Diagnostic (synchronises the stream): the pose batches the device cut the latest
@@ -302,6 +299,9 @@ int dmf_rccl_version(int32_t* version);
 int dmf_comm_unique_id(void* id);
 int dmf_comm_init_rank(void** comm, int32_t nranks, const void* id, int32_t rank, int32_t device);
 int dmf_comm_destroy(void* comm);
+/* ncclCommCount / ncclCommUserRank of a communicator (e.g. torch's, to report the ranks the
+ * merge's collectives span). */
+int dmf_comm_shape(void* comm, int32_t* nranks, int32_t* rank);
 /* Tiled counter elements per array padded to whole tile rows per rank (>= the unpadded
  * dmf_fuse_counter_cells), and the padded int16 log-odds grid (>= xdim*ydim*zdim) used by
  * dmf_fuse_merge_finalize_device.  Counters = [hits | misses], each n_padded elements. */

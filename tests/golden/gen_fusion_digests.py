@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/fusion_digests.json: the CPU oracle's 3D-DDA log-odds fusion
+(oracle.cpp dda_ray / fuse_finalize) of bench.py's synthetic workloads at
+their FULL size, so that the GPU runs check themselves against the oracle without running
+it: bench.py prints digest_expected / digest_match, and the -m gpu suite compares the timed
+(pipelined) mode's grid with it (tests/test_gpu_pipeline.py).
+
+Inputs are bench.py's own (make_inputs): the GLOBAL pose set of a run on N GPUs is
+scene.fibonacci_poses(P_per_gpu * N, seed=1234), depth rendered by scene.render_frames with
+scene.intrinsics(W, H), grid [-0.5, 0.5]^3 at n^3, depth accepted in [DEPTH_MIN_MM,
+DEPTH_MAX_MM), OctoMap-default log-odds parameters.  The merged grid after the rank shards
+are summed equals the oracle fusing all global poses (integer counters), so one digest per
+global pose set covers N = 1 and the N-GPU merge alike.  Digest = sha256 of the x-major
+int16 log-odds bytes, first 16 hex digits (bench.py logodds_digest).
+
+usage: python tests/golden/gen_fusion_digests.py [keys...]   (OpenMP oracle, all host cores;
+       config4 N = 1/2/4/8 take ~1-8 min each here)
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "depth-map-fusion-utils_amd")]
+from dmf_amd import scene  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+OUT = os.path.join(HERE, "fusion_digests.json")
+SEED = 1234
+# key -> (grid, W, H, global poses): bench.py at --gpus N (config 4: 128 poses per GPU, the
+# N = 8 set is the 1024-pose anchor), config 2 and config 3 at N = 1
+WORKLOADS = {
+    "config4_shard_N1": (512, 640, 480, 128),
+    "config4_N2": (512, 640, 480, 256),
+    "config4_N4": (512, 640, 480, 512),
+    "config4_N8_anchor": (512, 640, 480, 1024),
+    "config2_N1": (256, 640, 480, 64),
+    "config3_N1": (512, 1280, 720, 256),
+}
+
+
+def oracle_digest(grid, W, H, P, threads):
+    K = scene.intrinsics(W, H)
+    poses = np.ascontiguousarray(scene.fibonacci_poses(P, seed=SEED), np.float32)
+    v = O.Volume()
+    v.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    v.setVolumeSize(grid, grid, grid)
+    v.constructVolume()
+    n = grid ** 3
+    hits = np.zeros(n, np.int32)
+    misses = np.zeros(n, np.int32)
+    tot = np.zeros(3, np.int64)
+    for c0 in range(0, P, 64):  # render and fuse in chunks (host memory)
+        depth = scene.render_frames(K, W, H, poses[c0:c0 + 64])
+        _, _, st = O.fuse_depth(v, K, depth, poses[c0:c0 + 64], dmin=scene.DEPTH_MIN_MM, dmax=scene.DEPTH_MAX_MM,
+                                hits=hits, misses=misses, threads=threads)
+        tot += np.asarray(st, np.int64)
+    lo = O.fuse_finalize(hits, misses, **O.LOGODDS_DEFAULT)
+    return {"grid": grid, "image": f"{W}x{H}", "global_poses": P, "seed": SEED,
+            "logodds_digest": hashlib.sha256(lo.tobytes()).hexdigest()[:16],
+            "updates": int(tot[0]), "rays": int(tot[1]), "hits": int(tot[2]),
+            "hit_cells": int(np.count_nonzero(hits)), "miss_cells": int(np.count_nonzero(misses))}
+
+
+def main():
+    keys = sys.argv[1:] or list(WORKLOADS)
+    out = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    threads = os.cpu_count() or 1
+    for k in keys:
+        t0 = time.time()
+        out[k] = oracle_digest(*WORKLOADS[k], threads=threads)
+        print(f"{k}: {out[k]} ({time.time() - t0:.0f} s)", flush=True)
+        json.dump(out, open(OUT, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -48,7 +48,7 @@ def _oracle_counts(oracle, depth, poses, n):
     return oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
 
 
-@pytest.mark.parametrize("n,variant", [(96, 53), (96, 40), (96, 31)])
+@pytest.mark.parametrize("n,variant", [(96, 57), (256, 0), (96, 40), (96, 31)])
 def test_fuse_device_never_blocks_the_host(oracle, n, variant):
     """dmf_fuse_depth_device only enqueues (include/dmf.h; brick pipeline and the LDS-box
     kernel): with its stream held busy by a ~1 s spin kernel, the call returns while the
@@ -65,33 +65,30 @@ def test_fuse_device_never_blocks_the_host(oracle, n, variant):
     lin = torch.empty(n ** 3, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream(dev)
     vol.set_stream(s.cuda_stream)
-    _lib.check(L.dmf_fuse_set_variant(variant))
-    try:
-        _lib.check(L.dmf_fuse_reserve(vol._h, C.addressof(cam), P, 0))
+    _lib.set_variant(vol, variant)
+    _lib.check(L.dmf_fuse_reserve(vol._h, C.addressof(cam), P, 0))
 
-        def fuse():
-            _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(), P,
-                                               C.addressof(prm), counters.data_ptr(), counters.data_ptr() + 4 * nt,
-                                               None))
-        fuse()  # first call: module loads
+    def fuse():
+        _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(), P,
+                                           C.addressof(prm), counters.data_ptr(), counters.data_ptr() + 4 * nt,
+                                           None))
+    fuse()  # first call: module loads
+    torch.cuda.synchronize(dev)
+    counters.zero_()
+    for _ in range(2):
+        torch.cuda._sleep(2_000_000_000)  # ~1 s of spinning at 2.1-2.4 GHz on the stream
+        t0 = time.perf_counter()
+        fuse()
+        dt = time.perf_counter() - t0
+        busy = not s.query()
         torch.cuda.synchronize(dev)
-        counters.zero_()
-        for _ in range(2):
-            torch.cuda._sleep(2_000_000_000)  # ~1 s of spinning at 2.1-2.4 GHz on the stream
-            t0 = time.perf_counter()
-            fuse()
-            dt = time.perf_counter() - t0
-            busy = not s.query()
-            torch.cuda.synchronize(dev)
-            assert busy and dt < 0.3, (busy, dt)
-        ho, mo, _ = _oracle_counts(oracle, depth, poses, n)
-        for half, exp in ((0, ho), (1, mo)):
-            _lib.check(L.dmf_fuse_counters_to_linear_device(vol._h, counters.data_ptr() + 4 * nt * half,
-                                                            lin.data_ptr()))
-            torch.cuda.synchronize(dev)
-            assert np.array_equal(lin.cpu().numpy(), 2 * exp)
-    finally:
-        _lib.check(L.dmf_fuse_set_variant(0))
+        assert busy and dt < 0.3, (busy, dt)
+    ho, mo, _ = _oracle_counts(oracle, depth, poses, n)
+    for half, exp in ((0, ho), (1, mo)):
+        _lib.check(L.dmf_fuse_counters_to_linear_device(vol._h, counters.data_ptr() + 4 * nt * half,
+                                                        lin.data_ptr()))
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(lin.cpu().numpy(), 2 * exp)
 
 
 def _fused_counters(torch, L, _lib, vol, dev, d_depth, d_poses, cam, prm, P, npad):

@@ -16,6 +16,8 @@ pipeline).  The reference sequence being scaled is the per-frame integration of
 tests/Raytracing.cpp:70-76 / Volume.hpp:199-228.
 """
 import ctypes as C
+import json
+import os
 
 import numpy as np
 import pytest
@@ -23,6 +25,9 @@ import pytest
 import helpers as Hh
 
 pytestmark = pytest.mark.gpu
+
+# the oracle's digests of bench.py's workloads at full size (tests/golden/gen_fusion_digests.py)
+GOLDEN = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fusion_digests.json")))
 
 
 class Fusion:
@@ -68,16 +73,24 @@ class Fusion:
         p1 = self.poses.shape[0] if p1 is None else p1
         c = torch.zeros(2 * self.nt, dtype=torch.int32, device=self.dev) if counters is None else counters
         st = torch.zeros(8, dtype=torch.int64, device=self.dev)
-        _lib.check(L.dmf_fuse_set_variant(variant))
-        try:
-            _lib.check(L.dmf_fuse_depth_device(self.vol._h, C.addressof(self.cam), self.d_depth[p0].data_ptr(),
-                                               self.d_poses[p0].data_ptr(), p1 - p0, C.addressof(self.prm),
-                                               c.data_ptr(), c.data_ptr() + 4 * self.nt, st.data_ptr()))
-            name = L.dmf_fuse_kernel().decode()
-        finally:
-            _lib.check(L.dmf_fuse_set_variant(0))
+        _lib.set_variant(self.vol, variant)
+        _lib.check(L.dmf_fuse_depth_device(self.vol._h, C.addressof(self.cam), self.d_depth[p0].data_ptr(),
+                                           self.d_poses[p0].data_ptr(), p1 - p0, C.addressof(self.prm),
+                                           c.data_ptr(), c.data_ptr() + 4 * self.nt, st.data_ptr()))
+        name = _lib.kernel_name(self.vol)
         torch.cuda.synchronize(self.dev)
         return c, st.cpu().numpy().astype(np.uint64), name
+
+    def digest(self, c):
+        """sha256[:16] of the finalized x-major int16 log-odds of tiled counters c (bench.py
+        logodds_digest, tests/golden/gen_fusion_digests.py)."""
+        import hashlib
+        torch, L, _lib = self.torch, self.L, self._lib
+        lo = torch.empty(self.grid ** 3, dtype=torch.int16, device=self.dev)
+        _lib.check(L.dmf_fuse_finalize_device(self.vol._h, c.data_ptr(), c.data_ptr() + 4 * self.nt,
+                                              C.addressof(self.prm), lo.data_ptr()))
+        torch.cuda.synchronize(self.dev)
+        return hashlib.sha256(lo.cpu().numpy().tobytes()).hexdigest()[:16]
 
     def linear(self, c):
         """Tiled device counters -> x-major host (hits, misses)."""
@@ -136,9 +149,12 @@ def test_config_full_poses(cfg):
     f = Fusion(grid, W, H, P)
     c0, s0, k0 = f.run(0)
     _invariants(f, c0, s0)
+    gkey = {"config2": "config2_N1", "config3": "config3_N1"}.get(cfg)
+    if gkey:  # bench.py's workload at N = 1: the committed oracle digest of all its frames
+        assert f.digest(c0) == GOLDEN[gkey]["logodds_digest"] and int(s0[0]) == GOLDEN[gkey]["updates"]
     # the other exact kernels: k_fuse_l (or the slab-walk brick pipeline when the default is
     # k_fuse_l) and the per-cell-walk brick pipeline (variant 40)
-    for other in (31 if k0.startswith("dmf::k_bk_fuse") else 53, 40):
+    for other in (31 if k0.startswith("dmf::k_bk_fuse") else 57, 40):
         c1, s1, k1 = f.run(other)
         assert k0 != k1
         assert np.array_equal(s0[:4], s1[:4])
@@ -149,15 +165,16 @@ def test_config_full_poses(cfg):
     assert k0.startswith("dmf::k_bk_fuse_s")
 
 
-def test_config3_batches_equal_single_batch(monkeypatch):
+def test_config3_batches_equal_single_batch():
     """Config 3's frames through the brick pipeline in batches of 7 poses (48 frames: 7
     batches) == the default (one batch: the device's cut by the real pair count)."""
     f = Fusion(512, 1280, 720, 48, seed=99)
     c0, s0, _ = f.run(57)
     assert f._lib.fuse_batches_used(f.vol) == 1
-    monkeypatch.setenv("DMF_BK_BATCH_POSES", "7")
+    f._lib.set_knob(f.vol, "batch_poses", 7)
     c1, s1, _ = f.run(57)
     assert f._lib.fuse_batches_used(f.vol) == 7
+    f._lib.set_knob(f.vol, "batch_poses", 0)
     assert np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
 
 
@@ -190,17 +207,14 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
     d_depth = torch.from_numpy(depth.view(np.int16)).to(dev)
     d_poses = torch.from_numpy(poses).to(dev)
     out = {}
-    try:
-        for variant in (57, 40, 31):
-            _lib.check(L.dmf_fuse_set_variant(variant))
-            c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
-            st = torch.zeros(8, dtype=torch.int64, device=dev)
-            _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(), 4,
-                                               C.addressof(prm), c.data_ptr(), c.data_ptr() + 4 * nt, st.data_ptr()))
-            torch.cuda.synchronize(dev)
-            out[variant] = (c, st.cpu().numpy(), L.dmf_fuse_kernel().decode())
-    finally:
-        _lib.check(L.dmf_fuse_set_variant(0))
+    for variant in (57, 40, 31):
+        _lib.set_variant(vol, variant)
+        c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
+        st = torch.zeros(8, dtype=torch.int64, device=dev)
+        _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(), 4,
+                                           C.addressof(prm), c.data_ptr(), c.data_ptr() + 4 * nt, st.data_ptr()))
+        torch.cuda.synchronize(dev)
+        out[variant] = (c, st.cpu().numpy(), _lib.kernel_name(vol))
     (c0, s0, k0), (c1, s1, k1), (c2, s2, k2) = out[57], out[31], out[40]
     assert k0.startswith("dmf::k_bk_fuse_s") and k1.startswith("dmf::k_fuse_l") and k2.startswith("dmf::k_bk_fuse<")
     assert s0[0] > 10 ** 8 and np.array_equal(s0[:4], s1[:4]) and torch.equal(c0, c1)
@@ -212,13 +226,10 @@ def test_anisotropic_grid_over_8192_bricks(oracle):
     ov.constructVolume()
     ho, mo, _ = oracle.fuse_depth(ov, K, depth[2:3], poses[2:3], dmin=scene.DEPTH_MIN_MM, dmax=scene.DEPTH_MAX_MM,
                                   threads=16)
-    _lib.check(L.dmf_fuse_set_variant(57))
-    try:
-        c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
-        _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth[2].data_ptr(), d_poses[2].data_ptr(), 1,
-                                           C.addressof(prm), c.data_ptr(), c.data_ptr() + 4 * nt, None))
-    finally:
-        _lib.check(L.dmf_fuse_set_variant(0))
+    _lib.set_variant(vol, 57)
+    c = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
+    _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth[2].data_ptr(), d_poses[2].data_ptr(), 1,
+                                       C.addressof(prm), c.data_ptr(), c.data_ptr() + 4 * nt, None))
     lin = torch.empty(int(np.prod(dims)), dtype=torch.int32, device=dev)
     for half, exp in ((0, ho), (1, mo)):
         _lib.check(L.dmf_fuse_counters_to_linear_device(vol._h, c.data_ptr() + 4 * nt * half, lin.data_ptr()))
@@ -244,6 +255,7 @@ def test_config4_shard_all_frames_oracle(oracle):
     assert k0.startswith("dmf::k_bk_fuse_s")
     _invariants(f, c0, s0)
     assert _plan(f, 128) == (1, 1)
+    assert f.digest(c0) == GOLDEN["config4_shard_N1"]["logodds_digest"]
     hg, mg = f.linear(c0)
     ho, mo, so = _oracle_subset(oracle, f, list(range(128)))
     assert np.array_equal(so, s0[:3].astype(np.int64))
@@ -267,6 +279,9 @@ def test_config4_anchor_1024_poses():
     _invariants(f, c0, s0)
     # the geometric bound would need several batches; the device's cut by the real pairs, one
     assert _plan(f, 1024)[1] > 1 and f._lib.fuse_batches_used(f.vol) == 1
+    # the 1024 global poses of bench.py at N = 8: the committed oracle digest
+    assert f.digest(c0) == GOLDEN["config4_N8_anchor"]["logodds_digest"]
+    assert int(s0[0]) == GOLDEN["config4_N8_anchor"]["updates"]
     c1, s1, k1 = f.run(31)
     assert k1.startswith("dmf::k_fuse_l") and np.array_equal(s0[:4], s1[:4]) and f.torch.equal(c0, c1)
     del c1

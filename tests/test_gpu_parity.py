@@ -580,20 +580,16 @@ def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
             L.dmf_device_free(h, p_)
 
 
-@pytest.fixture(params=[40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63, 64, 65, 66, 67])
-def brick_variant(dmf, request):
-    """Select a brick-owned fusion variant for one test: DMF_FUSE_VARIANT 40-43 = the
-    per-cell walk (k_bk_fuse: refill threshold, pair order, interleaving), 44-51 = the
-    slab walk (k_bk_fuse_s, the default: refill threshold, unroll, two pairs per lane,
-    branch-free body), 52-56 = refill threshold 20 / 24 / 28 with pair order spread
-    16 / 32 / 64 on 24-B pair records (53 = <24, 32>, the round-2 default), 57 = <24, 32> on
-    20-B records (the default: the walk on beta = b >> 9, dmf_brick.hpp pack20)."""
-    from dmf_amd import _lib
-    L = _lib.load()
-    _lib.check(L.dmf_fuse_set_variant(request.param))
-    assert L.dmf_fuse_kernel().decode().startswith("dmf::k_bk_fuse_s<" if request.param >= 44 else "dmf::k_bk_fuse<")
-    yield
-    _lib.check(L.dmf_fuse_set_variant(0))
+@pytest.fixture(params=[57, 40])
+def brick_variant(request):
+    """A brick-pipeline fusion implementation (include/dmf_diag.h): 57 = DMF_FUSE_SLAB, the
+    production kernel (slab walk on 20-B records, k_bk_fuse_s) at any grid; 40 =
+    DMF_FUSE_CELL_WALK (per-cell walk on 24-B records, k_bk_fuse), an independent exact walk."""
+    return request.param
+
+
+def _brick_kernel(variant):
+    return "dmf::k_bk_fuse_s<" if variant == 57 else "dmf::k_bk_fuse<"
 
 
 @pytest.mark.parametrize("dims,nframes", [((128, 128, 128), 6),   # 4^3 bricks
@@ -601,9 +597,10 @@ def brick_variant(dmf, request):
                                           ((61, 50, 47), 3),      # odd dims, padded tiles
                                           ((32, 32, 32), 6)])     # one brick, ~30 parts: atomic flush
 def test_fuse_brick_path(oracle, engine, dmf, brick_variant, dims, nframes):
-    """Brick-owned fusion (k_bk_rays / k_bk_pairs / k_bk_fuse, dmf_brick.hpp): the
+    """Brick-owned fusion (k_bk_rays / k_bk_pairs / k_bk_fuse(_s), dmf_brick.hpp): the
     per-brick restart of the exact walk must give the oracle's counters bit for bit,
     for single-part bricks (plain adds) and multi-part bricks (device atomics)."""
+    from dmf_amd import _lib
     poses, depth, _ = Hh.frames()
     poses = np.concatenate([poses, Hh.ref_style_poses()[:2]])[:nframes + 2]
     depth = np.concatenate([depth, depth[:2]])[:nframes + 2]
@@ -616,38 +613,57 @@ def test_fuse_brick_path(oracle, engine, dmf, brick_variant, dims, nframes):
     gv.setDimensions(*Hh.BOUNDS)
     gv.setVolumeSize(*dims)
     gv.constructVolume()
+    _lib.set_variant(gv, brick_variant)
     prm = dmf.FuseParams(dmin_mm=200, dmax_mm=1000)
     for _ in range(2):  # repeatable (LDS counters, work queue)
         hg, mg, sg = engine.fuse_depth(gv, depth, poses, prm)
+        assert _lib.kernel_name(gv).startswith(_brick_kernel(brick_variant))
         assert np.array_equal(so, sg)
         assert np.array_equal(ho, hg) and np.array_equal(mo, mg)
 
 
 def test_fuse_lds_box_kernel(oracle, engine, dmf):
-    """k_fuse_l<12, 1280> (variant 31; the path for grids over 1024 cells per axis) stays
-    bit-exact now that the brick pipeline is the default."""
+    """k_fuse_l<12, 1280> (DMF_FUSE_LDS_BOX; the path for grids under 256 or over 1024 cells
+    per axis) stays bit-exact now that the brick pipeline is the default."""
     from dmf_amd import _lib
-    L = _lib.load()
     _, depth, _ = Hh.frames()
     poses = np.concatenate([Hh.ref_style_poses()[:2], Hh.frames()[0][:2]])
     frames = np.concatenate([depth[:2], depth[2:4]])
     ov = Hh.oracle_volume(oracle, n=96, clouds=[])
     ho, mo, so = oracle.fuse_depth(ov, K, frames, poses)
     gv = Hh.gpu_volume(n=96, clouds=[])
-    _lib.check(L.dmf_fuse_set_variant(31))
-    try:
-        assert L.dmf_fuse_kernel().decode() == "dmf::k_fuse_l<12, 1280>"
-        hg, mg, sg = engine.fuse_depth(gv, frames, poses)
-    finally:
-        _lib.check(L.dmf_fuse_set_variant(0))
+    _lib.set_variant(gv, 31)
+    assert _lib.kernel_name(gv) == "dmf::k_fuse_l<12, 1280>"
+    hg, mg, sg = engine.fuse_depth(gv, frames, poses)
+    assert _lib.kernel_name(gv) == "dmf::k_fuse_l<12, 1280>"
     assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
+
+
+def test_fuse_variant_controls(dmf):
+    """dmf_diag.h: the fusion implementation and the knobs are per volume (a second volume
+    keeps the defaults); unknown variants and knobs are rejected."""
+    import ctypes as C
+    from dmf_amd import _lib
+    L = _lib.load()
+    a, b = Hh.gpu_volume(n=64, clouds=[]), Hh.gpu_volume(n=64, clouds=[])
+    _lib.set_variant(a, 40)
+    _lib.set_knob(a, "pair_cap", 12345)
+    va, vb, kb = C.c_int32(), C.c_int32(), C.c_int64()
+    _lib.check(L.dmf_fuse_get_variant(a._h, C.addressof(va)))
+    _lib.check(L.dmf_fuse_get_variant(b._h, C.addressof(vb)))
+    _lib.check(L.dmf_volume_get_knob(b._h, _lib.KNOBS["pair_cap"], C.addressof(kb)))
+    assert (va.value, vb.value, kb.value) == (40, 0, 0)
+    assert _lib.kernel_name(a) == "dmf::k_bk_fuse<16, 8, 8>" and _lib.kernel_name(b).startswith("dmf::k_bk_fuse_s<")
+    assert L.dmf_fuse_set_variant(a._h, 53) == _lib.DMF_ERR_INVALID
+    assert L.dmf_volume_set_knob(a._h, 99, 1) == _lib.DMF_ERR_INVALID
 
 
 def test_fuse_brick_vs_lds_box_full_size(dmf):
     """Size-independent check at the bench's grid (512^3, 8 frames of 640x480): the brick
-    pipeline (default) and k_fuse_l<12, 1280> (variant 31) are independent exact
-    implementations of the same DDA spec and must agree counter for counter; every update
-    is either a hit or a miss, and there is one hit per ray ending inside the grid."""
+    pipeline (default), k_fuse_l<12, 1280> (31) and the per-cell brick walk (40) are
+    independent exact implementations of the same DDA spec and must agree counter for
+    counter; every update is either a hit or a miss, and there is one hit per ray ending
+    inside the grid."""
     import ctypes as C
     from dmf_amd import _lib, scene
     L = _lib.load()
@@ -675,7 +691,7 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
     out = {}
     try:
         for variant in (0, 31, 40):
-            _lib.check(L.dmf_fuse_set_variant(variant))
+            _lib.set_variant(vol, variant)
             _lib.check(L.dmf_memset_device(h, dc, 0, 8 * nt))
             _lib.check(L.dmf_memset_device(h, ds, 0, 64))
             _lib.check(L.dmf_fuse_depth_device(h, C.addressof(cam), dd, dp, P, C.addressof(prm), dc, dc + 4 * nt, ds))
@@ -685,7 +701,6 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
             _lib.check(L.dmf_memcpy_d2h(h, st.ctypes.data, ds, st.nbytes))
             out[variant] = (cnt, st)
     finally:
-        _lib.check(L.dmf_fuse_set_variant(0))
         for ptr_ in (dd, dp, dc, ds):
             L.dmf_device_free(h, ptr_)
     (c0, s0), (c1, s1), (c2, s2) = out[0], out[31], out[40]
@@ -696,13 +711,13 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
 
 
 @pytest.mark.parametrize("mode", ["poses2", "paircap"])
-def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, mode):
-    """The brick pipeline (variants 0 = the default 20-B record slab walk, 53 = the 24-B
-    record, 40 = per-cell walk) cut into several pose batches accumulates the same counters
-    as the oracle.  poses2: at most 2 poses per batch (DMF_BK_BATCH_POSES) over 5 frames;
-    paircap: a pair capacity of 1.6 x the largest frame's pairs (DMF_BK_PAIR_CAP), so the
-    DEVICE cuts the batches by the pairs each frame really makes (k_bk_batches) and the host's
-    geometric-bound launches past the device's batch count exit at once."""
+def test_fuse_brick_multi_batch(oracle, engine, dmf, mode):
+    """The brick pipeline (57 = the production slab walk on 20-B records, 40 = per-cell walk)
+    cut into several pose batches accumulates the same counters as the oracle.  poses2: at
+    most 2 poses per batch (DMF_KNOB_BATCH_POSES) over 5 frames; paircap: a pair capacity of
+    1.6 x the largest frame's pairs (DMF_KNOB_PAIR_CAP), so the DEVICE cuts the batches by the
+    pairs each frame really makes (k_bk_batches) and the host's geometric-bound launches past
+    the device's batch count exit at once."""
     poses, depth, _ = Hh.frames()
     poses, depth = poses[:5], depth[:5]
     ov = Hh.oracle_volume(oracle, n=80, clouds=[])
@@ -711,8 +726,9 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, mode):
     from dmf_amd import _lib
     L = _lib.load()
     prm = dmf.FuseParams(dmin_mm=200, dmax_mm=1000)
+    _lib.set_variant(gv, 57)  # the brick pipeline at this small grid
     if mode == "poses2":
-        monkeypatch.setenv("DMF_BK_BATCH_POSES", "2")
+        _lib.set_knob(gv, "batch_poses", 2)
         expect = 3
     else:  # pairs per frame from single-frame device calls (stats[4] = pairs)
         import ctypes as C
@@ -725,35 +741,27 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, monkeypatch, mode):
         d_poses = torch.from_numpy(np.ascontiguousarray(poses, np.float32)).to(dev)
         cam = _lib.make_camera(K, 480, 640)
         cnt = torch.zeros(2 * nct.value, dtype=torch.int32, device=dev)
-        _lib.check(L.dmf_fuse_set_variant(57))
         per = []
-        try:
-            for i in range(5):
-                st = torch.zeros(8, dtype=torch.int64, device=dev)
-                _lib.check(L.dmf_fuse_depth_device(gv._h, C.addressof(cam), d_depth[i].data_ptr(), d_poses[i].data_ptr(),
-                                                   1, C.addressof(prm), cnt.data_ptr(), cnt.data_ptr() + 4 * nct.value,
-                                                   st.data_ptr()))
-                torch.cuda.synchronize(dev)
-                per.append(int(st[4].item()))
-        finally:
-            _lib.check(L.dmf_fuse_set_variant(0))
+        for i in range(5):
+            st = torch.zeros(8, dtype=torch.int64, device=dev)
+            _lib.check(L.dmf_fuse_depth_device(gv._h, C.addressof(cam), d_depth[i].data_ptr(), d_poses[i].data_ptr(),
+                                               1, C.addressof(prm), cnt.data_ptr(), cnt.data_ptr() + 4 * nct.value,
+                                               st.data_ptr()))
+            torch.cuda.synchronize(dev)
+            per.append(int(st[4].item()))
         cap = int(1.6 * max(per))
-        monkeypatch.setenv("DMF_BK_PAIR_CAP", str(cap))
+        _lib.set_knob(gv, "pair_cap", cap)
         expect, acc = 0, None  # the greedy cut, restated
         for c in per:
             if acc is None or acc + c > cap:
                 expect, acc = expect + 1, 0
             acc += c
         assert expect >= 3
-    for variant, name in ((0, "dmf::k_bk_fuse_s<24, 32, 4, 1, false, true>"),
-                          (53, "dmf::k_bk_fuse_s<24, 32, 4, 1, false>"), (40, "dmf::k_bk_fuse<16, 8, 8, 1, 0, true>")):
-        _lib.check(L.dmf_fuse_set_variant(variant if variant else 57))  # the brick pipeline at this small grid
-        try:
-            hg, mg, sg = engine.fuse_depth(gv, depth, poses, prm)
-            assert L.dmf_fuse_kernel().decode() == name
-            assert _lib.fuse_batches_used(gv) == expect
-        finally:
-            _lib.check(L.dmf_fuse_set_variant(0))
+    for variant, name in ((57, "dmf::k_bk_fuse_s<24, 32, 4>"), (40, "dmf::k_bk_fuse<16, 8, 8>")):
+        _lib.set_variant(gv, variant)
+        hg, mg, sg = engine.fuse_depth(gv, depth, poses, prm)
+        assert _lib.kernel_name(gv) == name
+        assert _lib.fuse_batches_used(gv) == expect
         assert np.array_equal(so, sg) and np.array_equal(ho, hg) and np.array_equal(mo, mg)
 
 
@@ -790,27 +798,27 @@ def _edge_fusion_cases():
     return cases
 
 
-@pytest.mark.parametrize("variant", [53, 44, 40, 31])
-def test_fuse_edge_cases(oracle, dmf, variant):
-    """Every edge case of _edge_fusion_cases through the slab-walk brick pipeline (53 = the
-    default kernel, 44 = its previous parameters), the
-    per-cell brick walk (40) and k_fuse_l (31): counters and statistics equal the oracle's
-    (zero where nothing is valid or nothing reaches the grid)."""
+@pytest.mark.parametrize("n,variant", [(256, 0), (96, 57), (96, 40), (96, 31)])
+def test_fuse_edge_cases(oracle, dmf, n, variant):
+    """Every edge case of _edge_fusion_cases through (256, 0) the DEFAULT dispatch at a grid
+    that takes the production kernel (the slab-walk brick pipeline on 20-B records,
+    k_bk_fuse_s: axis-aligned rays exercise the zero |dq| minor axes of pack20's beta state),
+    (96, 57) the same kernel at a small grid (several rays per brick boundary), (96, 40) the
+    per-cell brick walk and (96, 31) k_fuse_l: counters and statistics equal the oracle's (zero
+    where nothing is valid or nothing reaches the grid)."""
     from dmf_amd import _lib
-    L = _lib.load()
-    _lib.check(L.dmf_fuse_set_variant(variant))
-    try:
-        for name, Kc, Hc, Wc, P, D in _edge_fusion_cases():
-            ov = Hh.oracle_volume(oracle, n=96, clouds=[])
-            gv = Hh.gpu_volume(n=96, clouds=[])
-            ho, mo, so = oracle.fuse_depth(ov, Kc, D, P, dmin=200, dmax=1000)
-            eng = dmf.RayTracingEngine(dmf.Camera(Kc, Hc, Wc))
-            hg, mg, sg = eng.fuse_depth(gv, D, P, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
-            assert np.array_equal(so, sg), (name, so, sg)
-            assert np.array_equal(ho, hg) and np.array_equal(mo, mg), name
-            if name in ("no_valid_pixel", "misses_grid", "ends_before_grid"):
-                assert so[0] == 0 and not hg.any() and not mg.any(), name
-            else:
-                assert so[0] > 0, name
-    finally:
-        _lib.check(L.dmf_fuse_set_variant(0))
+    for name, Kc, Hc, Wc, P, D in _edge_fusion_cases():
+        ov = Hh.oracle_volume(oracle, n=n, clouds=[])
+        gv = Hh.gpu_volume(n=n, clouds=[])
+        _lib.set_variant(gv, variant)
+        ho, mo, so = oracle.fuse_depth(ov, Kc, D, P, dmin=200, dmax=1000)
+        eng = dmf.RayTracingEngine(dmf.Camera(Kc, Hc, Wc))
+        hg, mg, sg = eng.fuse_depth(gv, D, P, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
+        if variant in (0, 57) and so[0] > 0:
+            assert _lib.kernel_name(gv) == "dmf::k_bk_fuse_s<24, 32, 4>", name
+        assert np.array_equal(so, sg), (name, so, sg)
+        assert np.array_equal(ho, hg) and np.array_equal(mo, mg), name
+        if name in ("no_valid_pixel", "misses_grid", "ends_before_grid"):
+            assert so[0] == 0 and not hg.any() and not mg.any(), name
+        else:
+            assert so[0] > 0, name

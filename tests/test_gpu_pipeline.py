@@ -1,18 +1,23 @@
 """GPU: pipelined fusion (dmf_fuse_set_input_stream).
 
-With an input stream declared, each call's pose table and pass A run on the volume's
-staging stream into one of two slots and overlap the previous call's passes B and F.  The
-counters and statistics must equal the serial order's exactly, also when
+With an input stream declared, each call's pose table, pass A, batch layout and pass B run
+on the volume's staging stream into one of two slots and overlap the previous call's
+phase F.  The counters and statistics must equal the serial order's exactly, also when
 * the inputs are rewritten on the input stream before every call (the call must have made
   the input stream wait for its pass A),
-* a call spans several super-batches (DMF_BK_SUPER_POSES: the slots alternate inside the
+* a call spans several super-batches (DMF_KNOB_SUPER_POSES: the slots alternate inside the
   call, slot reuse waits for the super-batch two back),
-* the device cuts a super-batch into several pose batches (DMF_BK_BATCH_POSES),
-* pass B is staged too (DMF_BK_STAGE=2: per-slot pair records, batch j+1's pass B after
-  batch j's phase F),
-and at 128^3 the sum over the calls equals the oracle's counters.
+* the device cuts a super-batch into several pose batches (DMF_KNOB_BATCH_POSES: batch j+1's
+  pass B after batch j's phase F),
+* serial and pipelined calls are mixed on one volume with no synchronisation between them
+  (a pipelined call must wait for the serial calls that used its slot),
+and at 128^3 the sum over the calls equals the oracle's counters.  At the bench's own shape
+(512^3, 128 frames of 640x480 per call: the timed mode of bench.py) several pipelined calls
+equal the serial calls and the committed oracle digest (tests/golden/fusion_digests.json).
 """
 import ctypes as C
+import json
+import os
 
 import numpy as np
 import pytest
@@ -21,80 +26,118 @@ import helpers as Hh
 
 pytestmark = pytest.mark.gpu
 
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fusion_digests.json")
 
-def _frames(P):
+
+def _frames(P, seed=77):
     from dmf_amd import scene
-    poses = np.ascontiguousarray(scene.fibonacci_poses(P, seed=77), np.float32)
+    poses = np.ascontiguousarray(scene.fibonacci_poses(P, seed=seed), np.float32)
     depth = np.ascontiguousarray(scene.render_frames(scene.intrinsics(640, 480), 640, 480, poses), np.uint16)
     return poses, depth
 
 
-def _run(n, poses, depth, per_call, pipelined, variant=0):
-    import torch
-    import dmf_amd
-    from dmf_amd import _lib, scene
-    L = _lib.load()
-    dev = torch.device("cuda", 0)
-    vol = dmf_amd.VoxelVolume()
-    vol.setDimensions(*Hh.BOUNDS)
-    vol.setVolumeSize(n, n, n)
-    vol.constructVolume()
-    main = torch.cuda.Stream(dev)
-    inp = torch.cuda.Stream(dev)
-    vol.set_stream(main.cuda_stream)
-    cam = _lib.make_camera(scene.intrinsics(640, 480), 480, 640)
-    prm = _lib.default_fuse_params(dmin_mm=scene.DEPTH_MIN_MM, dmax_mm=scene.DEPTH_MAX_MM)
-    nct = C.c_int64()
-    _lib.check(L.dmf_fuse_counter_cells(vol._h, C.addressof(nct)))
-    nt = nct.value
-    all_depth = torch.from_numpy(depth.view(np.int16)).to(dev)
-    all_poses = torch.from_numpy(poses).to(dev)
-    # one input buffer of per_call frames, rewritten on the input stream before every call
-    d_depth = torch.empty_like(all_depth[:per_call])
-    d_poses = torch.empty_like(all_poses[:per_call])
-    counters = torch.zeros(2 * nt, dtype=torch.int32, device=dev)
-    stats = torch.zeros(8, dtype=torch.int64, device=dev)
-    torch.cuda.synchronize(dev)
-    _lib.check(L.dmf_fuse_set_variant(variant))
-    try:
-        if pipelined:
-            _lib.check(L.dmf_fuse_set_input_stream(vol._h, inp.cuda_stream))
-        _lib.check(L.dmf_fuse_reserve(vol._h, C.addressof(cam), per_call, 0))
-        for c0 in range(0, poses.shape[0], per_call):
-            with torch.cuda.stream(inp if pipelined else main):
-                d_depth.copy_(all_depth[c0:c0 + per_call])
-                d_poses.copy_(all_poses[c0:c0 + per_call])
-            _lib.check(L.dmf_fuse_depth_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(),
-                                               per_call, C.addressof(prm), counters.data_ptr(),
-                                               counters.data_ptr() + 4 * nt, stats.data_ptr()))
-        torch.cuda.synchronize(dev)
-        lin = torch.empty(n ** 3, dtype=torch.int32, device=dev)
+class _Vol:
+    """A device-API fusion volume with its own main / input streams."""
+
+    def __init__(self, n, per_call, knobs=None, variant=0):
+        import torch
+        import dmf_amd
+        from dmf_amd import _lib, scene
+        self.torch, self._lib, self.L = torch, _lib, _lib.load()
+        self.dev = torch.device("cuda", 0)
+        self.vol = dmf_amd.VoxelVolume()
+        self.vol.setDimensions(*Hh.BOUNDS)
+        self.vol.setVolumeSize(n, n, n)
+        self.vol.constructVolume()
+        self.n = n
+        self.main = torch.cuda.Stream(self.dev)
+        self.inp = torch.cuda.Stream(self.dev)
+        self.vol.set_stream(self.main.cuda_stream)
+        self.cam = _lib.make_camera(scene.intrinsics(640, 480), 480, 640)
+        self.prm = _lib.default_fuse_params(dmin_mm=scene.DEPTH_MIN_MM, dmax_mm=scene.DEPTH_MAX_MM)
+        nct = C.c_int64()
+        _lib.check(self.L.dmf_fuse_counter_cells(self.vol._h, C.addressof(nct)))
+        self.nt = nct.value
+        self.per_call = per_call
+        _lib.set_variant(self.vol, variant)
+        for k, v in (knobs or {}).items():
+            _lib.set_knob(self.vol, k, v)
+        self.counters = torch.zeros(2 * self.nt, dtype=torch.int32, device=self.dev)
+        self.stats = torch.zeros(8, dtype=torch.int64, device=self.dev)
+
+    def pipelined(self, on):
+        self._lib.check(self.L.dmf_fuse_set_input_stream(self.vol._h, self.inp.cuda_stream if on else None))
+
+    def reserve(self):
+        self._lib.check(self.L.dmf_fuse_reserve(self.vol._h, C.addressof(self.cam), self.per_call, 0))
+
+    def call(self, d_depth, d_poses):
+        self._lib.check(self.L.dmf_fuse_depth_device(
+            self.vol._h, C.addressof(self.cam), d_depth.data_ptr(), d_poses.data_ptr(), self.per_call,
+            C.addressof(self.prm), self.counters.data_ptr(), self.counters.data_ptr() + 4 * self.nt,
+            self.stats.data_ptr()))
+
+    def linear(self):
+        torch = self.torch
+        torch.cuda.synchronize(self.dev)
+        lin = torch.empty(self.n ** 3, dtype=torch.int32, device=self.dev)
         out = []
         for half in range(2):
-            _lib.check(L.dmf_fuse_counters_to_linear_device(vol._h, counters.data_ptr() + 4 * nt * half,
-                                                            lin.data_ptr()))
-            vol.synchronize()
+            self._lib.check(self.L.dmf_fuse_counters_to_linear_device(
+                self.vol._h, self.counters.data_ptr() + 4 * self.nt * half, lin.data_ptr()))
+            self.vol.synchronize()
             out.append(lin.cpu().numpy())
-        return out[0], out[1], stats.cpu().numpy()
+        return out[0], out[1], self.stats.cpu().numpy()
+
+    def logodds_digest(self):
+        """sha256[:16] of the finalized int16 grid (bench.py logodds_digest)."""
+        import hashlib
+        torch = self.torch
+        torch.cuda.synchronize(self.dev)
+        lo = torch.empty(self.n ** 3, dtype=torch.int16, device=self.dev)
+        self._lib.check(self.L.dmf_fuse_finalize_device(self.vol._h, self.counters.data_ptr(),
+                                                        self.counters.data_ptr() + 4 * self.nt,
+                                                        C.addressof(self.prm), lo.data_ptr()))
+        self.vol.synchronize()
+        return hashlib.sha256(lo.cpu().numpy().tobytes()).hexdigest()[:16]
+
+    def close(self):
+        self.pipelined(False)
+        self.vol.close()
+
+
+def _run(n, poses, depth, per_call, pipelined, variant=0, knobs=None):
+    """Calls of per_call frames through ONE input buffer rewritten before every call (on the
+    input stream when pipelined)."""
+    v = _Vol(n, per_call, knobs, variant)
+    torch = v.torch
+    all_depth = torch.from_numpy(depth.view(np.int16)).to(v.dev)
+    all_poses = torch.from_numpy(poses).to(v.dev)
+    d_depth = torch.empty_like(all_depth[:per_call])
+    d_poses = torch.empty_like(all_poses[:per_call])
+    torch.cuda.synchronize(v.dev)
+    try:
+        if pipelined:
+            v.pipelined(True)
+        v.reserve()
+        for c0 in range(0, poses.shape[0], per_call):
+            with torch.cuda.stream(v.inp if pipelined else v.main):
+                d_depth.copy_(all_depth[c0:c0 + per_call])
+                d_poses.copy_(all_poses[c0:c0 + per_call])
+            v.call(d_depth, d_poses)
+        return v.linear()
     finally:
-        _lib.check(L.dmf_fuse_set_input_stream(vol._h, None))
-        _lib.check(L.dmf_fuse_set_variant(0))
+        v.close()
 
 
-@pytest.mark.parametrize("stage", ["1", "2"])
 @pytest.mark.parametrize("case", ["calls", "super2", "super1_batches"])
-def test_pipelined_equals_serial_256(monkeypatch, case, stage):
-    """256^3 (the default brick pipeline), 4 calls of 3 frames; stage 1 = pass A staged,
-    2 = pass A, the batch layout and pass B staged (DMF_BK_STAGE)."""
-    monkeypatch.setenv("DMF_BK_STAGE", stage)
+def test_pipelined_equals_serial_256(case):
+    """256^3 (the default brick pipeline), 4 calls of 3 frames."""
     poses, depth = _frames(12)
-    if case == "super2":
-        monkeypatch.setenv("DMF_BK_SUPER_POSES", "2")  # 3 frames -> super-batches of 2 + 1
-    elif case == "super1_batches":
-        monkeypatch.setenv("DMF_BK_SUPER_POSES", "3")
-        monkeypatch.setenv("DMF_BK_BATCH_POSES", "1")  # three device batches per super-batch
-    hs, ms, ss = _run(256, poses, depth, 3, pipelined=False)
-    hp, mp, sp = _run(256, poses, depth, 3, pipelined=True)
+    knobs = {"calls": {}, "super2": {"super_poses": 2},  # 3 frames -> super-batches of 2 + 1
+             "super1_batches": {"super_poses": 3, "batch_poses": 1}}[case]  # three device batches each
+    hs, ms, ss = _run(256, poses, depth, 3, pipelined=False, knobs=knobs)
+    hp, mp, sp = _run(256, poses, depth, 3, pipelined=True, knobs=knobs)
     assert ss[0] > 10 ** 7 and ss[3] == 0
     # stats[5] (parts) differs by design: serial calls cut the part queue's tail (k_bk_scan),
     # pipelined ones do not; stats[6] (flushed cells) depends on which pairs share a part, i.e.
@@ -103,10 +146,9 @@ def test_pipelined_equals_serial_256(monkeypatch, case, stage):
     assert np.array_equal(hs, hp) and np.array_equal(ms, mp)
 
 
-@pytest.mark.parametrize("stage", ["1", "2"])
-def test_pipelined_oracle_128(oracle, monkeypatch, stage):
-    """128^3 through the brick pipeline (variant 57), 3 calls of 2 frames, vs the oracle."""
-    monkeypatch.setenv("DMF_BK_STAGE", stage)
+def test_pipelined_oracle_128(oracle):
+    """128^3 through the brick pipeline (DMF_FUSE_SLAB), 3 pipelined calls of 2 frames, vs
+    the oracle."""
     poses, depth = _frames(6)
     hp, mp, sp = _run(128, poses, depth, 2, pipelined=True, variant=57)
     ov = oracle.Volume()
@@ -118,3 +160,96 @@ def test_pipelined_oracle_128(oracle, monkeypatch, stage):
                                    dmin=scene.DEPTH_MIN_MM, dmax=scene.DEPTH_MAX_MM)
     assert np.array_equal(np.asarray(so)[:3], sp[:3])
     assert np.array_equal(ho, hp) and np.array_equal(mo, mp)
+
+
+def test_serial_then_pipelined_without_sync():
+    """a serial call on the volume's stream, then dmf_fuse_set_input_stream
+    and pipelined calls with NO synchronisation by the caller.  The first pipelined call's pass
+    A reuses slot 0's buffers, which the serial call's pass B and phase F may still be reading
+    (the serial call is held back by a ~0.5 s spin kernel queued ahead of it, so an unordered
+    pass A would overwrite its records).  The mode switch orders it: it frees and re-plans the
+    fusion scratch after the volume's streams drain, and staged calls wait for the serial
+    slot's last reader (st_free[0]).  Counters equal an all-serial volume's."""
+    poses, depth = _frames(9, seed=5)
+    hs, ms, ss = _run(256, poses, depth, 3, pipelined=False)
+    v = _Vol(256, 3)
+    torch = v.torch
+    d_depth = torch.from_numpy(depth.view(np.int16)).to(v.dev)
+    d_poses = torch.from_numpy(poses).to(v.dev)
+    torch.cuda.synchronize(v.dev)
+    try:
+        v.reserve()
+        with torch.cuda.stream(v.main):
+            torch.cuda._sleep(1_000_000_000)
+        v.call(d_depth[0:3], d_poses[0:3])        # serial, slot 0, behind the spin
+        v.pipelined(True)                         # the mode switch
+        v.call(d_depth[3:6], d_poses[3:6])        # staged: slot 0 again
+        v.call(d_depth[6:9], d_poses[6:9])        # staged: slot 1
+        v.pipelined(False)
+        hp, mp, sp = v.linear()
+    finally:
+        v.close()
+    assert np.array_equal(ss[:5], sp[:5])
+    assert np.array_equal(hs, hp) and np.array_equal(ms, mp)
+
+
+def test_pipelined_then_serial_mixed():
+    """Pipelined calls, then serial calls on the same volume (input stream cleared) with no
+    synchronisation, then pipelined again: equal to all-serial."""
+    poses, depth = _frames(12, seed=6)
+    hs, ms, ss = _run(256, poses, depth, 3, pipelined=False)
+    v = _Vol(256, 3)
+    torch = v.torch
+    d_depth = torch.from_numpy(depth.view(np.int16)).to(v.dev)
+    d_poses = torch.from_numpy(poses).to(v.dev)
+    torch.cuda.synchronize(v.dev)
+    try:
+        v.pipelined(True)
+        v.reserve()
+        v.call(d_depth[0:3], d_poses[0:3])
+        v.pipelined(False)
+        v.call(d_depth[3:6], d_poses[3:6])
+        v.pipelined(True)
+        v.call(d_depth[6:9], d_poses[6:9])
+        v.call(d_depth[9:12], d_poses[9:12])
+        hp, mp, sp = v.linear()
+    finally:
+        v.close()
+    assert np.array_equal(ss[:5], sp[:5])
+    assert np.array_equal(hs, hp) and np.array_equal(ms, mp)
+
+
+def test_timed_mode_config4_shape():
+    """The bench's timed mode at its own shape: 512^3, calls of the 128 frames of config 4's
+    per-GPU shard (bench.py at N = 1), pipelined through an idle input stream exactly as
+    bench.py does (three calls back to back, no synchronisation), equal counter for counter to
+    three serial calls, and the finalized grid of ONE pipelined call equals the committed
+    oracle digest of the same 128 frames (tests/golden/fusion_digests.json, generated by the
+    oracle in tests/golden/gen_fusion_digests.py)."""
+    from dmf_amd import scene
+    golden = json.load(open(GOLDEN))["config4_shard_N1"]
+    poses = np.ascontiguousarray(scene.fibonacci_poses(128, seed=1234), np.float32)
+    depth = np.ascontiguousarray(scene.render_frames(scene.intrinsics(640, 480), 640, 480, poses), np.uint16)
+    results = {}
+    for mode in ("serial", "pipelined"):
+        v = _Vol(512, 128)
+        torch = v.torch
+        d_depth = torch.from_numpy(depth.view(np.int16)).to(v.dev)
+        d_poses = torch.from_numpy(poses).to(v.dev)
+        torch.cuda.synchronize(v.dev)
+        try:
+            v.pipelined(mode == "pipelined")
+            v.reserve()
+            v.call(d_depth, d_poses)
+            if mode == "pipelined":
+                assert v.logodds_digest() == golden["logodds_digest"]
+                assert int(v.stats.cpu()[0]) == golden["updates"]
+            for _ in range(2):
+                v.call(d_depth, d_poses)
+            torch.cuda.synchronize(v.dev)
+            results[mode] = (v.counters.clone(), v.stats.cpu().numpy())
+        finally:
+            v.close()
+    (cs, ss), (cp, sp) = results["serial"], results["pipelined"]
+    assert np.array_equal(ss[:5], sp[:5]) and int(ss[0]) == 3 * golden["updates"]
+    assert results["serial"][0].equal(cp)

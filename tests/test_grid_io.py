@@ -65,3 +65,35 @@ def test_rejects_bad_files(tmp_path):
     assert load(raw, cap=g.size - 1) == _lib.DMF_ERR_CAPACITY
     with pytest.raises(ValueError):
         _lib.grid_save(path, g, (6, 5, 5), (0, 1, 0, 1, 0, 1))
+
+
+def test_huge_dims_rejected_before_allocation(tmp_path):
+    """a corrupted header naming 2^20 x 2^20 x 2^20 cells is rejected from the
+    file's size in the header-only read (DMF_ERR_INVALID), before grid_load sizes a buffer."""
+    import struct
+    g = _grid((4, 4, 4), 2)
+    path = tmp_path / "g.dmf"
+    _lib.grid_save(path, g, g.shape, (0, 1, 0, 1, 0, 1))
+    raw = bytearray(path.read_bytes())
+    struct.pack_into("<iii", raw, 16, 1 << 20, 1 << 20, 1 << 20)
+    bad = tmp_path / "huge.dmf"
+    bad.write_bytes(bytes(raw))
+    with pytest.raises(_lib.DmfError) as e:
+        _lib.grid_load(bad)
+    assert e.value.status == _lib.DMF_ERR_INVALID
+
+
+def test_save_replaces_atomically(tmp_path):
+    """dmf_grid_save writes path.tmp and renames it over path: a save that fails
+    (here: an unwritable temporary) leaves the previous file intact and no temporary behind."""
+    g = _grid((5, 4, 3), 3)
+    path = tmp_path / "g.dmf"
+    _lib.grid_save(path, g, g.shape, (0, 1, 0, 1, 0, 1))
+    before = path.read_bytes()
+    assert not (tmp_path / "g.dmf.tmp").exists()
+    (tmp_path / "g.dmf.tmp").mkdir()  # fopen of the temporary fails
+    with pytest.raises(_lib.DmfError):
+        _lib.grid_save(path, _grid((5, 4, 3), 4), (5, 4, 3), (0, 1, 0, 1, 0, 1))
+    assert path.read_bytes() == before
+    g2, _, _ = _lib.grid_load(path)
+    assert np.array_equal(g2, g)

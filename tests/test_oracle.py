@@ -310,3 +310,21 @@ def test_collision_cost_map_py_vs_cpp(oracle, gold):
     coll = got == 2 ** 31 - 1
     assert coll.any() and not coll.all()
     assert got[0, 8] == 0 and np.all(np.diag(got) == 0)
+
+
+def test_fusion_digest_fixture_reproduces():
+    """tests/golden/fusion_digests.json (the oracle digests bench.py and the GPU suite check
+    against) is reproducible: config 2's entry (256^3, 64 frames of 640x480) regenerated by
+    the same script equals the committed one, and every bench workload (config 4 at N = 1, 2,
+    4, 8) has an entry."""
+    import json
+    import os
+    import sys
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, here)
+    import gen_fusion_digests as G
+    table = json.load(open(os.path.join(here, "fusion_digests.json")))
+    for k in ("config4_shard_N1", "config4_N2", "config4_N4", "config4_N8_anchor", "config2_N1"):
+        assert k in table and len(table[k]["logodds_digest"]) == 16
+    got = G.oracle_digest(*G.WORKLOADS["config2_N1"], threads=os.cpu_count() or 1)
+    assert got == table["config2_N1"]

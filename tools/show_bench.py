@@ -4,8 +4,11 @@ import sys
 
 d = json.load(open(sys.argv[1]))
 r = d["roofline"]
-print("fusion %.3f ms/launch  %.4e updates/s  frac %.3f  step %.3f ms  %s" % (r["kernel_ms"], d["value"], r["frac"],
-                                                                           d["ms_per_step"], r["kernel"]))
+print("fusion step %.3f ms  %.4e updates/s  frac %.3f  (ms_per_step %.3f)  %s  F %s ms  valu-issue %s" % (
+    r.get("step_ms", r.get("kernel_ms")), d["value"], r["frac"], d["ms_per_step"], r["kernel"], r.get("f_kernel_ms"),
+    (r.get("companion") or {}).get("frac")))
+print("digest %s expected %s match %s  rccl %s" % (d.get("logodds_digest"), d.get("digest_expected"),
+                                                   d.get("digest_match"), d.get("rccl")))
 s = d.get("secondary") or {}
 if s:
     print("reverse %.3f ms/batch  forward %.3f ms/batch  costmap %.3f ms" % (
