@@ -513,6 +513,7 @@ static int integrate_impl(dmf_volume* v, const float* d_xyz, const float* d_nrm,
   v->hazards += (int64_t)hz;
   v->enum_valid = false;
   v->bdist_valid = false;
+  v->sorder_valid = false;
   // CSR over all points, stable in point order within each slot.
   const int64_t N = v->npts;
   void *keys, *vals;
@@ -671,7 +672,10 @@ static void free_state(dmf_volume* v) {
   auto f = [&](void* p) { if (p) (void)hipFree(p); };
   f(v->d_occ); f(v->d_brick); f(v->d_bdist); f(v->d_slot_of); f(v->d_hash); f(v->d_view); f(v->d_good);
   f(v->d_pts); f(v->d_pnrm); f(v->d_pslot); f(v->d_off); f(v->d_csr_nrm); f(v->d_csr_pts);
-  f(v->d_axes); f(v->d_enum);
+  f(v->d_axes); f(v->d_enum); f(v->d_sorder);
+  v->d_sorder = nullptr;
+  v->sorder_cap = 0;
+  v->sorder_valid = false;
   for (auto& s : v->scratch) f(s.first);
   v->scratch.clear();
   v->d_occ = nullptr; v->d_brick = nullptr; v->d_bdist = nullptr; v->bdist_valid = false; v->d_slot_of = nullptr; v->d_hash = nullptr; v->d_view = nullptr; v->d_good = nullptr;

@@ -834,6 +834,31 @@ __device__ inline uint32_t bk_e30(int32_t e) {
   return (uint32_t)(e > lim ? lim : (e < -lim ? -lim : e)) & 0x3fffffffu;
 }
 
+#if defined(DMF_EXP_B_F64)
+// Boundary counts in double arithmetic (experiment): every quantity of count_at is an
+// integer below 2^41, exact in a double; q = floor(X * RN(1/Y)) is within one of
+// floor(X / Y) and the exact remainder X - qY (fma, exact) corrects it.
+struct BF64 {
+  double adq[3], h[3], inv[3];
+};
+template <int A>
+__device__ inline void counts_f64(const bk::QRay& r, const BF64& f, int32_t k, int32_t c[3]) {
+  const double Ha = fma(2.0 * (double)bk::kQ, (double)k, f.h[A]);
+  const double Y = 2.0 * (double)bk::kQ * f.adq[A];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    if (b == A) { c[b] = k + 1; continue; }
+    const double X = fma(Ha, f.adq[b], -(f.h[b] * f.adq[A])) - (b > A ? 1.0 : 0.0);
+    double q = floor(X * f.inv[A]);
+    const double rm = fma(-q, Y, X);
+    q += rm < 0.0 ? -1.0 : (rm >= Y ? 1.0 : 0.0);
+    const int32_t cq = (int32_t)q + 1;
+    const bool none = b > A ? X < 0.0 : X < 0.0;  // X (biased for b > A) < 0: no crossing yet
+    c[b] = (r.st[b] == 0 || none) ? 0 : (cq < r.n[b] ? cq : r.n[b]);
+  }
+}
+#endif
+
 template <bool SLAB>
 __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose, int wg_pose, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
@@ -925,8 +950,12 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
         uint32_t w[5];
         bk::pack20((int32_t)e.x, (int32_t)e.y, (int32_t)e.z, aM, a1, a2, e.w, last, steps, signs >> 22, (uint32_t)M,
                    ends, w);
+#if defined(DMF_DIAG_B_NOSTORE)  // diagnostic build (wrong results): no record stores
+        if ((w[0] ^ w[1] ^ w[2] ^ w[3] ^ w[4] ^ slot) == 0x9e3779b9u) pw[0] = 0;  // keep the record live
+#else
         pa[slot] = make_uint4(w[0], w[1], w[2], w[3]);
         pw[slot] = w[4];
+#endif
       } else {
         e.x = bk_e30((int32_t)e.x) | (steps & 3u) << 30;
         e.y = bk_e30((int32_t)e.y) | ((steps >> 2) & 3u) << 30;
@@ -945,6 +974,15 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
     auto boundary_k = [&](int ax, int nb) {
       return R.st[ax] > 0 ? (nb << bk::kLog) - R.cs[ax] - 1 : R.cs[ax] - (nb << bk::kLog) - bk::kB;
     };
+#if defined(DMF_EXP_B_F64)
+    BF64 fd;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+      fd.adq[ax] = (double)R.adq[ax];
+      fd.h[ax] = (double)R.h0[ax];
+      fd.inv[ax] = R.adq[ax] ? 1.0 / (double)(2 * bk::kQ * R.adq[ax]) : 0.0;
+    }
+#endif
     const int32_t c00[3] = {0, 0, 0};
     uint4 cur = entry(c00);
     int32_t idx = 0;                    // crossings before the current pair's first cell
@@ -960,10 +998,20 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
     bk_coarse(bg, R, [&](int b, int a, int bx, int by, int bz) {
       if (a >= 0) {
         int32_t c[3];
+#if defined(DMF_EXP_B_F64)  // experiment: boundary counts in double arithmetic (count_at_f64)
+        if (a == 0) counts_f64<0>(R, fd, boundary_k(0, bx), c);
+        else if (a == 1) counts_f64<1>(R, fd, boundary_k(1, by), c);
+        else counts_f64<2>(R, fd, boundary_k(2, bz), c);
+#elif defined(DMF_DIAG_B_NOCOUNT)  // diagnostic build (wrong results): no boundary counts
+        c[0] = bx + (a == 0);
+        c[1] = by + (a == 1);
+        c[2] = bz + (a == 2);
+#else
         // constant axis in each call: no dynamically indexed (scratch) arrays
         if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
         else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
         else bk::counts_at(R, 2, boundary_k(2, bz), c);
+#endif
         put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
         cur = entry(c);
         idx = c[0] + c[1] + c[2];
@@ -971,7 +1019,11 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
         ci1 = c[1];
         ci2 = c[2];
       }
+#if defined(DMF_DIAG_B_NOATOMIC)  // diagnostic build (wrong results): no slot atomics
+      slot = hist[b] + (uint32_t)(threadIdx.x & 63);
+#else
       slot = atomicAdd(&hist[b], 1u);
+#endif
     });
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }

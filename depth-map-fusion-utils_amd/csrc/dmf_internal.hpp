@@ -214,6 +214,11 @@ struct dmf_volume {
   uint32_t* d_brick = nullptr;  // one bit per 8^3 brick
   uint8_t* d_bdist = nullptr;   // brick distance field (DevVol::bdist), valid when bdist_valid
   bool bdist_valid = false;
+  // occupied voxels in spatial (3D Morton) order: d_sorder[k] = slot of the k-th, followed by
+  // the inverse rank[slot] (sorder_cap entries each); reverseRayTraceFast's work order
+  uint32_t* d_sorder = nullptr;
+  int64_t sorder_cap = 0;
+  bool sorder_valid = false;
   int brick_shift = dmf::kBrickShiftDefault, brick_cap = dmf::kBrickDistCapDefault;
   int32_t nb[3] = {0, 0, 0};
   int32_t* d_slot_of = nullptr;

@@ -204,16 +204,12 @@ __global__ __launch_bounds__(256) void k_reverse(Geom g, DevVol vd, CamP cam, co
 struct RevLane {
   float cen[3], v[3], rv[3];
   int cx, cy, cz;
-  bool fdiv;            // march_sample_fast is exact for this lane's v
   int s;                // next sample index
   uint32_t known_full;  // last brick found occupied / not skippable
   int item;             // local item index, -1 = idle
   int32_t slot;
   float tz;             // camera-frame z of the centroid (z-range test)
   uint32_t occi, occw;  // cached occupancy word
-  bool pend;            // kDefer: sample s is an unverified jump landing
-  int ps, pR, pb[3];    // its origin sample, cube radius and origin brick
-  uint32_t pbl;         // the origin brick's index
 };
 
 __device__ inline bool valid_points_f(const Geom& g, const float p[3]) {
@@ -222,43 +218,23 @@ __device__ inline bool valid_points_f(const Geom& g, const float p[3]) {
          (p[2] <= g.vhi[2]);
 }
 
-// march_sample without div_rn's range guard: exact when every non-zero |v_a| >= 2^-30, so
-// that |v_a * depth| lies in div_rn's checked domain [2^-40, 2^40] (tools/fastdiv_selftest.cpp)
-// or is +-0 (whose sign no later step can see: it is only added to the centre and then
-// compared / binned).  Lanes flag it at setup (RevLane::fdiv); a wave takes this path when
-// all its busy lanes do.
-__device__ inline void march_sample_fast(const float cen[3], const float v[3], int depth, float p[3]) {
-  const float fd = (float)depth, y = 1.0f / 1000.0f;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const float n = v[a] * fd;
-    const float q0 = n * y;
-    const float r = fmaf(-1000.0f, q0, n);
-    p[a] = cen[a] + fmaf(r, y, q0);
-  }
-}
-
-template <bool kFastDiv>
-__device__ inline void rev_sample(const float cen[3], const float v[3], int depth, float p[3]) {
-  if (kFastDiv) march_sample_fast(cen, v, depth, p);
-  else march_sample(cen, v, depth, p);
-}
-
 // getVoxel of a point inside the volume in the reference's double arithmetic (bin_axis).
 // (The certified float bins of dmf_geom.hpp bin_axis_f, exact by tools/binning_selftest.cpp,
 // measured SLOWER in the reverse march: 8.35 vs 7.57 ms per 128-pose batch -- gfx950 runs
-// the fp64 add / mul / floor / converts at the non-packed fp32 rate, and the certification
-// adds instructions and a branch; kept as k_reverse_q mode 2 for A/B.)
+// the fp64 add / mul / floor / converts at the non-packed fp32 rate)
 __device__ inline void bin_point(const Geom& g, const float p[3], int& a, int& b, int& c) {
   a = bin_axis(g, 0, p[0]);
   b = bin_axis(g, 1, p[1]);
   c = bin_axis(g, 2, p[2]);
 }
 
-__device__ inline void bin_point_f(const Geom& g, const float p[3], int& a, int& b, int& c) {
-  const int ok = (int)bin_axis_f(g, 0, p[0], &a) & (int)bin_axis_f(g, 1, p[1], &b) & (int)bin_axis_f(g, 2, p[2], &c);
-  if (!(g.fbin && ok)) bin_point(g, p, a, b, c);
-}
+// Diagnostic build (DMF_EXP_STATS): sample categories into stats[2..12]
+#if defined(DMF_EXP_STATS)
+#define DMF_RS(i, x) (rst[(i) - 2] += (unsigned long long)(x))
+#else
+#define DMF_RS(i, x) ((void)0)
+#endif
+constexpr int kRevStatN = 11;
 
 // One sample of the reverse march (RayTracingEngine.hpp:172-200): 0 = continue,
 // 1 = collided, 2 = left the volume (visible), 3 = capped (collided, hazard).
@@ -270,62 +246,21 @@ __device__ inline void bin_point_f(const Geom& g, const float p[3], int& a, int&
 // (and inside the volume) so does every sample between them — none can hit an
 // occupied cell, the centroid's cell (occupied) or leave the volume.  j is estimated
 // from the cube faces and verified by evaluating sample j exactly.
-template <bool kFBin>
-__device__ inline void bin_point_t(const Geom& g, const float p[3], int& a, int& b, int& c) {
-  if (kFBin) bin_point_f(g, p, a, b, c);
-  else bin_point(g, p, a, b, c);
-}
-
-// Diagnostic build (DMF_EXP_STATS): sample categories into stats[2..12] (tools/gpu_rev_stats.sh)
-#if defined(DMF_EXP_STATS)
-#define DMF_RS(i, x) (rst[(i) - 2] += (unsigned long long)(x))
-#else
-#define DMF_RS(i, x) ((void)0)
-#endif
-constexpr int kRevStatN = 11;
-
-// kDefer: a jump to sample j is not verified in the call that finds it.  The call sets
-// L.s = j and records the cube (origin brick, radius) and the sample it jumped from; the
-// next call evaluates sample j as its ordinary sample and accepts the jump if j lies in
-// the cube (then j is inside the volume, empty and not the centroid's cell, and the brick
-// logic continues from j at once), else it steps on from the origin sample + 1 as the
-// plain march would.  Every call is then one sample evaluation (the landing sample is no
-// longer a second one inside the divergent jump branch).
-template <bool kFastDiv, bool kFBin, bool kDefer = false>
 __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int depth0, int max_steps,
                                int64_t& samples, unsigned long long* rst) {
   (void)rst;
   if (L.s >= max_steps) return 3;
   float p[3];
-  rev_sample<kFastDiv>(L.cen, L.v, depth0 + L.s, p);
+  march_sample(L.cen, L.v, depth0 + L.s, p);
   ++samples;
   int a, b, c;
-  if (kDefer && L.pend) {
-    L.pend = false;
-    bool in = valid_points_f(g, p);
-    if (in) {
-      bin_point_t<kFBin>(g, p, a, b, c);
-      const int R = L.pR;
-      in = a >= 0 && b >= 0 && c >= 0 && a < g.n[0] && b < g.n[1] && c < g.n[2] &&
-           abs((a >> vd.bsh) - L.pb[0]) <= R && abs((b >> vd.bsh) - L.pb[1]) <= R && abs((c >> vd.bsh) - L.pb[2]) <= R;
-    }
-    if (!in) {  // jump rejected: step on from the sample after its origin
-      DMF_RS(12, 1);
-      L.known_full = L.pbl;
-      L.s = L.ps + 1;
-      return 0;
-    }
-    DMF_RS(5, 1);
-    DMF_RS(6, L.s - L.ps - 1);
-  } else {
-    if (!valid_points_f(g, p)) return 2;
-    bin_point_t<kFBin>(g, p, a, b, c);
-    if (a == L.cx && b == L.cy && c == L.cz) { DMF_RS(2, 1); ++L.s; return 0; }
-    if (!valid_coords(g, a, b, c)) return 2;
-    const uint32_t ob = occ_bit(g, a, b, c);
-    if ((ob >> 5) != L.occi) { L.occi = ob >> 5; L.occw = vd.occ[L.occi]; }
-    if ((L.occw >> (ob & 31)) & 1u) return 1;
-  }
+  if (!valid_points_f(g, p)) return 2;
+  bin_point(g, p, a, b, c);
+  if (a == L.cx && b == L.cy && c == L.cz) { DMF_RS(2, 1); ++L.s; return 0; }
+  if (!valid_coords(g, a, b, c)) return 2;
+  const uint32_t ob = occ_bit(g, a, b, c);
+  if ((ob >> 5) != L.occi) { L.occi = ob >> 5; L.occw = vd.occ[L.occi]; }
+  if ((L.occw >> (ob & 31)) & 1u) return 1;
   const int ba = a >> vd.bsh, bb = b >> vd.bsh, bc = c >> vd.bsh;
   const uint32_t bl = ((uint32_t)ba * (uint32_t)vd.nb[1] + (uint32_t)bb) * (uint32_t)vd.nb[2] + (uint32_t)bc;
   if (bl != L.known_full) {
@@ -347,29 +282,17 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
       if (jf > (float)(L.s + 1) && jf < (float)max_steps) {
         const int j = (int)jf;
         DMF_RS(4, 1);
-        if constexpr (kDefer) {
-          L.pend = true;
-          L.ps = L.s;
-          L.pbl = bl;
-          L.pR = R;
-          L.pb[0] = ba;
-          L.pb[1] = bb;
-          L.pb[2] = bc;
-          L.s = j;
-          return 0;
-        } else {
-          float q[3];
-          rev_sample<kFastDiv>(L.cen, L.v, depth0 + j, q);
-          ++samples;
-          if (valid_points_f(g, q)) {
-            int qa, qb, qc;
-            bin_point_t<kFBin>(g, q, qa, qb, qc);
-            if (qa >= clo[0] && qa < chi[0] && qb >= clo[1] && qb < chi[1] && qc >= clo[2] && qc < chi[2]) {
-              DMF_RS(5, 1);
-              DMF_RS(6, j - L.s);
-              L.s = j + 1;  // samples s+1 .. j lie inside the empty cube
-              return 0;
-            }
+        float q[3];
+        march_sample(L.cen, L.v, depth0 + j, q);
+        ++samples;
+        if (valid_points_f(g, q)) {
+          int qa, qb, qc;
+          bin_point(g, q, qa, qb, qc);
+          if (qa >= clo[0] && qa < chi[0] && qb >= clo[1] && qb < chi[1] && qc >= clo[2] && qc < chi[2]) {
+            DMF_RS(5, 1);
+            DMF_RS(6, j - L.s);
+            L.s = j + 1;  // samples s+1 .. j lie inside the empty cube
+            return 0;
           }
         }
       }
@@ -383,17 +306,22 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   return 0;
 }
 
-// kMode (A/B): bit 0 = the guard-free division for waves that allow it, bit 1 = the
-// certified float bins.  Measured per 128-pose batch (414k voxels): 0 7.57-7.61 ms,
-// 1 7.55-7.59, 2 8.35, 3 8.73: the default is 0.
-template <bool kEnum, int kItems, int kRefill, int kBurst, int kMode = 0>
+// kOrder (reverseRayTraceFast only): the wave's items are the occupied voxels in SPATIAL
+// order (order[k] = the slot of the k-th voxel along a 3D Morton curve of its cell,
+// ensure_spatial_order), so that a wave's 64 lanes start in neighbouring voxels: their rays
+// toward the camera are near-parallel, cross the same bricks and end alike (all occluded or
+// all visible).  The result bits are then in item order: vis_mask / good_mask receive
+// item-ordered words, which k_mask_to_slots permutes into occupied_cells_ order (the output
+// is a per-slot bitmask, so the processing order is free).
+template <bool kEnum, int kItems, int kRefill, int kBurst, bool kOrder = false>
 __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses,
-                                                   int64_t nelem, EnumList el, int depth0, int max_steps, float dstar,
-                                                   int viz, int normal_test, uint64_t* __restrict__ vis_mask,
-                                                   uint64_t* __restrict__ good_mask, int64_t words,
-                                                   unsigned long long* __restrict__ stats, int* __restrict__ found,
-                                                   unsigned long long* __restrict__ hazards) {
+                                                   int64_t nelem, EnumList el, const uint32_t* __restrict__ order,
+                                                   int depth0, int max_steps, float dstar, int viz, int normal_test,
+                                                   uint64_t* __restrict__ vis_mask, uint64_t* __restrict__ good_mask,
+                                                   int64_t words, unsigned long long* __restrict__ stats,
+                                                   int* __restrict__ found, unsigned long long* __restrict__ hazards) {
   static_assert(kItems % 64 == 0, "whole mask words per wave");
+  static_assert(!(kEnum && kOrder), "spatial order: occupied_cells_ items only");
   stats = stat_slot(stats);
   __shared__ uint32_t lvis[4][kItems / 32], lgood[4][kItems / 32];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -423,8 +351,8 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
           float cen[3];
           int32_t slot;
           if (!kEnum) {
-            slot = (int32_t)e;
-            const uint64_t h = vd.hash[e];
+            slot = kOrder ? (int32_t)order[e] : (int32_t)e;
+            const uint64_t h = vd.hash[slot];
             const int xid = (int)(h >> 40), yid = (int)((h >> 20) & 0xFFFFF), zid = (int)(h & 0xFFFFF);
             const float x = (float)((double)xid * g.dl[0] + g.mn[0]);
             const float y = (float)((double)yid * g.dl[1] + g.mn[1]);
@@ -453,16 +381,12 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
               L.cen[a] = cen[a];
               L.rv[a] = L.v[a] != 0.0f ? 1000.0f / L.v[a] : 0.0f;
             }
-            L.fdiv = true;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) L.fdiv &= L.v[a] == 0.0f || fabsf(L.v[a]) >= 0x1p-30f;
             L.cx = bin_axis(g, 0, cen[0]);
             L.cy = bin_axis(g, 1, cen[1]);
             L.cz = bin_axis(g, 2, cen[2]);
             L.s = 0;
             L.known_full = 0xffffffffu;
             L.occi = 0xffffffffu;
-            L.pend = false;
             L.item = it;
             L.slot = slot;
             L.tz = t[2];
@@ -476,24 +400,14 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
       if (next >= nitems) break;
       continue;
     }
-    // march: up to kBurst samples per busy lane (the guard-free division when every busy
-    // lane allows it: a wave-uniform choice)
+    // march: up to kBurst samples per busy lane
     int st = 0;
-    constexpr bool kFB = (kMode & 2) != 0, kCH = (kMode & 4) != 0;
-    if ((kMode & 1) && __builtin_amdgcn_ballot_w64(L.item >= 0 && !L.fdiv) == 0) {
 #pragma unroll 1
-      for (int b = 0; b < kBurst; ++b) {
-        if (L.item >= 0 && st == 0) st = rev_step<true, kFB, kCH>(g, vd, L, depth0, max_steps, samples, rst);
-        if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
-      }
-    } else {
-#pragma unroll 1
-      for (int b = 0; b < kBurst; ++b) {
-        DMF_RS(10, l == 0);
-        DMF_RS(11, L.item >= 0 && st == 0);
-        if (L.item >= 0 && st == 0) st = rev_step<false, kFB, kCH>(g, vd, L, depth0, max_steps, samples, rst);
-        if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
-      }
+    for (int b = 0; b < kBurst; ++b) {
+      DMF_RS(10, l == 0);
+      DMF_RS(11, L.item >= 0 && st == 0);
+      if (L.item >= 0 && st == 0) st = rev_step(g, vd, L, depth0, max_steps, samples, rst);
+      if (__builtin_amdgcn_ballot_w64(L.item >= 0 && st == 0) == 0) break;
     }
     if (L.item >= 0 && st != 0) {
       DMF_RS(7, st == 1);
@@ -545,6 +459,84 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
     for (int i = 0; i < kRevStatN; ++i) wave_add_u64(&stats[2 + i], rst[i]);
 #endif
   }
+}
+
+// Item-ordered result bits (k_reverse_q<*, kOrder>) -> occupied_cells_ order: one wave per
+// output word of 64 slots, all P poses; lane l takes slot 64 w + l, whose item is rank[slot].
+__global__ __launch_bounds__(256) void k_mask_to_slots(const uint64_t* __restrict__ vis_items,
+                                                       const uint64_t* __restrict__ good_items,
+                                                       const uint32_t* __restrict__ rank, int64_t V, int64_t words,
+                                                       int P, uint64_t* __restrict__ vis, uint64_t* __restrict__ good) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int l = threadIdx.x & 63;
+  if (w >= words) return;
+  const int64_t s = w * 64 + l;
+  const uint32_t k = s < V ? rank[s] : 0u;
+  for (int p = 0; p < P; ++p) {
+    const int64_t row = (int64_t)p * words;
+    bool bv = false, bg = false;
+    if (s < V) {
+      bv = (vis_items[row + (k >> 6)] >> (k & 63)) & 1ull;
+      bg = (good_items[row + (k >> 6)] >> (k & 63)) & 1ull;
+    }
+    const uint64_t mv = __builtin_amdgcn_ballot_w64(bv), mg = __builtin_amdgcn_ballot_w64(bg);
+    if (l == 0) {
+      vis[row + w] = mv;
+      good[row + w] = mg;
+    }
+  }
+}
+
+// 3D Morton key of an occupied voxel (21 bits per axis; the hash holds 20) and the slot as value.
+__device__ inline uint64_t morton_spread(uint64_t x) {
+  x &= 0x1fffffull;
+  x = (x | x << 32) & 0x1f00000000ffffull;
+  x = (x | x << 16) & 0x1f0000ff0000ffull;
+  x = (x | x << 8) & 0x100f00f00f00f00full;
+  x = (x | x << 4) & 0x10c30c30c30c30c3ull;
+  x = (x | x << 2) & 0x1249249249249249ull;
+  return x;
+}
+__global__ void k_morton_keys(const uint64_t* __restrict__ hash, int64_t V, uint64_t* __restrict__ keys,
+                              uint64_t* __restrict__ vals) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= V) return;
+  const uint64_t h = hash[s];
+  keys[s] = morton_spread(h >> 40) << 2 | morton_spread((h >> 20) & 0xFFFFF) << 1 | morton_spread(h & 0xFFFFF);
+  vals[s] = (uint64_t)s;
+}
+__global__ void k_order_store(const uint64_t* __restrict__ vals, int64_t V, uint32_t* __restrict__ order,
+                              uint32_t* __restrict__ rank) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= V) return;
+  const uint32_t s = (uint32_t)vals[k];
+  order[k] = s;
+  rank[s] = (uint32_t)k;
+}
+
+// The occupied voxels in spatial (3D Morton) order, rebuilt after an integration changed them.
+static int ensure_spatial_order(dmf_volume* v) {
+  if (v->sorder_valid) return DMF_OK;
+  const int64_t V = v->V;
+  if (V > v->sorder_cap) {
+    if (v->d_sorder) DMF_HIP(hipFree(v->d_sorder));
+    v->d_sorder = nullptr;
+    v->sorder_cap = 0;
+    DMF_HIP(hipMalloc((void**)&v->d_sorder, sizeof(uint32_t) * 2 * (size_t)V));
+    v->sorder_cap = V;
+  }
+  void *keys, *vals;
+  DMF_TRY(scratch(v, kScOut2, sizeof(uint64_t) * (size_t)V, &keys));
+  DMF_TRY(scratch(v, kScOut3, sizeof(uint64_t) * (size_t)V, &vals));
+  const dim3 blk(256), grd((unsigned)((V + 255) / 256));
+  hipLaunchKernelGGL(k_morton_keys, grd, blk, 0, v->stream, v->d_hash, V, (uint64_t*)keys, (uint64_t*)vals);
+  DMF_LAUNCH_CHECK();
+  DMF_TRY(sort_pairs_u64(v, (uint64_t*)keys, (uint64_t*)vals, (size_t)V, 63));
+  hipLaunchKernelGGL(k_order_store, grd, blk, 0, v->stream, (const uint64_t*)vals, V, v->d_sorder,
+                     v->d_sorder + v->sorder_cap);
+  DMF_LAUNCH_CHECK();
+  v->sorder_valid = true;
+  return DMF_OK;
 }
 
 // ---- greedy set cover over per-pose good bitmasks (Algorithms.hpp:38-86) ---------
@@ -688,53 +680,53 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
     EnumList el{v->d_axes, {v->nax[0], v->nax[1], v->nax[2]}, v->d_enum};
     const dim3 grid((unsigned)((nelem + 255) / 256), (unsigned)P);
     const int depth0 = enumerate ? 1 : 50;  // :81 vs :172
-    // DMF_KNOB_REVERSE_KERNEL (dmf_diag.h): 0 = the queue + distance field (internal mode 2),
-    // 1 = the plain march, 2 = plain + brick skip (internal 0, 1); >= 3 measured alternatives
+    // DMF_KNOB_REVERSE_KERNEL (dmf_diag.h): 0 = default (the work-queue march with the brick
+    // distance field, items in spatial order for reverseRayTraceFast), 1 = lane per (voxel,
+    // pose), 2 = the same with brick skipping, 3 = the work queue in occupied_cells_ order
     const int64_t kr = v->knob[DMF_KNOB_REVERSE_KERNEL];
-    const int rev_kernel = kr == 0 ? 2 : (kr == 1 ? 0 : (kr == 2 ? 1 : (int)kr));
-#define DMF_REV(E, S, NT)                                                                                        \
-  hipLaunchKernelGGL((k_reverse<E, S>), grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab, \
-                     nelem, el, depth0, max_march_steps(v), v->dstar, viz, NT, vis, good, words, st, found, hz)
-#define DMF_REVQ(E, NT)                                                                                           \
-  hipLaunchKernelGGL((k_reverse_q<E, kRevItems, 8, 8>), gridq, dim3(256), 0, v->stream, v->geom(), v->dev(),       \
-                     cam_params(cam), tab, nelem, el, depth0, max_march_steps(v), v->dstar, viz, NT, vis, good, words, \
-                     st, found, hz)
-#define DMF_REVQM(E, NT, MODE)                                                                                     \
-  hipLaunchKernelGGL((k_reverse_q<E, kRevItems, 8, 8, MODE>), gridq, dim3(256), 0, v->stream, v->geom(), v->dev(), \
-                     cam_params(cam), tab, nelem, el, depth0, max_march_steps(v), v->dstar, viz, NT, vis, good, words, \
-                     st, found, hz)
-#define DMF_REVQX(E, NT, IT, RF, BU)                                                                              \
-  hipLaunchKernelGGL((k_reverse_q<E, IT, RF, BU>), dim3((unsigned)((nelem + 4 * IT - 1) / (4 * IT)), (unsigned)P),       \
-                     dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab, nelem, el, depth0,             \
-                     max_march_steps(v), v->dstar, viz, NT, vis, good, words, st, found, hz)
     constexpr int kRevItems = 512;
     const dim3 gridq((unsigned)((nelem + 4 * kRevItems - 1) / (4 * kRevItems)), (unsigned)P);
-    if (rev_kernel >= 2) {
+    const Geom g = v->geom();
+    const DevVol dv = v->dev();
+    const CamP cp = cam_params(cam);
+    const int ms = max_march_steps(v);
+    if (kr == 1 || kr == 2) {
+      const bool skip = kr == 2;
+      if (enumerate) {
+        if (skip) hipLaunchKernelGGL((k_reverse<true, true>), grid, dim3(256), 0, v->stream, g, dv, cp, tab, nelem, el,
+                                     depth0, ms, v->dstar, viz, 0, vis, good, words, st, found, hz);
+        else hipLaunchKernelGGL((k_reverse<true, false>), grid, dim3(256), 0, v->stream, g, dv, cp, tab, nelem, el,
+                                depth0, ms, v->dstar, viz, 0, vis, good, words, st, found, hz);
+      } else {
+        if (skip) hipLaunchKernelGGL((k_reverse<false, true>), grid, dim3(256), 0, v->stream, g, dv, cp, tab, nelem,
+                                     el, depth0, ms, v->dstar, viz, 1, vis, good, words, st, found, hz);
+        else hipLaunchKernelGGL((k_reverse<false, false>), grid, dim3(256), 0, v->stream, g, dv, cp, tab, nelem, el,
+                                depth0, ms, v->dstar, viz, 1, vis, good, words, st, found, hz);
+      }
+    } else {
       DMF_TRY(ensure_brick_dist(v));
       // the queue kernel writes every mask word it owns; words past the last wave stay 0
-      switch (rev_kernel) {
-        case 3: if (enumerate) DMF_REVQX(true, 0, 512, 32, 8); else DMF_REVQX(false, 1, 512, 32, 8); break;
-        case 4: if (enumerate) DMF_REVQX(true, 0, 512, 16, 8); else DMF_REVQX(false, 1, 512, 16, 8); break;
-        case 5: if (enumerate) DMF_REVQX(true, 0, 512, 16, 16); else DMF_REVQX(false, 1, 512, 16, 16); break;
-        case 6: if (enumerate) DMF_REVQX(true, 0, 1024, 16, 8); else DMF_REVQX(false, 1, 1024, 16, 8); break;
-        case 7: if (enumerate) DMF_REVQX(true, 0, 256, 16, 4); else DMF_REVQX(false, 1, 256, 16, 4); break;
-        case 8: if (enumerate) DMF_REVQX(true, 0, 512, 24, 4); else DMF_REVQX(false, 1, 512, 24, 4); break;
-        case 9: if (enumerate) DMF_REVQM(true, 0, 3); else DMF_REVQM(false, 1, 3); break;    // fast division + float bins
-        case 10: if (enumerate) DMF_REVQM(true, 0, 2); else DMF_REVQM(false, 1, 2); break;   // float bins only
-        case 11: if (enumerate) DMF_REVQM(true, 0, 1); else DMF_REVQM(false, 1, 1); break;   // fast division only
-        case 12: if (enumerate) DMF_REVQM(true, 0, 4); else DMF_REVQM(false, 1, 4); break;   // deferred jump verification
-        case 13: if (enumerate) DMF_REVQM(true, 0, 5); else DMF_REVQM(false, 1, 5); break;   // deferred + fast division
-        default: if (enumerate) DMF_REVQ(true, 0); else DMF_REVQ(false, 1); break;
+      if (enumerate) {
+        hipLaunchKernelGGL((k_reverse_q<true, kRevItems, 8, 8>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab, nelem,
+                           el, nullptr, depth0, ms, v->dstar, viz, 0, vis, good, words, st, found, hz);
+      } else if (kr == 3) {
+        hipLaunchKernelGGL((k_reverse_q<false, kRevItems, 8, 8>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab,
+                           nelem, el, nullptr, depth0, ms, v->dstar, viz, 1, vis, good, words, st, found, hz);
+      } else {
+        DMF_TRY(ensure_spatial_order(v));
+        void* items;
+        DMF_TRY(scratch(v, kScRevItems, sizeof(uint64_t) * (size_t)(2 * P * words), &items));
+        uint64_t* vis_i = (uint64_t*)items;
+        uint64_t* good_i = vis_i + P * words;
+        hipLaunchKernelGGL((k_reverse_q<false, kRevItems, 8, 8, true>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab,
+                           nelem, el, (const uint32_t*)v->d_sorder, depth0, ms, v->dstar, viz, 1, vis_i, good_i, words,
+                           st, found, hz);
+        DMF_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_mask_to_slots, dim3((unsigned)((words * 64 + 255) / 256)), dim3(256), 0, v->stream,
+                           (const uint64_t*)vis_i, (const uint64_t*)good_i, (const uint32_t*)(v->d_sorder + v->sorder_cap),
+                           nelem, words, P, vis, good);
       }
-    } else if (enumerate) {
-      if (rev_kernel == 1) DMF_REV(true, true, 0); else DMF_REV(true, false, 0);
-    } else {
-      if (rev_kernel == 1) DMF_REV(false, true, 1); else DMF_REV(false, false, 1);
     }
-#undef DMF_REV
-#undef DMF_REVQ
-#undef DMF_REVQX
-#undef DMF_REVQM
     DMF_LAUNCH_CHECK();
   }
 #if defined(DMF_EXP_STATS)

@@ -94,9 +94,17 @@ def _flags(v_or, v_gpu):
     return ov, og, gview, ggood
 
 
-def test_reverse_fast_parity(oracle, engine, oeng):
+@pytest.mark.parametrize("kernel", [0, 3, 1, 2])
+def test_reverse_fast_parity(oracle, engine, oeng, kernel):
+    """reverseRayTraceFast (RayTracingEngine.hpp:136-226) over 12 poses, every march kernel
+    (DMF_KNOB_REVERSE_KERNEL): 0 = the default work queue in spatial (Morton) item order with
+    the item -> slot mask permutation, 3 = the work queue in occupied_cells_ order, 1 / 2 =
+    one lane per (voxel, pose) without / with brick skipping: lists (order included), found
+    and view / good flags equal the oracle's."""
+    from dmf_amd import _lib
     ov = Hh.oracle_volume(oracle)
     gv = Hh.gpu_volume()
+    _lib.set_knob(gv, "reverse_kernel", kernel)
     poses = Hh.all_poses()
     found, lists = engine.reverseRayTraceFastBatch(gv, poses, viz=False)
     for i, T in enumerate(poses):

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""A/B of reverseRayTraceFast work orders (DMF_KNOB_REVERSE_KERNEL 0 = spatial order, 3 =
+occupied_cells_ order) on bench.py's secondary workload: a 512^3 volume integrated from 16
+back-projected 640x480 frames, 128 poses per launch.  Prints ms per launch for each and
+checks the visibility / good masks are identical."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "depth-map-fusion-utils_amd")]
+import dmf_amd  # noqa: E402
+from dmf_amd import _lib, scene  # noqa: E402
+
+W, H, P, NI = 640, 480, 128, 16
+dev = torch.device("cuda", 0)
+K = scene.intrinsics(W, H)
+poses = np.ascontiguousarray(scene.fibonacci_poses(P, seed=1234), np.float32)
+cache = f"/tmp/exp_depth_{W}x{H}_{P}.npy"
+depth = np.load(cache) if os.path.exists(cache) else np.ascontiguousarray(scene.render_frames(K, W, H, poses), np.uint16)
+L = _lib.load()
+vol = dmf_amd.VoxelVolume(0)
+s = torch.cuda.current_stream(dev)
+vol.set_stream(s.cuda_stream)
+vol.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+vol.setVolumeSize(512, 512, 512)
+vol.constructVolume()
+cam = _lib.make_camera(K, H, W)
+d_depth = torch.from_numpy(depth.view(np.int16)).to(dev)
+d_poses = torch.from_numpy(poses).to(dev)
+xyz = torch.empty((NI, H, W, 3), dtype=torch.float32, device=dev)
+_lib.check(L.dmf_backproject_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(), NI, xyz.data_ptr()))
+valid = (d_depth[:NI].view(torch.int16) > 0).reshape(-1)
+pts = xyz.reshape(-1, 3)[valid].contiguous()
+nrm = np.concatenate([scene.render(K, W, H, poses[i])[1].reshape(-1, 3) for i in range(NI)])
+d_nrm = torch.from_numpy(nrm).to(dev).reshape(-1, 3)[valid].contiguous()
+vol.integrate_device(pts.data_ptr(), d_nrm.data_ptr(), pts.shape[0])
+V = vol.info()["num_occupied"]
+words = (V + 63) // 64
+out = {"voxels": int(V), "poses": P}
+res = {}
+for kr in (3, 0, 3, 0):
+    _lib.set_knob(vol, "reverse_kernel", kr)
+    vis = torch.zeros(P * words, dtype=torch.int64, device=dev)
+    good = torch.zeros(P * words, dtype=torch.int64, device=dev)
+    st = torch.zeros(16, dtype=torch.int64, device=dev)
+
+    def run():
+        _lib.check(L.dmf_reverse_visibility_device(vol._h, C.addressof(cam), d_poses.data_ptr(), P, 0, vis.data_ptr(),
+                                                   good.data_ptr(), st.data_ptr()))
+    run()
+    torch.cuda.synchronize(dev)
+    st.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(5):
+        run()
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    out[f"ms_kernel{kr}"] = e0.elapsed_time(e1) / 5
+    out[f"samples_kernel{kr}"] = int(st[0].item()) // 5
+    res[kr] = (vis.cpu().numpy(), good.cpu().numpy())
+out["masks_equal"] = bool(np.array_equal(res[0][0], res[3][0]) and np.array_equal(res[0][1], res[3][1]))
+print(json.dumps(out), flush=True)

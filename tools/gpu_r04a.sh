@@ -10,7 +10,7 @@ tail -40 gpurun_out/r04a/gpu_tests.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "TESTS ABORTED rc=$rc"; exit 1; }
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04a/smoke.log 2>&1 || { echo SMOKEFAIL; tail -20 gpurun_out/r04a/smoke.log; exit 2; }
 timeout -k 10 400 python bench.py --pmc-dir gpurun_out/r04a/pmc > gpurun_out/r04a/bench.json 2> gpurun_out/r04a/bench.err || { echo BENCHFAIL; tail -20 gpurun_out/r04a/bench.err; exit 3; }
-python3 tools/show_bench.py gpurun_out/r04a/bench.json
+python3 tools/show_bench.py gpurun_out/r04a/bench.json || true
 timeout -k 10 300 python3 bench.py --grid 256 --poses-per-gpu 64 --cpu-frames 8 --no-secondary > gpurun_out/r04a/config2.json 2> gpurun_out/r04a/config2.err || { echo FAIL2; tail gpurun_out/r04a/config2.err; exit 4; }
 python3 tools/show_bench.py gpurun_out/r04a/config2.json
 echo "TESTRC $rc"

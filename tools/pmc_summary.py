@@ -20,7 +20,7 @@ os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
 tot = collections.defaultdict(float)
 ndisp = collections.defaultdict(set)
-for f in sorted(glob.glob(os.path.join(src, "pmc*", "run_counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(src, "pmc*", "run_counter_collection.csv")) + glob.glob(os.path.join(src, "p[0-9]*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
         if not k.startswith("dmf::"):
