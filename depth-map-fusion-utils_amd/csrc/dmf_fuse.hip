@@ -895,11 +895,24 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
   constexpr uint32_t m5 = bk::kB - 1;
   // the next packet's ray record is loaded one packet ahead: its HBM latency hides behind
   // this packet's coarse walk (B 2.03 -> 1.92 ms) instead of stalling the wave per packet
+#if defined(DMF_EXP_B_STRIDE)
+  // experiment: lane l of virtual packet v takes pixel l of packet (v + l) mod npk of the
+  // workgroup's span, so that a wave's lanes walk rays up to a span apart (different bricks:
+  // fewer same-address slot atomics) instead of one 8x8 packet's neighbouring rays
+  const int npk = (int)(pk1 - pk0);
+  auto ray_at = [&](int vp) { return rays[(pk0 + (int64_t)((vp + l) % npk)) * 64 + l]; };
+  ulonglong2 rnext = make_ulonglong2(0, 0);
+  if (w < npk) rnext = ray_at(w);
+  for (int vp = w; vp < npk; vp += nw) {
+    const ulonglong2 rec = rnext;
+    if (vp + nw < npk) rnext = ray_at(vp + nw);
+#else
   ulonglong2 rnext = make_ulonglong2(0, 0);
   if (pk0 + w < pk1) rnext = rays[(pk0 + w) * 64 + l];
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
     const ulonglong2 rec = rnext;
     if (pk + nw < pk1) rnext = rays[(pk + nw) * 64 + l];
+#endif
     if ((rec.y >> 63) == 0) continue;  // no ray
     bk::QRay R;
     bk::decode_ray(rec.x, rec.y, R);
@@ -1021,6 +1034,18 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
       }
 #if defined(DMF_DIAG_B_NOATOMIC)  // diagnostic build (wrong results): no slot atomics
       slot = hist[b] + (uint32_t)(threadIdx.x & 63);
+#elif defined(DMF_EXP_B_UNI)  // experiment: one atomic when every active lane names the same brick
+      {
+        const uint64_t act = __builtin_amdgcn_ballot_w64(true);
+        const int b0 = __builtin_amdgcn_readfirstlane(b);
+        if (__builtin_amdgcn_ballot_w64(b == b0) == act) {
+          uint32_t old = 0;
+          if (l == __builtin_ctzll(act)) old = atomicAdd(&hist[b0], (uint32_t)__builtin_popcountll(act));
+          slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)old) + (uint32_t)lane_prefix(act);
+        } else {
+          slot = atomicAdd(&hist[b], 1u);
+        }
+      }
 #else
       slot = atomicAdd(&hist[b], 1u);
 #endif

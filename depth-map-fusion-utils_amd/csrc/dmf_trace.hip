@@ -684,7 +684,11 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
     // distance field, items in spatial order for reverseRayTraceFast), 1 = lane per (voxel,
     // pose), 2 = the same with brick skipping, 3 = the work queue in occupied_cells_ order
     const int64_t kr = v->knob[DMF_KNOB_REVERSE_KERNEL];
-    constexpr int kRevItems = 512;
+#if defined(DMF_EXP_REV_ITEMS)  // experiment builds: work-queue shape
+    constexpr int kRevItems = DMF_EXP_REV_ITEMS, kRevRefill = DMF_EXP_REV_REFILL, kRevBurst = DMF_EXP_REV_BURST;
+#else
+    constexpr int kRevItems = 512, kRevRefill = 8, kRevBurst = 8;
+#endif
     const dim3 gridq((unsigned)((nelem + 4 * kRevItems - 1) / (4 * kRevItems)), (unsigned)P);
     const Geom g = v->geom();
     const DevVol dv = v->dev();
@@ -707,10 +711,10 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
       DMF_TRY(ensure_brick_dist(v));
       // the queue kernel writes every mask word it owns; words past the last wave stay 0
       if (enumerate) {
-        hipLaunchKernelGGL((k_reverse_q<true, kRevItems, 8, 8>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab, nelem,
+        hipLaunchKernelGGL((k_reverse_q<true, kRevItems, kRevRefill, kRevBurst>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab, nelem,
                            el, nullptr, depth0, ms, v->dstar, viz, 0, vis, good, words, st, found, hz);
       } else if (kr == 3) {
-        hipLaunchKernelGGL((k_reverse_q<false, kRevItems, 8, 8>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab,
+        hipLaunchKernelGGL((k_reverse_q<false, kRevItems, kRevRefill, kRevBurst>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab,
                            nelem, el, nullptr, depth0, ms, v->dstar, viz, 1, vis, good, words, st, found, hz);
       } else {
         DMF_TRY(ensure_spatial_order(v));
@@ -718,7 +722,7 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
         DMF_TRY(scratch(v, kScRevItems, sizeof(uint64_t) * (size_t)(2 * P * words), &items));
         uint64_t* vis_i = (uint64_t*)items;
         uint64_t* good_i = vis_i + P * words;
-        hipLaunchKernelGGL((k_reverse_q<false, kRevItems, 8, 8, true>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab,
+        hipLaunchKernelGGL((k_reverse_q<false, kRevItems, kRevRefill, kRevBurst, true>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab,
                            nelem, el, (const uint32_t*)v->d_sorder, depth0, ms, v->dstar, viz, 1, vis_i, good_i, words,
                            st, found, hz);
         DMF_LAUNCH_CHECK();

@@ -8,10 +8,12 @@ NAME=$1; shift
 OUT=build_exp/$NAME
 mkdir -p "$OUT"
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-function -I../include -Icsrc"
-# ALL=1: rebuild every object with the extra flags (needed when they change shared headers)
+# ALL=1: rebuild every object with the extra flags (needed when they change shared headers);
+# REBUILD="dmf_trace ...": the objects to rebuild (default dmf_fuse)
+REBUILD=${REBUILD:-dmf_fuse}
 OBJS=""
 for f in dmf_core dmf_trace dmf_fuse dmf_ogrid dmf_comm dmf_io; do
-  if [ "$f" = dmf_fuse ] || [ -n "$ALL" ]; then
+  if [[ " $REBUILD " == *" $f "* ]] || [ -n "$ALL" ]; then
     /opt/rocm/bin/hipcc $FLAGS "$@" -c csrc/$f.hip -o "$OUT/$f.o" &
     OBJS="$OBJS $OUT/$f.o"
   else

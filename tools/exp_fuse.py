@@ -37,6 +37,7 @@ poses = np.ascontiguousarray(scene.fibonacci_poses(a.poses, seed=1234), np.float
 if os.path.exists(cache):
     depth = np.load(cache)
 else:
+    print(f"[exp_fuse] rendering {a.poses} frames", file=sys.stderr, flush=True)
     depth = np.ascontiguousarray(scene.render_frames(K, W, H, poses), np.uint16)
     np.save(cache, depth)
 L = _lib.load()
@@ -67,6 +68,7 @@ def call():
 out = {"tag": a.tag, "grid": a.grid, "poses": P, "image": a.image, "kernel": None}
 torch.cuda.synchronize(dev)
 for mode in a.modes.split(","):
+    print(f"[exp_fuse {a.tag}] mode {mode}", file=sys.stderr, flush=True)
     _lib.check(L.dmf_fuse_set_input_stream(vol._h, inp.cuda_stream if mode == "pipelined" else None))
     _lib.check(L.dmf_fuse_reserve(vol._h, C.addressof(cam), P, 0))
     cnt.zero_()
