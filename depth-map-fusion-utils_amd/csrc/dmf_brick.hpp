@@ -23,6 +23,7 @@
 // device atomics per update).  All functions are __host__ __device__: the CPU
 // self-test (tools/brick_selftest.cpp) checks them against the plain fine walk.
 #pragma once
+#include <cmath>
 #include <cstdint>
 
 #ifndef __HIPCC__
@@ -182,6 +183,43 @@ __host__ __device__ inline void counts_at_sel(const QRay& r, int a, int32_t k, i
   c[0] = a0 ? k + 1 : c1;
   c[1] = a1 ? k + 1 : (a0 ? c1 : c2);
   c[2] = a2 ? k + 1 : c2;
+}
+
+// counts_at in double arithmetic (pass B's boundary counts).  Every quantity of count_at is
+// an integer below 2^41 -- Ha < 2^20, |dq| < 2^19 on grids <= 2048 cells per axis -- so
+// X = Ha |dq_b| - h_b |dq_a| is exact as fma(Ha, |dq_b|, -(h_b |dq_a|)) (the product h_b |dq_a|
+// and the fma's exact result both fit 53 bits).  q = floor(X * RN(1/Y)) is within one of
+// floor(X / Y) (X / Y < 2^12, relative error < 2^-51), and the remainder X - qY, exact by fma,
+// corrects it.  The tie rule of count_at (b > a: X - 1) is the same bias.  Checked against
+// counts_at by the brick self-test (check 7).
+struct QRayF64 {
+  double adq[3], h[3], inv[3];  // |dq|, first-crossing numerator h0, RN(1 / (2Q |dq|)) (0: non-moving)
+};
+__host__ __device__ inline void qray_f64(const QRay& r, QRayF64& f) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    f.adq[a] = (double)r.adq[a];
+    f.h[a] = (double)r.h0[a];
+    f.inv[a] = r.adq[a] ? 1.0 / (2.0 * (double)kQ * (double)r.adq[a]) : 0.0;
+  }
+}
+template <int A>
+__host__ __device__ inline void counts_at_f64(const QRay& r, const QRayF64& f, int32_t k, int32_t c[3]) {
+  const double Ha = fma(2.0 * (double)kQ, (double)k, f.h[A]);
+  const double Y = 2.0 * (double)kQ * f.adq[A];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    if (b == A) {
+      c[b] = k + 1;
+      continue;
+    }
+    const double X = fma(Ha, f.adq[b], -(f.h[b] * f.adq[A])) - (b > A ? 1.0 : 0.0);
+    double q = floor(X * f.inv[A]);
+    const double rm = fma(-q, Y, X);
+    q += rm < 0.0 ? -1.0 : (rm >= Y ? 1.0 : 0.0);
+    const int32_t cq = (int32_t)q + 1;
+    c[b] = (r.st[b] == 0 || X < 0.0) ? 0 : (cq < r.n[b] ? cq : r.n[b]);
+  }
 }
 
 // One (ray, brick) pair: where the fine walk enters brick (bx, by, bz), how many

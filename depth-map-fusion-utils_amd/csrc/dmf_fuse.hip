@@ -834,30 +834,6 @@ __device__ inline uint32_t bk_e30(int32_t e) {
   return (uint32_t)(e > lim ? lim : (e < -lim ? -lim : e)) & 0x3fffffffu;
 }
 
-#if defined(DMF_EXP_B_F64)
-// Boundary counts in double arithmetic (experiment): every quantity of count_at is an
-// integer below 2^41, exact in a double; q = floor(X * RN(1/Y)) is within one of
-// floor(X / Y) and the exact remainder X - qY (fma, exact) corrects it.
-struct BF64 {
-  double adq[3], h[3], inv[3];
-};
-template <int A>
-__device__ inline void counts_f64(const bk::QRay& r, const BF64& f, int32_t k, int32_t c[3]) {
-  const double Ha = fma(2.0 * (double)bk::kQ, (double)k, f.h[A]);
-  const double Y = 2.0 * (double)bk::kQ * f.adq[A];
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    if (b == A) { c[b] = k + 1; continue; }
-    const double X = fma(Ha, f.adq[b], -(f.h[b] * f.adq[A])) - (b > A ? 1.0 : 0.0);
-    double q = floor(X * f.inv[A]);
-    const double rm = fma(-q, Y, X);
-    q += rm < 0.0 ? -1.0 : (rm >= Y ? 1.0 : 0.0);
-    const int32_t cq = (int32_t)q + 1;
-    const bool none = b > A ? X < 0.0 : X < 0.0;  // X (biased for b > A) < 0: no crossing yet
-    c[b] = (r.st[b] == 0 || none) ? 0 : (cq < r.n[b] ? cq : r.n[b]);
-  }
-}
-#endif
 
 template <bool SLAB>
 __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose, int wg_pose, int span, BkGeom bg,
@@ -988,13 +964,8 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
       return R.st[ax] > 0 ? (nb << bk::kLog) - R.cs[ax] - 1 : R.cs[ax] - (nb << bk::kLog) - bk::kB;
     };
 #if defined(DMF_EXP_B_F64)
-    BF64 fd;
-#pragma unroll
-    for (int ax = 0; ax < 3; ++ax) {
-      fd.adq[ax] = (double)R.adq[ax];
-      fd.h[ax] = (double)R.h0[ax];
-      fd.inv[ax] = R.adq[ax] ? 1.0 / (double)(2 * bk::kQ * R.adq[ax]) : 0.0;
-    }
+    bk::QRayF64 fd;
+    bk::qray_f64(R, fd);
 #endif
     const int32_t c00[3] = {0, 0, 0};
     uint4 cur = entry(c00);
@@ -1007,24 +978,88 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
       const int32_t cin[3] = {ci0, ci1, ci2}, cL[3] = {L0, L1, L2};
       return bk::slab_rcode(M, sb1, sb2, KM, Km1, Km2, cin, cL);
     };
+    // crossing counts per axis at the boundary event of axis a into brick coordinate (bx, by, bz)
+    auto counts = [&](int a, int bx, int by, int bz, int32_t c[3]) {
+#if defined(DMF_EXP_B_F64)  // experiment: boundary counts in double arithmetic (counts_at_f64)
+      if (a == 0) bk::counts_at_f64<0>(R, fd, boundary_k(0, bx), c);
+      else if (a == 1) bk::counts_at_f64<1>(R, fd, boundary_k(1, by), c);
+      else bk::counts_at_f64<2>(R, fd, boundary_k(2, bz), c);
+#elif defined(DMF_DIAG_B_NOCOUNT)  // diagnostic build (wrong results): no boundary counts
+      c[0] = bx + (a == 0);
+      c[1] = by + (a == 1);
+      c[2] = bz + (a == 2);
+#else
+      // constant axis in each call: no dynamically indexed (scratch) arrays
+      if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
+      else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
+      else bk::counts_at(R, 2, boundary_k(2, bz), c);
+#endif
+    };
+#if defined(DMF_EXP_B_DEFER)
+    // experiment: an explicit wave-uniform boundary loop (iteration t = boundary t for the live
+    // lanes, t < total; the final put at t == total).  The lanes active at iteration t + 1 are
+    // exactly those live at t, so a slot taken at t by ONE LDS atomic for every live lane (all
+    // naming the same brick: the common case for a packet's parallel rays) is resolved one
+    // iteration later by a readlane of the leader's return -- no 64-way same-address atomic,
+    // and the atomic's latency still hides behind a boundary's work.  Lanes in different
+    // bricks take per-lane atomics as before.
+    {
+      int bx = R.cs[0] >> bk::kLog, by = R.cs[1] >> bk::kLog, bz = R.cs[2] >> bk::kLog;
+      bk::Coarse cw;
+      bk::coarse_init(R, cw);
+      const int total = cw.total;
+      uint32_t pold = 0, poff = 0;
+      int plead = 0;
+      bool puni = false;
+      auto take = [&](int b) {  // exec = the live lanes
+        const uint64_t act = __builtin_amdgcn_ballot_w64(true);
+        const int b0 = __builtin_amdgcn_readfirstlane(b);
+        puni = __builtin_amdgcn_ballot_w64(b == b0) == act;
+        if (puni) {
+          plead = __builtin_ctzll(act);
+          poff = (uint32_t)lane_prefix(act);
+          pold = 0;
+          if (l == plead) pold = atomicAdd(&hist[b0], (uint32_t)__builtin_popcountll(act));
+        } else {
+          pold = atomicAdd(&hist[b], 1u);
+        }
+      };
+      auto resolve = [&]() -> uint32_t {  // exec = the lanes live at the previous iteration
+        if (puni) return (uint32_t)__builtin_amdgcn_readlane((int)pold, __builtin_amdgcn_readfirstlane(plead)) + poff;
+        return pold;
+      };
+      take(bk_index(bg, bx, by, bz));
+      for (int t = 0;; ++t) {
+        const bool live = t < total, fin = t == total;
+        if (__builtin_amdgcn_ballot_w64(live || fin) == 0) break;
+        if (!(live || fin)) continue;
+        if (live) {
+          const int a = bk::coarse_next(cw);
+          bx += a == 0 ? R.st[0] : 0;
+          by += a == 1 ? R.st[1] : 0;
+          bz += a == 2 ? R.st[2] : 0;
+          int32_t c[3];
+          counts(a, bx, by, bz, c);
+          const uint32_t slot = resolve();
+          put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
+          cur = entry(c);
+          idx = c[0] + c[1] + c[2];
+          ci0 = c[0];
+          ci1 = c[1];
+          ci2 = c[2];
+          take(bk_index(bg, bx, by, bz));
+        } else {
+          put(resolve(), cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
+        }
+      }
+      continue;
+    }
+#endif
     uint32_t slot = 0;
     bk_coarse(bg, R, [&](int b, int a, int bx, int by, int bz) {
       if (a >= 0) {
         int32_t c[3];
-#if defined(DMF_EXP_B_F64)  // experiment: boundary counts in double arithmetic (count_at_f64)
-        if (a == 0) counts_f64<0>(R, fd, boundary_k(0, bx), c);
-        else if (a == 1) counts_f64<1>(R, fd, boundary_k(1, by), c);
-        else counts_f64<2>(R, fd, boundary_k(2, bz), c);
-#elif defined(DMF_DIAG_B_NOCOUNT)  // diagnostic build (wrong results): no boundary counts
-        c[0] = bx + (a == 0);
-        c[1] = by + (a == 1);
-        c[2] = bz + (a == 2);
-#else
-        // constant axis in each call: no dynamically indexed (scratch) arrays
-        if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
-        else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
-        else bk::counts_at(R, 2, boundary_k(2, bz), c);
-#endif
+        counts(a, bx, by, bz, c);
         put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
         cur = entry(c);
         idx = c[0] + c[1] + c[2];
