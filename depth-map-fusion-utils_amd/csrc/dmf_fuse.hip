@@ -28,6 +28,16 @@ namespace dmf {
 constexpr int64_t kQ = 256;  // fixed-point sub-cell resolution (1/256 cell)
 
 __device__ inline int64_t clampi(int64_t v, int64_t lo, int64_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ inline int32_t clamp32(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// (int64_t) floor(x) as the oracle's x86 conversion gives it (cvttsd2si: NaN and |x| >= 2^63
+// -> INT64_MIN), saturated to +-2^30: a v_cvt_i32_f64 and a select instead of the int64
+// conversion sequence.  Every use clamps the result into [0, n * kQ) with n * kQ <= 2^19
+// (fusion grids <= 2048 cells per axis, check_fuse), so the clamped values are identical.
+__device__ inline int32_t floor_sat32(double x) {
+  const double f = floor(x);
+  return fabs(f) < 9223372036854775808.0 ? (int32_t)fmin(fmax(f, -1073741824.0), 1073741824.0) : -(1 << 30);
+}
 
 __device__ inline void atomic_add_dev(int32_t* p, int32_t v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -137,10 +147,11 @@ __device__ inline bool dda_quantize_go(const Geom& g, const double go[3], const 
   for (int a = 0; a < 3; ++a) {
     const double gs = go[a] + t0 * D[a];
     const double gx = end_inside ? ge[a] : go[a] + t1 * D[a];
-    const int64_t cs = clampi((int64_t)floor(gs), 0, g.n[a] - 1);
-    const int64_t ce = end_inside ? (int64_t)floor(ge[a]) : clampi((int64_t)floor(gx), 0, g.n[a] - 1);
-    qs[a] = clampi((int64_t)floor(gs * (double)kQ), cs * kQ, cs * kQ + kQ - 1);
-    qe[a] = clampi((int64_t)floor(gx * (double)kQ), ce * kQ, ce * kQ + kQ - 1);
+    const int32_t n = (int32_t)g.n[a], Q = (int32_t)kQ;
+    const int32_t cs = clamp32(floor_sat32(gs), 0, n - 1);
+    const int32_t ce = end_inside ? floor_sat32(ge[a]) : clamp32(floor_sat32(gx), 0, n - 1);
+    qs[a] = clamp32(floor_sat32(gs * (double)kQ), cs * Q, cs * Q + Q - 1);
+    qe[a] = clamp32(floor_sat32(gx * (double)kQ), ce * Q, ce * Q + Q - 1);
   }
   return true;
 }

@@ -684,12 +684,18 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
     // distance field, items in spatial order for reverseRayTraceFast), 1 = lane per (voxel,
     // pose), 2 = the same with brick skipping, 3 = the work queue in occupied_cells_ order
     const int64_t kr = v->knob[DMF_KNOB_REVERSE_KERNEL];
-#if defined(DMF_EXP_REV_ITEMS)  // experiment builds: work-queue shape
-    constexpr int kRevItems = DMF_EXP_REV_ITEMS, kRevRefill = DMF_EXP_REV_REFILL, kRevBurst = DMF_EXP_REV_BURST;
-#else
+    // work-queue shape (items per wave, refill threshold, burst): 512 / 8 / 8 in enumeration
+    // or insertion order; in spatial order smaller queues pay (neighbouring lanes agree, so
+    // the per-wave tail is the cost): 128 / 8 / 16 measured 5.92 ms vs 6.51 at 512 / 8 / 8
+    // (profiles/r04/reverse_queue_sweep.json)
     constexpr int kRevItems = 512, kRevRefill = 8, kRevBurst = 8;
+#if defined(DMF_EXP_REV_ITEMS)  // experiment builds: the spatial-order queue's shape
+    constexpr int kSpItems = DMF_EXP_REV_ITEMS, kSpRefill = DMF_EXP_REV_REFILL, kSpBurst = DMF_EXP_REV_BURST;
+#else
+    constexpr int kSpItems = 128, kSpRefill = 8, kSpBurst = 16;
 #endif
     const dim3 gridq((unsigned)((nelem + 4 * kRevItems - 1) / (4 * kRevItems)), (unsigned)P);
+    const dim3 gridqs((unsigned)((nelem + 4 * kSpItems - 1) / (4 * kSpItems)), (unsigned)P);
     const Geom g = v->geom();
     const DevVol dv = v->dev();
     const CamP cp = cam_params(cam);
@@ -722,7 +728,7 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
         DMF_TRY(scratch(v, kScRevItems, sizeof(uint64_t) * (size_t)(2 * P * words), &items));
         uint64_t* vis_i = (uint64_t*)items;
         uint64_t* good_i = vis_i + P * words;
-        hipLaunchKernelGGL((k_reverse_q<false, kRevItems, kRevRefill, kRevBurst, true>), gridq, dim3(256), 0, v->stream, g, dv, cp, tab,
+        hipLaunchKernelGGL((k_reverse_q<false, kSpItems, kSpRefill, kSpBurst, true>), gridqs, dim3(256), 0, v->stream, g, dv, cp, tab,
                            nelem, el, (const uint32_t*)v->d_sorder, depth0, ms, v->dstar, viz, 1, vis_i, good_i, words,
                            st, found, hz);
         DMF_LAUNCH_CHECK();

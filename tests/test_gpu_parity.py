@@ -803,6 +803,16 @@ def _edge_fusion_cases():
               ("ends_before_grid", Ka, 48, 64, axis, bounds),
               ("no_valid_pixel", Ka, 48, 64, axis, np.zeros((3, 48, 64), np.uint16)),
               ("misses_grid", Ka, 48, 64, pose(np.eye(3), [0.0, 0.0, 0.9])[None], plane[:1])]
+    # non-finite and far poses: a NaN rotation (finite origin, NaN endpoints: the clip keeps
+    # t0 = 0, t1 = 1 and the NaN end cell converts to the low clamp, as the oracle's x86
+    # int64 conversion gives it), NaN / inf translations, a translation of 1e20 (nothing
+    # reaches the grid)
+    bad = np.stack([axis[0], axis[1], axis[2], axis[0]]).copy()
+    bad[0, 0] = np.nan
+    bad[1, 3] = np.nan
+    bad[2, 7] = np.inf
+    bad[3, 11] = np.float32(-1e20)
+    cases.append(("nonfinite_poses", Ka, 48, 64, bad, np.concatenate([plane, plane[:1]])))
     return cases
 
 

@@ -28,6 +28,7 @@ ap.add_argument("--image", default="640x480")
 ap.add_argument("--calls", type=int, default=30)
 ap.add_argument("--modes", default="serial,pipelined")
 ap.add_argument("--tag", default=os.environ.get("DMF_LIB", "product"))
+ap.add_argument("--knob", action="append", default=[], help="name=value (dmf_diag.h knob), repeatable")
 a = ap.parse_args()
 W, H = (int(x) for x in a.image.split("x"))
 dev = torch.device("cuda", 0)
@@ -48,6 +49,9 @@ vol.set_stream(main.cuda_stream)
 vol.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
 vol.setVolumeSize(a.grid, a.grid, a.grid)
 vol.constructVolume()
+for kv in a.knob:
+    k, val = kv.split("=")
+    _lib.set_knob(vol, k, int(val))
 cam = _lib.make_camera(K, H, W)
 prm = _lib.default_fuse_params(dmin_mm=scene.DEPTH_MIN_MM, dmax_mm=scene.DEPTH_MAX_MM)
 nct = C.c_int64()
@@ -65,7 +69,7 @@ def call():
                                        C.addressof(prm), cnt.data_ptr(), cnt.data_ptr() + 4 * nt, st.data_ptr()))
 
 
-out = {"tag": a.tag, "grid": a.grid, "poses": P, "image": a.image, "kernel": None}
+out = {"tag": a.tag, "knobs": a.knob, "grid": a.grid, "poses": P, "image": a.image, "kernel": None}
 torch.cuda.synchronize(dev)
 for mode in a.modes.split(","):
     print(f"[exp_fuse {a.tag}] mode {mode}", file=sys.stderr, flush=True)
@@ -77,14 +81,14 @@ for mode in a.modes.split(","):
     with torch.cuda.stream(main):
         call()
     torch.cuda.synchronize(dev)
-    if mode == a.modes.split(",")[0]:
-        lo = torch.empty(a.grid ** 3, dtype=torch.int16, device=dev)
-        _lib.check(L.dmf_fuse_finalize_device(vol._h, cnt.data_ptr(), cnt.data_ptr() + 4 * nt, C.addressof(prm),
-                                              lo.data_ptr()))
-        torch.cuda.synchronize(dev)
-        out["digest"] = hashlib.sha256(lo.cpu().numpy().tobytes()).hexdigest()[:16]
-        out["updates"] = int(st[0].item())
-        out["pairs"] = int(st[4].item())
+    # the digest of every mode (== tests/golden when exact)
+    lo = torch.empty(a.grid ** 3, dtype=torch.int16, device=dev)
+    _lib.check(L.dmf_fuse_finalize_device(vol._h, cnt.data_ptr(), cnt.data_ptr() + 4 * nt, C.addressof(prm),
+                                          lo.data_ptr()))
+    torch.cuda.synchronize(dev)
+    out[mode + "_digest"] = out["digest"] = hashlib.sha256(lo.cpu().numpy().tobytes()).hexdigest()[:16]
+    out["updates"] = int(st[0].item())
+    out["pairs"] = int(st[4].item())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
         call()
