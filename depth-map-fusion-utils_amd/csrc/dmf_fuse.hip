@@ -1841,10 +1841,10 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       DMF_TRY(pose_table_into(d_poses + (size_t)s0 * 12, (int)ps, (PoseX*)t, sa));
       tab_a = (const PoseX*)t;
       if (st) {
-        void* sb;
-        DMF_TRY(scratch(v, slot ? kScStStats1 : kScStStats0, sizeof(unsigned long long) * kStatSlots * kStatWidth, &sb));
-        DMF_HIP(hipMemsetAsync(sb, 0, sizeof(unsigned long long) * kStatSlots * kStatWidth, sa));
-        st_a = (unsigned long long*)sb;
+        void* sbuf;
+        DMF_TRY(scratch(v, slot ? kScStStats1 : kScStStats0, sizeof(unsigned long long) * kStatSlots * kStatWidth, &sbuf));
+        DMF_HIP(hipMemsetAsync(sbuf, 0, sizeof(unsigned long long) * kStatSlots * kStatWidth, sa));
+        st_a = (unsigned long long*)sbuf;
       }
     }
     DMF_HIP(hipMemsetAsync(b.pose_cnt, 0, pl.hist_bytes * (size_t)ps, sa));
