@@ -62,11 +62,9 @@ __host__ __device__ inline void pack_ray(const int64_t qs[3], const int64_t qe[3
   B = (uint64_t)qe[0] | ((uint64_t)qe[1] << 19) | ((uint64_t)qe[2] << 38) | ((uint64_t)1 << 63);
 }
 
-__host__ __device__ inline void decode_ray(uint64_t A, uint64_t B, QRay& r) {
-  constexpr uint64_t m = (1u << 19) - 1;
-  const int32_t qs[3] = {(int32_t)(A & m), (int32_t)((A >> 19) & m), (int32_t)((A >> 38) & m)};
-  const int32_t qe[3] = {(int32_t)(B & m), (int32_t)((B >> 19) & m), (int32_t)((B >> 38) & m)};
-  r.end_inside = (A >> 63) != 0;
+// The QRay of quantised endpoints qs, qe (what decode_ray gives for their record).
+__host__ __device__ inline void qray_from(const int32_t qs[3], const int32_t qe[3], bool end_inside, QRay& r) {
+  r.end_inside = end_inside;
   r.nsteps = 0;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
@@ -82,6 +80,13 @@ __host__ __device__ inline void decode_ray(uint64_t A, uint64_t B, QRay& r) {
   }
 }
 
+__host__ __device__ inline void decode_ray(uint64_t A, uint64_t B, QRay& r) {
+  constexpr uint64_t m = (1u << 19) - 1;
+  const int32_t qs[3] = {(int32_t)(A & m), (int32_t)((A >> 19) & m), (int32_t)((A >> 38) & m)};
+  const int32_t qe[3] = {(int32_t)(B & m), (int32_t)((B >> 19) & m), (int32_t)((B >> 38) & m)};
+  qray_from(qs, qe, (A >> 63) != 0, r);
+}
+
 // Fine-walk E of the pair (a, b) at the ray start (dmf_fuse.hip dda_setup).
 __host__ __device__ inline int32_t e0_pair(const QRay& r, int a, int b) {
   if (r.st[a] && r.st[b]) return (int32_t)((int64_t)r.h0[a] * r.adq[b] - (int64_t)r.h0[b] * r.adq[a]);
@@ -94,62 +99,44 @@ __host__ __device__ inline bool ev_before(const QRay& r, int a, int64_t Ha, int 
   return L < R || (L == R && a < b);
 }
 
-// floor(X / Y) for 0 <= X < 2^41, 0 < Y < 2^29 with a small quotient: count_at's quotient
+// floor(X / Y) for 0 <= X < 2^41, 0 < Y < 2^28 with a small quotient: count_at's quotient
 // counts b-crossings up to a crossing event of the same ray, so it is <= n_b + 1 <= 2^11.
 // Float estimate (relative error < 2^-21, so within 1 of the floor) and one exact
-// correction in either direction.
-__host__ __device__ inline int64_t small_quot(int64_t X, int64_t Y) {
-  const float xf = (float)(int32_t)(X >> 20) * 1048576.0f + (float)(int32_t)(X & 0xfffff);
-  const float yf = (float)(int32_t)Y;
-#if defined(__HIP_DEVICE_COMPILE__)
-  int32_t q = (int32_t)(xf * __builtin_amdgcn_rcpf(yf));  // v_rcp_f32: 1 ulp
-#else
-  int32_t q = (int32_t)(xf / yf);
-#endif
-  const int64_t rm = X - (int64_t)q * Y;
-  q += rm < 0 ? -1 : (rm >= Y ? 1 : 0);
-  return q;
-}
-
-// Number of b-crossings taken at or before the event (a, Ha) (a's own crossings are
-// the caller's: k + 1).  b != a.
-__host__ __device__ inline int32_t count_at(const QRay& r, int b, int a, int64_t Ha) {
-  if (r.st[b] == 0) return 0;
-  const int64_t X = Ha * (int64_t)r.adq[b] - (int64_t)r.h0[b] * r.adq[a];
-  const int64_t Y = 2 * kQ * (int64_t)r.adq[a];
-  int64_t c;
-  if (b < a) c = X < 0 ? 0 : small_quot(X, Y) + 1;
-  else c = X <= 0 ? 0 : small_quot(X - 1, Y) + 1;
-  return c < r.n[b] ? (int32_t)c : r.n[b];
-}
-
-// Crossing counts per axis at (and including) event (a, k); a < 0 = the ray start.
-__host__ __device__ inline void counts_at(const QRay& r, int a, int32_t k, int32_t c[3]) {
-  if (a < 0) { c[0] = c[1] = c[2] = 0; return; }
-  const int64_t Ha = (int64_t)r.h0[a] + 2 * kQ * (int64_t)k;
-#pragma unroll
-  for (int b = 0; b < 3; ++b) c[b] = (b == a) ? k + 1 : count_at(r, b, a, Ha);
-}
-
-// counts_at for an axis a that differs between the lanes of a wave (pass B's boundary
-// events): one straight code path of selects.  counts_at's constant-axis branches run
-// once per distinct axis among a wave's lanes; here the two other axes (ascending:
-// o1 = a == 0 ? 1 : 0, o2 = a == 2 ? 1 : 2) are picked and counted by the same code, with
-// count_at's tie rule as a bias (b > a: X - 1).  The quotient's remainder is taken in 32
-// bits: with q within 1 of floor(X / Y) it lies in (-Y, 2Y), |.| < 2^28 (Y = 2Q|dq_a| <
-// 2^27), so the wrapped difference of the low words is exact.  A non-moving axis (n = 0)
-// is clamped to 0 whatever its quotient.  Checked against counts_at by the brick self-test.
+// correction in either direction.  The remainder is taken in 32 bits: with q within 1 of
+// floor(X / Y) it lies in (-Y, 2Y), |.| < 2^29, so the wrapped difference of the low words
+// is exact.
 __host__ __device__ inline int32_t quot_small32(int64_t X, int32_t Y) {
   const float xf = (float)(int32_t)(X >> 20) * 1048576.0f + (float)(int32_t)(X & 0xfffff);
   const float yf = (float)Y;
 #if defined(__HIP_DEVICE_COMPILE__)
-  int32_t q = (int32_t)(xf * __builtin_amdgcn_rcpf(yf));
+  int32_t q = (int32_t)(xf * __builtin_amdgcn_rcpf(yf));  // v_rcp_f32: 1 ulp
 #else
   int32_t q = (int32_t)(xf / yf);
 #endif
   const int32_t rm = (int32_t)((uint32_t)X - (uint32_t)q * (uint32_t)Y);
   q += rm < 0 ? -1 : (rm >= Y ? 1 : 0);
   return q;
+}
+
+// Number of b-crossings taken at or before the event (a, Ha) (a's own crossings are
+// the caller's: k + 1).  b != a.  Ha = h0_a + 2Qk < 2^21 and |dq| < 2^19 (grids <= 2048
+// cells per axis): X is a difference of two 32x32-bit products, Y = 2Q|dq_a| < 2^28.
+__host__ __device__ inline int32_t count_at(const QRay& r, int b, int a, int32_t Ha) {
+  if (r.st[b] == 0) return 0;
+  const int64_t X = (int64_t)Ha * (int64_t)r.adq[b] - (int64_t)r.h0[b] * (int64_t)r.adq[a];
+  const int32_t Y = (int32_t)(2 * kQ) * r.adq[a];
+  int32_t c;
+  if (b < a) c = X < 0 ? 0 : quot_small32(X, Y) + 1;
+  else c = X <= 0 ? 0 : quot_small32(X - 1, Y) + 1;
+  return c < r.n[b] ? c : r.n[b];
+}
+
+// Crossing counts per axis at (and including) event (a, k); a < 0 = the ray start.
+__host__ __device__ inline void counts_at(const QRay& r, int a, int32_t k, int32_t c[3]) {
+  if (a < 0) { c[0] = c[1] = c[2] = 0; return; }
+  const int32_t Ha = r.h0[a] + (int32_t)(2 * kQ) * k;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) c[b] = (b == a) ? k + 1 : count_at(r, b, a, Ha);
 }
 
 // The value of x, opaque to the optimiser: a select between struct fields must stay a
@@ -165,6 +152,15 @@ __host__ __device__ inline int32_t sel3(bool a0, bool a1, int32_t v0, int32_t v1
   return a0 ? opaque(v0) : (a1 ? opaque(v1) : opaque(v2));
 }
 
+// counts_at for an axis a that differs between the lanes of a wave (pass B's boundary
+// events): one straight code path of selects.  counts_at's constant-axis branches run
+// once per distinct axis among a wave's lanes; here the two other axes (ascending:
+// o1 = a == 0 ? 1 : 0, o2 = a == 2 ? 1 : 2) are picked and counted by the same code, with
+// count_at's tie rule as a bias (b > a: X - 1).  The quotient's remainder is taken in 32
+// bits: with q within 1 of floor(X / Y) it lies in (-Y, 2Y), |.| < 2^28 (Y = 2Q|dq_a| <
+// 2^27), so the wrapped difference of the low words is exact (quot_small32).  A non-moving
+// axis (n = 0) is clamped to 0 whatever its quotient.  Checked against counts_at by the brick
+// self-test.
 __host__ __device__ inline void counts_at_sel(const QRay& r, int a, int32_t k, int32_t c[3]) {
   const bool a0 = a == 0, a1 = a == 1, a2 = a == 2;
   const int32_t ha = sel3(a0, a1, r.h0[0], r.h0[1], r.h0[2]);
@@ -276,17 +272,17 @@ struct Coarse {
 };
 
 __host__ __device__ inline void coarse_init(const QRay& r, Coarse& w) {
-  int64_t H[3];
+  int32_t H[3];  // < 2Q (kB + 1): 32x32-bit products below
   w.total = 0;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const int32_t off = r.cs[a] & (kB - 1);
     const int32_t k0 = r.st[a] > 0 ? kB - 1 - off : off;  // first boundary crossing
-    H[a] = (int64_t)r.h0[a] + 2 * kQ * (int64_t)k0;
+    H[a] = r.h0[a] + (int32_t)(2 * kQ) * k0;
     if (r.st[a] != 0 && r.n[a] > k0) w.total += (r.n[a] - 1 - k0) / kB + 1;
   }
   auto pr = [&](int a, int b) -> int64_t {
-    if (r.st[a] && r.st[b]) return H[a] * (int64_t)r.adq[b] - H[b] * (int64_t)r.adq[a];
+    if (r.st[a] && r.st[b]) return (int64_t)H[a] * (int64_t)r.adq[b] - (int64_t)H[b] * (int64_t)r.adq[a];
     return r.st[a] ? -kNever64 : (r.st[b] ? kNever64 : 0);
   };
   w.E01 = pr(0, 1);

@@ -618,7 +618,9 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
       rec.x = A;
       rec.y = B;
       bk::QRay R;
-      bk::decode_ray(A, B, R);
+      const int32_t qs32[3] = {(int32_t)qs[0], (int32_t)qs[1], (int32_t)qs[2]},
+                    qe32[3] = {(int32_t)qe[0], (int32_t)qe[1], (int32_t)qe[2]};
+      bk::qray_from(qs32, qe32, inside, R);  // = decode_ray(A, B), without the round trip
       upd += (unsigned long long)(R.nsteps + 1);
       nhit += inside ? 1 : 0;
       bk_coarse(bg, R, [&](int b, int, int, int, int) { hist_add_agg<H16>(hist, b); });
