@@ -271,15 +271,26 @@ struct Coarse {
   int32_t total;                      // boundary crossings of the whole ray
 };
 
+// Brick boundaries the ray crosses (the coarse walk's step count).
+__host__ __device__ inline int32_t coarse_total(const QRay& r) {
+  int32_t total = 0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int32_t off = r.cs[a] & (kB - 1);
+    const int32_t k0 = r.st[a] > 0 ? kB - 1 - off : off;  // first boundary crossing
+    if (r.st[a] != 0 && r.n[a] > k0) total += (r.n[a] - 1 - k0) / kB + 1;
+  }
+  return total;
+}
+
 __host__ __device__ inline void coarse_init(const QRay& r, Coarse& w) {
   int32_t H[3];  // < 2Q (kB + 1): 32x32-bit products below
-  w.total = 0;
+  w.total = coarse_total(r);
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const int32_t off = r.cs[a] & (kB - 1);
     const int32_t k0 = r.st[a] > 0 ? kB - 1 - off : off;  // first boundary crossing
     H[a] = r.h0[a] + (int32_t)(2 * kQ) * k0;
-    if (r.st[a] != 0 && r.n[a] > k0) w.total += (r.n[a] - 1 - k0) / kB + 1;
   }
   auto pr = [&](int a, int b) -> int64_t {
     if (r.st[a] && r.st[b]) return (int64_t)H[a] * (int64_t)r.adq[b] - (int64_t)H[b] * (int64_t)r.adq[a];
@@ -303,6 +314,15 @@ __host__ __device__ inline int coarse_next(Coarse& w) {
   w.E12 += s1 ? w.K2 : (s2 ? -w.K1 : 0);
   return s2 ? 2 : (s1 ? 1 : 0);
 }
+
+// The coarse walk's crossing axes, 2 bits per brick boundary (step t at bits 2t, 2t + 1), for
+// the first kPathSteps boundaries: pass A records them with its walk so that pass B replays
+// the brick sequence without the 64-bit comparisons (a ray with more boundaries walks again).
+constexpr int kPathSteps = 32;
+__host__ __device__ inline uint64_t path_put(uint64_t path, int t, int a) {
+  return t < kPathSteps ? path | (uint64_t)a << (2 * t) : path;
+}
+__host__ __device__ inline int path_axis(uint64_t path, int t) { return (int)(path >> (2 * t)) & 3; }
 
 // ---- Major-axis ("slab") form of the fine walk (phase F) ----
 //

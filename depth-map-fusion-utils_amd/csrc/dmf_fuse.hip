@@ -544,6 +544,28 @@ __device__ inline void bk_coarse(const BkGeom& bg, const bk::QRay& R, F&& f) {
   }
 }
 
+// Pass B's coarse walk: the brick sequence from the crossing axes pass A recorded (path, see
+// dmf_brick.hpp path_put), calling f exactly as bk_coarse does; a ray with more than
+// kPathSteps boundaries walks them again.
+template <class F>
+__device__ inline void bk_replay(const BkGeom& bg, const bk::QRay& R, uint64_t path, F&& f) {
+  const int total = bk::coarse_total(R);
+  const bool walk = total > bk::kPathSteps;
+  bk::Coarse cw;
+  if (walk) bk::coarse_init(R, cw);
+  int b0 = R.cs[0] >> bk::kLog, b1 = R.cs[1] >> bk::kLog, b2 = R.cs[2] >> bk::kLog;
+  f(bk_index(bg, b0, b1, b2), -1, b0, b1, b2);
+  for (int t = 0; t < total; ++t) {
+    int a;
+    if (walk) a = bk::coarse_next(cw);  // (branch: skipped by the waves whose lanes all replay)
+    else a = bk::path_axis(path, t);
+    b0 += a == 0 ? R.st[0] : 0;
+    b1 += a == 1 ? R.st[1] : 0;
+    b2 += a == 2 ? R.st[2] : 0;
+    f(bk_index(bg, b0, b1, b2), a, b0, b1, b2);
+  }
+}
+
 // Wave-aggregated LDS histogram add: the lanes of a packet walk near-parallel rays and
 // name the same brick at the same coarse step, so one atomic per distinct brick among
 // the active lanes replaces a same-address atomic per lane (which the LDS serialises).
@@ -579,6 +601,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
                                                         const PoseX* __restrict__ poses, int dmin, int dmax,
                                                         int packets_x, int packets_pose, int wg_pose, int span,
                                                         BkGeom bg, ulonglong2* __restrict__ rays,
+                                                        uint64_t* __restrict__ paths,
                                                         uint32_t* __restrict__ pose_cnt,
                                                         uint32_t* __restrict__ wg_base,
                                                         uint32_t* __restrict__ wg_list, int wgl_stride,
@@ -612,6 +635,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
     ulonglong2 rec;
     rec.x = 0;
     rec.y = 0;
+    uint64_t path = 0;  // the crossing axes of the coarse walk (pass B replays them)
     if (pixel_quant_go(g, cam, d, poses[p], go, r, c, dmin, dmax, qs, qe, inside, valid)) {
       uint64_t A, B;
       bk::pack_ray(qs, qe, inside, A, B);
@@ -623,10 +647,15 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
       bk::qray_from(qs32, qe32, inside, R);  // = decode_ray(A, B), without the round trip
       upd += (unsigned long long)(R.nsteps + 1);
       nhit += inside ? 1 : 0;
-      bk_coarse(bg, R, [&](int b, int, int, int, int) { hist_add_agg<H16>(hist, b); });
+      int t = 0;
+      bk_coarse(bg, R, [&](int b, int a, int, int, int) {
+        hist_add_agg<H16>(hist, b);
+        if (a >= 0) path = bk::path_put(path, t++, a);
+      });
     }
     nvalid += valid ? 1 : 0;
     rays[pk * 64 + l] = rec;
+    paths[pk * 64 + l] = path;
   }
   __syncthreads();
   uint32_t* const pc = pose_cnt + (size_t)pw * bg.nbricks;
@@ -851,6 +880,7 @@ __device__ inline uint32_t bk_e30(int32_t e) {
 template <bool SLAB>
 __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose, int wg_pose, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
+                                                         const uint64_t* __restrict__ paths,
                                                          const uint32_t* __restrict__ off,
                                                          const uint32_t* __restrict__ pose_base,
                                                          const uint32_t* __restrict__ wg_base,
@@ -884,24 +914,19 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
   constexpr uint32_t m5 = bk::kB - 1;
   // the next packet's ray record is loaded one packet ahead: its HBM latency hides behind
   // this packet's coarse walk (B 2.03 -> 1.92 ms) instead of stalling the wave per packet
-#if defined(DMF_EXP_B_STRIDE)
-  // experiment: lane l of virtual packet v takes pixel l of packet (v + l) mod npk of the
-  // workgroup's span, so that a wave's lanes walk rays up to a span apart (different bricks:
-  // fewer same-address slot atomics) instead of one 8x8 packet's neighbouring rays
-  const int npk = (int)(pk1 - pk0);
-  auto ray_at = [&](int vp) { return rays[(pk0 + (int64_t)((vp + l) % npk)) * 64 + l]; };
   ulonglong2 rnext = make_ulonglong2(0, 0);
-  if (w < npk) rnext = ray_at(w);
-  for (int vp = w; vp < npk; vp += nw) {
-    const ulonglong2 rec = rnext;
-    if (vp + nw < npk) rnext = ray_at(vp + nw);
-#else
-  ulonglong2 rnext = make_ulonglong2(0, 0);
-  if (pk0 + w < pk1) rnext = rays[(pk0 + w) * 64 + l];
+  uint64_t pnext = 0;
+  if (pk0 + w < pk1) {
+    rnext = rays[(pk0 + w) * 64 + l];
+    pnext = paths[(pk0 + w) * 64 + l];
+  }
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
     const ulonglong2 rec = rnext;
-    if (pk + nw < pk1) rnext = rays[(pk + nw) * 64 + l];
-#endif
+    const uint64_t path = pnext;
+    if (pk + nw < pk1) {
+      rnext = rays[(pk + nw) * 64 + l];
+      pnext = paths[(pk + nw) * 64 + l];
+    }
     if ((rec.y >> 63) == 0) continue;  // no ray
     bk::QRay R;
     bk::decode_ray(rec.x, rec.y, R);
@@ -952,12 +977,8 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
         uint32_t w[5];
         bk::pack20((int32_t)e.x, (int32_t)e.y, (int32_t)e.z, aM, a1, a2, e.w, last, steps, signs >> 22, (uint32_t)M,
                    ends, w);
-#if defined(DMF_DIAG_B_NOSTORE)  // diagnostic build (wrong results): no record stores
-        if ((w[0] ^ w[1] ^ w[2] ^ w[3] ^ w[4] ^ slot) == 0x9e3779b9u) pw[0] = 0;  // keep the record live
-#else
         pa[slot] = make_uint4(w[0], w[1], w[2], w[3]);
         pw[slot] = w[4];
-#endif
       } else {
         e.x = bk_e30((int32_t)e.x) | (steps & 3u) << 30;
         e.y = bk_e30((int32_t)e.y) | ((steps >> 2) & 3u) << 30;
@@ -976,10 +997,6 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
     auto boundary_k = [&](int ax, int nb) {
       return R.st[ax] > 0 ? (nb << bk::kLog) - R.cs[ax] - 1 : R.cs[ax] - (nb << bk::kLog) - bk::kB;
     };
-#if defined(DMF_EXP_B_F64)
-    bk::QRayF64 fd;
-    bk::qray_f64(R, fd);
-#endif
     const int32_t c00[3] = {0, 0, 0};
     uint4 cur = entry(c00);
     int32_t idx = 0;                    // crossings before the current pair's first cell
@@ -993,83 +1010,13 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
     };
     // crossing counts per axis at the boundary event of axis a into brick coordinate (bx, by, bz)
     auto counts = [&](int a, int bx, int by, int bz, int32_t c[3]) {
-#if defined(DMF_EXP_B_F64)  // experiment: boundary counts in double arithmetic (counts_at_f64)
-      if (a == 0) bk::counts_at_f64<0>(R, fd, boundary_k(0, bx), c);
-      else if (a == 1) bk::counts_at_f64<1>(R, fd, boundary_k(1, by), c);
-      else bk::counts_at_f64<2>(R, fd, boundary_k(2, bz), c);
-#elif defined(DMF_DIAG_B_NOCOUNT)  // diagnostic build (wrong results): no boundary counts
-      c[0] = bx + (a == 0);
-      c[1] = by + (a == 1);
-      c[2] = bz + (a == 2);
-#else
       // constant axis in each call: no dynamically indexed (scratch) arrays
       if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
       else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
       else bk::counts_at(R, 2, boundary_k(2, bz), c);
-#endif
     };
-#if defined(DMF_EXP_B_DEFER)
-    // experiment: an explicit wave-uniform boundary loop (iteration t = boundary t for the live
-    // lanes, t < total; the final put at t == total).  The lanes active at iteration t + 1 are
-    // exactly those live at t, so a slot taken at t by ONE LDS atomic for every live lane (all
-    // naming the same brick: the common case for a packet's parallel rays) is resolved one
-    // iteration later by a readlane of the leader's return -- no 64-way same-address atomic,
-    // and the atomic's latency still hides behind a boundary's work.  Lanes in different
-    // bricks take per-lane atomics as before.
-    {
-      int bx = R.cs[0] >> bk::kLog, by = R.cs[1] >> bk::kLog, bz = R.cs[2] >> bk::kLog;
-      bk::Coarse cw;
-      bk::coarse_init(R, cw);
-      const int total = cw.total;
-      uint32_t pold = 0, poff = 0;
-      int plead = 0;
-      bool puni = false;
-      auto take = [&](int b) {  // exec = the live lanes
-        const uint64_t act = __builtin_amdgcn_ballot_w64(true);
-        const int b0 = __builtin_amdgcn_readfirstlane(b);
-        puni = __builtin_amdgcn_ballot_w64(b == b0) == act;
-        if (puni) {
-          plead = __builtin_ctzll(act);
-          poff = (uint32_t)lane_prefix(act);
-          pold = 0;
-          if (l == plead) pold = atomicAdd(&hist[b0], (uint32_t)__builtin_popcountll(act));
-        } else {
-          pold = atomicAdd(&hist[b], 1u);
-        }
-      };
-      auto resolve = [&]() -> uint32_t {  // exec = the lanes live at the previous iteration
-        if (puni) return (uint32_t)__builtin_amdgcn_readlane((int)pold, __builtin_amdgcn_readfirstlane(plead)) + poff;
-        return pold;
-      };
-      take(bk_index(bg, bx, by, bz));
-      for (int t = 0;; ++t) {
-        const bool live = t < total, fin = t == total;
-        if (__builtin_amdgcn_ballot_w64(live || fin) == 0) break;
-        if (!(live || fin)) continue;
-        if (live) {
-          const int a = bk::coarse_next(cw);
-          bx += a == 0 ? R.st[0] : 0;
-          by += a == 1 ? R.st[1] : 0;
-          bz += a == 2 ? R.st[2] : 0;
-          int32_t c[3];
-          counts(a, bx, by, bz, c);
-          const uint32_t slot = resolve();
-          put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
-          cur = entry(c);
-          idx = c[0] + c[1] + c[2];
-          ci0 = c[0];
-          ci1 = c[1];
-          ci2 = c[2];
-          take(bk_index(bg, bx, by, bz));
-        } else {
-          put(resolve(), cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
-        }
-      }
-      continue;
-    }
-#endif
     uint32_t slot = 0;
-    bk_coarse(bg, R, [&](int b, int a, int bx, int by, int bz) {
+    bk_replay(bg, R, path, [&](int b, int a, int bx, int by, int bz) {
       if (a >= 0) {
         int32_t c[3];
         counts(a, bx, by, bz, c);
@@ -1080,23 +1027,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
         ci1 = c[1];
         ci2 = c[2];
       }
-#if defined(DMF_DIAG_B_NOATOMIC)  // diagnostic build (wrong results): no slot atomics
-      slot = hist[b] + (uint32_t)(threadIdx.x & 63);
-#elif defined(DMF_EXP_B_UNI)  // experiment: one atomic when every active lane names the same brick
-      {
-        const uint64_t act = __builtin_amdgcn_ballot_w64(true);
-        const int b0 = __builtin_amdgcn_readfirstlane(b);
-        if (__builtin_amdgcn_ballot_w64(b == b0) == act) {
-          uint32_t old = 0;
-          if (l == __builtin_ctzll(act)) old = atomicAdd(&hist[b0], (uint32_t)__builtin_popcountll(act));
-          slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)old) + (uint32_t)lane_prefix(act);
-        } else {
-          slot = atomicAdd(&hist[b], 1u);
-        }
-      }
-#else
       slot = atomicAdd(&hist[b], 1u);
-#endif
     });
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }
@@ -1667,7 +1598,7 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   pl.hist_bytes = sizeof(uint32_t) * (size_t)pl.bg.nbricks;
   // per pose: ray records, per-workgroup brick bases, pose counts and bases, pose pairs + batch table
   pl.wgl_stride = 1 + (pl.bg.nbricks + 1) / 2;  // touched-brick list per workgroup: count + uint16 ids
-  pl.per_pose_bytes = (uint64_t)rays_pose * sizeof(ulonglong2) + (uint64_t)pl.wg_pose * pl.hist_bytes +
+  pl.per_pose_bytes = (uint64_t)rays_pose * (sizeof(ulonglong2) + sizeof(uint64_t)) + (uint64_t)pl.wg_pose * pl.hist_bytes +
                       (uint64_t)pl.wg_pose * sizeof(uint32_t) * (uint64_t)pl.wgl_stride + 2 * (uint64_t)pl.hist_bytes +
                       sizeof(unsigned long long) + sizeof(uint32_t);
   // pipelined calls: two staging slots, each with its own pair records, share the budget
@@ -1717,6 +1648,7 @@ static int bk_attributes() {
 // batch table, pair records.
 struct BkBufs {
   ulonglong2* rays = nullptr;
+  uint64_t* paths = nullptr;
   uint32_t *cnt = nullptr, *off = nullptr, *part_pref = nullptr, *wgb = nullptr, *wgl = nullptr;
   uint32_t *pose_cnt = nullptr, *pose_base = nullptr, *bt = nullptr;
   unsigned long long* pose_pairs = nullptr;
@@ -1731,7 +1663,8 @@ struct BkBufs {
 static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b, int slot) {
   const size_t PS = (size_t)pl.PS, nb = (size_t)pl.bg.nbricks;
   void *rays, *bricks, *ctl, *wgb, *wgl, *pra, *prb, *pcnt, *pbase, *batch;
-  DMF_TRY(scratch(v, slot ? kScBkRays1 : kScBkRays, sizeof(ulonglong2) * (size_t)(pl.PS * pl.ppose * 64), &rays));
+  const size_t nrays = (size_t)(pl.PS * pl.ppose * 64);  // ray records, then the crossing paths
+  DMF_TRY(scratch(v, slot ? kScBkRays1 : kScBkRays, (sizeof(ulonglong2) + sizeof(uint64_t)) * nrays, &rays));
   // cnt | off | part_pref (nbricks + 1) | order (uint2 per part)
   DMF_TRY(scratch(v, slot ? kScBkBricks1 : kScBkBricks, sizeof(uint32_t) * (3 * nb + 6 + 2 * pl.max_parts()), &bricks));
   DMF_TRY(scratch(v, slot ? kScBkCtl1 : kScBkCtl, sizeof(unsigned long long) * 4, &ctl));
@@ -1745,6 +1678,7 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b, int slot) {
   DMF_TRY(scratch(v, slot ? kScBkBatch1 : kScBkBatch, sizeof(unsigned long long) * PS + sizeof(uint32_t) * (PS + 4),
                   &batch));
   b.rays = (ulonglong2*)rays;
+  b.paths = (uint64_t*)(b.rays + nrays);
   b.cnt = (uint32_t*)bricks;
   b.off = b.cnt + nb;
   b.part_pref = b.off + nb;  // nbricks + 1
@@ -1854,12 +1788,12 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     if (a16)
       hipLaunchKernelGGL(k_bk_rays<true>, dim3(nwg), dim3(pl.ab_threads), sizeof(uint32_t) * ((bg.nbricks + 1) / 2), sa,
                          g, cp, d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx,
-                         (int)pl.ppose, pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride,
+                         (int)pl.ppose, pl.wg_pose, pl.span, bg, b.rays, b.paths, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride,
                          b.pose_pairs, st_a);
     else
       hipLaunchKernelGGL(k_bk_rays<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, g, cp,
                          d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
-                         pl.wg_pose, pl.span, bg, b.rays, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st_a);
+                         pl.wg_pose, pl.span, bg, b.rays, b.paths, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st_a);
     DMF_LAUNCH_CHECK();
     if (staged) {
       DMF_HIP(hipEventRecord(v->st_done[slot], sa));
@@ -1890,12 +1824,12 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       DMF_LAUNCH_CHECK();
       if (slab)
         hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,
-                           pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off,
+                           pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
                            (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb);
       else
         hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,
-                           pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint32_t*)b.off,
+                           pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
                            (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb);
       DMF_LAUNCH_CHECK();
