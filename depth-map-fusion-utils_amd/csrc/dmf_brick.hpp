@@ -409,8 +409,10 @@ __host__ __device__ inline uint32_t slab_rcode(int M, int32_t sb1, int32_t sb2, 
                 L2 = pick3(cL[0], cL[1], cL[2], m2);
   const int32_t S = LM - pick3(cin[0], cin[1], cin[2], M);
   const uint32_t steps = (uint32_t)((cL[0] - cin[0]) + (cL[1] - cin[1]) + (cL[2] - cin[2]));
-  const int64_t e1 = (int64_t)sb1 + (int64_t)(LM - 1) * (int64_t)K1 - (int64_t)(L1 - 1) * (int64_t)KM;
-  const int64_t e2 = (int64_t)sb2 + (int64_t)(LM - 1) * (int64_t)K2 - (int64_t)(L2 - 1) * (int64_t)KM;
+  // e = the state one M- and one minor crossing before the last cell's: within K_1 + K_M of a
+  // walk state (|b| < 2^29), so |e| < 2^30 and the wrapped 32-bit sum is exact
+  const int32_t e1 = (int32_t)((uint32_t)sb1 + (uint32_t)(LM - 1) * K1 - (uint32_t)(L1 - 1) * KM);
+  const int32_t e2 = (int32_t)((uint32_t)sb2 + (uint32_t)(LM - 1) * K2 - (uint32_t)(L2 - 1) * KM);
   const uint32_t s = (L1 >= 1 && e1 < 0 ? 1u : 0u) + (L2 >= 1 && e2 < 0 ? 1u : 0u);
   return S == 0 ? steps : 3u * (uint32_t)S + s;
 }
