@@ -1525,7 +1525,10 @@ static bool use_bricks(const dmf_volume* v, const Geom& g) {
   return fv == DMF_FUSE_SLAB || fv == DMF_FUSE_CELL_WALK || (fv == DMF_FUSE_DEFAULT && brick_preferred(g));
 }
 
-constexpr const char* kNameSlab = "dmf::k_bk_fuse_s<24, 32, 4>";
+// slabs per walk block of phase F: 8 (round 4 sweep 4/5/6/8/10/12 with pipelined calls: 8 is
+// 1 % faster than 4 at 512^3 and at config 2, the others slower)
+constexpr int kBkUnroll = 8;
+constexpr const char* kNameSlab = "dmf::k_bk_fuse_s<24, 32, 8>";
 constexpr const char* kNameCell = "dmf::k_bk_fuse<16, 8, 8>";
 constexpr const char* kNameLds = "dmf::k_fuse_l<12, 1280>";
 
@@ -1838,7 +1841,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         DMF_HIP(hipStreamWaitEvent(v->stream, v->st_b[slot], 0));
       }
       if (slab)
-        hipLaunchKernelGGL((k_bk_fuse_s<24, 32, 4>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,
+        hipLaunchKernelGGL((k_bk_fuse_s<24, 32, kBkUnroll>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,
                            (const uint4*)b.pra, (const uint32_t*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
                            (const uint2*)b.order, pl.part_max, b.ctl, d_hits, d_misses, st);
       else
