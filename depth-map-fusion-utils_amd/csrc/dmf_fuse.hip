@@ -1526,9 +1526,16 @@ static bool use_bricks(const dmf_volume* v, const Geom& g) {
 }
 
 // slabs per walk block of phase F: 8 (round 4 sweep 4/5/6/8/10/12 with pipelined calls: 8 is
-// 1 % faster than 4 at 512^3 and at config 2, the others slower)
+// 1 % faster than 4 at 512^3 and at config 2, the others slower); with 8-slab blocks a wave
+// refills at >= 16 idle lanes (sweep 16/20/24/32, picks over 16/32/64 regions: serial -1 %,
+// config 2 -0.5 %, pipelined within the box's drift)
 constexpr int kBkUnroll = 8;
-constexpr const char* kNameSlab = "dmf::k_bk_fuse_s<24, 32, 8>";
+#if defined(DMF_EXP_F_REFILL)  // experiment builds: refill threshold / pick spread of phase F
+constexpr int kBkRefill = DMF_EXP_F_REFILL, kBkSpread = DMF_EXP_F_SPREAD;
+#else
+constexpr int kBkRefill = 16, kBkSpread = 32;
+#endif
+constexpr const char* kNameSlab = "dmf::k_bk_fuse_s<16, 32, 8>";
 constexpr const char* kNameCell = "dmf::k_bk_fuse<16, 8, 8>";
 constexpr const char* kNameLds = "dmf::k_fuse_l<12, 1280>";
 
@@ -1841,7 +1848,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         DMF_HIP(hipStreamWaitEvent(v->stream, v->st_b[slot], 0));
       }
       if (slab)
-        hipLaunchKernelGGL((k_bk_fuse_s<24, 32, kBkUnroll>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,
+        hipLaunchKernelGGL((k_bk_fuse_s<kBkRefill, kBkSpread, kBkUnroll>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,
                            (const uint4*)b.pra, (const uint32_t*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
                            (const uint2*)b.order, pl.part_max, b.ctl, d_hits, d_misses, st);
       else

@@ -765,7 +765,7 @@ def test_fuse_brick_multi_batch(oracle, engine, dmf, mode):
                 expect, acc = expect + 1, 0
             acc += c
         assert expect >= 3
-    for variant, name in ((57, "dmf::k_bk_fuse_s<24, 32, 8>"), (40, "dmf::k_bk_fuse<16, 8, 8>")):
+    for variant, name in ((57, "dmf::k_bk_fuse_s<16, 32, 8>"), (40, "dmf::k_bk_fuse<16, 8, 8>")):
         _lib.set_variant(gv, variant)
         hg, mg, sg = engine.fuse_depth(gv, depth, poses, prm)
         assert _lib.kernel_name(gv) == name
@@ -833,7 +833,7 @@ def test_fuse_edge_cases(oracle, dmf, n, variant):
         eng = dmf.RayTracingEngine(dmf.Camera(Kc, Hc, Wc))
         hg, mg, sg = eng.fuse_depth(gv, D, P, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
         if variant in (0, 57) and so[0] > 0:
-            assert _lib.kernel_name(gv) == "dmf::k_bk_fuse_s<24, 32, 8>", name
+            assert _lib.kernel_name(gv) == "dmf::k_bk_fuse_s<16, 32, 8>", name
         assert np.array_equal(so, sg), (name, so, sg)
         assert np.array_equal(ho, hg) and np.array_equal(mo, mg), name
         if name in ("no_valid_pixel", "misses_grid", "ends_before_grid"):
