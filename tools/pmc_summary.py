@@ -33,6 +33,10 @@ with open(os.path.join(dst, "pmc_per_kernel.csv"), "w", newline="") as f:
     for (k, c), v in sorted(tot.items()):
         n = len(ndisp[(k, c)])
         w.writerow([k, c, f"{v:.0f}", n, f"{v / n:.1f}"])
+if not os.path.exists(os.path.join(src, "bench_kt.json")):
+    # a bench.py --pmc-dir directory (the bench line carries its own summary): counters and
+    # kernel statistics only
+    sys.exit(0)
 bench = json.load(open(os.path.join(src, "bench_kt.json")))
 # the fusion launch = every kernel of the fusion pipeline (brick path: k_bk_rays, k_bk_scan,
 # k_bk_pairs, k_bk_fuse; LDS-box path: k_fuse_l alone), priced per bench step
