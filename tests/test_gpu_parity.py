@@ -816,6 +816,41 @@ def _edge_fusion_cases():
     return cases
 
 
+def _diagonal_pose(origin):
+    """Camera at `origin` looking along +(1, 1, 1) (its z axis), row-major 3x4."""
+    z = np.ones(3) / np.sqrt(3.0)
+    x = np.cross([0.0, 0.0, 1.0], z)
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x)
+    R = np.stack([x, y, z], 1)  # columns: camera axes in the world
+    return np.concatenate([R, np.asarray(origin, float)[:, None]], 1).astype(np.float32).reshape(12)
+
+
+@pytest.mark.parametrize("n", [512, 1024])
+def test_fuse_long_rays_walk_fallback(oracle, dmf, n):
+    """Rays that cross more than bk::kPathSteps = 32 brick boundaries: pass A records only the
+    first 32 crossing axes, so pass B walks such rays again (bk_replay's fallback).  A camera
+    outside a grid corner looking along the diagonal, depth 1.7 m: every ray crosses most of
+    the grid (46+ boundaries at 512^3, 90+ at 1024^3), some packets mix them with shorter
+    ones (the image corners).  Counters and statistics equal the oracle's."""
+    from dmf_amd import _lib
+    Kc = np.array([40.0, 0.0, 31.5, 0.0, 40.0, 23.5, 0.0, 0.0, 1.0], np.float32)
+    P = np.stack([_diagonal_pose([-0.62, -0.6, -0.61]), _diagonal_pose([-0.6, -0.63, -0.6])])
+    D = np.full((2, 48, 64), 1700, np.uint16)
+    D[:, :8, :] = 600  # shorter rays (fewer than 32 boundaries) in the same packets as long ones
+    ov = Hh.oracle_volume(oracle, n=n, clouds=[])
+    gv = Hh.gpu_volume(n=n, clouds=[])
+    ho, mo, so = oracle.fuse_depth(ov, Kc, D, P, dmin=200, dmax=2000)
+    eng = dmf.RayTracingEngine(dmf.Camera(Kc, 48, 64))
+    hg, mg, sg = eng.fuse_depth(gv, D, P, dmf.FuseParams(dmin_mm=200, dmax_mm=2000))
+    assert _lib.kernel_name(gv) == "dmf::k_bk_fuse_s<16, 32, 8>"
+    # rays average over 0.9 n cells (the diagonal ones cross ~47 boundaries at 512^3, ~94 at
+    # 1024^3; the image's edge rays leave the grid earlier, under 32)
+    assert so[0] / so[1] > 0.9 * n, so
+    assert np.array_equal(so, sg), (so, sg)
+    assert np.array_equal(ho, hg) and np.array_equal(mo, mg)
+
+
 @pytest.mark.parametrize("n,variant", [(256, 0), (96, 57), (96, 40), (96, 31)])
 def test_fuse_edge_cases(oracle, dmf, n, variant):
     """Every edge case of _edge_fusion_cases through (256, 0) the DEFAULT dispatch at a grid
