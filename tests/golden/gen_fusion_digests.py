@@ -33,7 +33,8 @@ from oracle import oracle as O  # noqa: E402
 OUT = os.path.join(HERE, "fusion_digests.json")
 SEED = 1234
 # key -> (grid, W, H, global poses): bench.py at --gpus N (config 4: 128 poses per GPU, the
-# N = 8 set is the 1024-pose anchor), config 2 and config 3 at N = 1
+# N = 8 set is the 1024-pose anchor), config 2 and config 3 at N = 1, and config 5's per-GPU
+# shard size (1280x720, 1024^3, 256 poses) run on one GPU
 WORKLOADS = {
     "config4_shard_N1": (512, 640, 480, 128),
     "config4_N2": (512, 640, 480, 256),
@@ -41,6 +42,7 @@ WORKLOADS = {
     "config4_N8_anchor": (512, 640, 480, 1024),
     "config2_N1": (256, 640, 480, 64),
     "config3_N1": (512, 1280, 720, 256),
+    "config5_shard_N1": (1024, 1280, 720, 256),  # config 5's per-GPU shard size (256 of 2048 poses)
 }
 
 
