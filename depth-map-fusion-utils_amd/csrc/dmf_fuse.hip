@@ -586,57 +586,108 @@ __device__ inline void hist_add_agg(uint32_t* hist, int b) {
   }
 }
 
-// Pass A.  Workgroup = 4 (or 16) waves over a span of 8x8 packets of ONE pose (wg_pose
-// workgroups per pose, the last one of a pose shorter); ray index = packet * 64 + lane.
-// Counts are kept per (pose, brick): pose_cnt[p][b] (the workgroup's base inside that
-// count is wg_base[wg][b]) and per pose: pose_pairs[p], so that the device can cut the
+// Pass A's hashed histogram (grids over kBkBigHist bricks): open addressing
+// over `mask + 1` words of (brick << 16 | 16-bit count); a workgroup touches a few hundred of
+// the up to 32768 bricks, so 8 KB of LDS replace the 64-KB direct table and pass A fits beside
+// phase F's box.  Returns false when the table is full (the workgroup is then redone with the
+// direct table by k_bk_rays_recover).
+constexpr uint32_t kHashEmpty = 0xffff0000u;  // key 0xffff: no brick (bricks < 32768)
+__device__ inline bool hash_add(uint32_t* tab, uint32_t mask, int shift, uint32_t b, uint32_t n) {
+  uint32_t h = (b * 2654435761u) >> shift;
+  for (uint32_t k = 0; k <= mask; ++k) {
+    const uint32_t old = atomicCAS(&tab[h], kHashEmpty, b << 16 | n);
+    if (old == kHashEmpty) return true;
+    if ((old >> 16) == b) {
+      atomicAdd(&tab[h], n);
+      return true;
+    }
+    h = (h + 1) & mask;
+  }
+  return false;
+}
+
+// hist_add_agg into the hashed histogram; sets *ovf when an insert finds the table full
+__device__ inline void hash_add_agg(uint32_t* tab, uint32_t mask, int shift, int b, uint32_t* ovf) {
+  uint64_t rem = __builtin_amdgcn_ballot_w64(true);
+  const int l = (int)(threadIdx.x & 63);
+  while (rem) {
+    const int leader = __builtin_ctzll(rem);
+    const int bl = __builtin_amdgcn_readlane(b, leader);
+    const uint64_t same = __builtin_amdgcn_ballot_w64(b == bl) & rem;
+    if (l == leader && !hash_add(tab, mask, shift, (uint32_t)bl, (uint32_t)__builtin_popcountll(same))) *ovf = 1u;
+    rem &= ~same;
+  }
+}
+
+struct BkRaysArgs {
+  Geom g;
+  CamP cam;
+  const uint16_t* depth;
+  const PoseX* poses;
+  int dmin, dmax, packets_x, packets_pose, wg_pose, span;
+  BkGeom bg;
+  ulonglong2* rays;
+  uint64_t* paths;
+  uint32_t* pose_cnt;
+  uint32_t* wg_base;
+  uint32_t* wg_list;
+  int wgl_stride;
+  unsigned long long* pose_pairs;
+  unsigned long long* stats;
+  uint32_t* ovl;   // [count | workgroups whose hashed histogram overflowed]
+  int hash_log;    // log2 of the hashed histogram's words (HASH)
+};
+
+// Pass A for workgroup wg.  Workgroup = 4 (or 16) waves over a span of 8x8 packets of ONE
+// pose (wg_pose workgroups per pose, the last one of a pose shorter); ray index = packet * 64
+// + lane.  Counts are kept per (pose, brick): pose_cnt[p][b] (the workgroup's base inside
+// that count is wg_base[wg][b]) and per pose: pose_pairs[p], so that the device can cut the
 // call into pose batches by the pairs they really make (k_bk_batches) and any batch's
 // per-brick lists can be laid out (k_bk_batch_counts) without re-running this pass.
 // H16: the histogram holds two 16-bit counts per word (brick b in half b & 1 of word b >> 1:
 // a workgroup's rays make at most span * 64 <= 65535 pairs in one brick).  Half the LDS, so
 // that two pass-A workgroups fit beside phase F's box on a CU when calls are pipelined
-// (DESIGN.md §5.10).
-template <bool H16>
-__global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam, const uint16_t* __restrict__ depth,
-                                                        const PoseX* __restrict__ poses, int dmin, int dmax,
-                                                        int packets_x, int packets_pose, int wg_pose, int span,
-                                                        BkGeom bg, ulonglong2* __restrict__ rays,
-                                                        uint64_t* __restrict__ paths,
-                                                        uint32_t* __restrict__ pose_cnt,
-                                                        uint32_t* __restrict__ wg_base,
-                                                        uint32_t* __restrict__ wg_list, int wgl_stride,
-                                                        unsigned long long* __restrict__ pose_pairs,
-                                                        unsigned long long* __restrict__ stats) {
-  extern __shared__ uint32_t hist[];
-  __shared__ uint32_t nlist;
-  stats = stat_slot(stats);
-  if (threadIdx.x == 0) nlist = 0;
-  const int nwords = H16 ? (bg.nbricks + 1) >> 1 : bg.nbricks;
-  for (int i = threadIdx.x; i < nwords; i += blockDim.x) hist[i] = 0;
+// (DESIGN.md §5.10).  HASH: the hashed histogram above; a workgroup whose table overflows
+// writes only its ray records, lists itself in ovl and leaves counts and statistics to
+// k_bk_rays_recover.  sh: two shared words (touched-list count, overflow flag).
+template <bool H16, bool HASH>
+__device__ inline void bk_rays_wg(const BkRaysArgs& A_, unsigned wg, uint32_t* hist, uint32_t* sh) {
+  const Geom& g = A_.g;
+  const BkGeom& bg = A_.bg;
+  unsigned long long* const stats = stat_slot(A_.stats);
+  const uint32_t hmask = (1u << A_.hash_log) - 1u;
+  const int hshift = 32 - A_.hash_log;
+  if (threadIdx.x == 0) {
+    sh[0] = 0;
+    sh[1] = 0;
+  }
+  const int nwords = HASH ? (int)hmask + 1 : (H16 ? (bg.nbricks + 1) >> 1 : bg.nbricks);
+  for (int i = threadIdx.x; i < nwords; i += blockDim.x) hist[i] = HASH ? kHashEmpty : 0u;
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const int pw = (int)(blockIdx.x / (unsigned)wg_pose);
-  const int q0 = (int)(blockIdx.x - (unsigned)pw * (unsigned)wg_pose) * span;
-  const int64_t pk0 = (int64_t)pw * packets_pose + q0, pk1 = (int64_t)pw * packets_pose + min(packets_pose, q0 + span);
+  const int pw = (int)(wg / (unsigned)A_.wg_pose);
+  const int q0 = (int)(wg - (unsigned)pw * (unsigned)A_.wg_pose) * A_.span;
+  const int64_t pk0 = (int64_t)pw * A_.packets_pose + q0,
+                pk1 = (int64_t)pw * A_.packets_pose + min(A_.packets_pose, q0 + A_.span);
   unsigned long long upd = 0, nvalid = 0, nhit = 0;
   // (loading the next packet's depth one packet ahead measured slower: 0.79 -> 0.84 ms)
   double go[3];
   {
-    const float O[3] = {poses[pw].f[3], poses[pw].f[7], poses[pw].f[11]};
+    const float O[3] = {A_.poses[pw].f[3], A_.poses[pw].f[7], A_.poses[pw].f[11]};
     grid_origin(g, O, go);
   }
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
     const int p = pw;
-    const int q = (int)(pk - (int64_t)p * packets_pose);
-    const int r = (q / packets_x) * 8 + (l >> 3), c = (q % packets_x) * 8 + (l & 7);
-    const int d = pixel_depth(cam, depth, p, r, c);
+    const int q = (int)(pk - (int64_t)p * A_.packets_pose);
+    const int r = (q / A_.packets_x) * 8 + (l >> 3), c = (q % A_.packets_x) * 8 + (l & 7);
+    const int d = pixel_depth(A_.cam, A_.depth, p, r, c);
     int64_t qs[3], qe[3];
     bool inside, valid;
     ulonglong2 rec;
     rec.x = 0;
     rec.y = 0;
     uint64_t path = 0;  // the crossing axes of the coarse walk (pass B replays them)
-    if (pixel_quant_go(g, cam, d, poses[p], go, r, c, dmin, dmax, qs, qe, inside, valid)) {
+    if (pixel_quant_go(g, A_.cam, d, A_.poses[p], go, r, c, A_.dmin, A_.dmax, qs, qe, inside, valid)) {
       uint64_t A, B;
       bk::pack_ray(qs, qe, inside, A, B);
       rec.x = A;
@@ -649,33 +700,82 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(Geom g, CamP cam,
       nhit += inside ? 1 : 0;
       int t = 0;
       bk_coarse(bg, R, [&](int b, int a, int, int, int) {
-        hist_add_agg<H16>(hist, b);
+        if constexpr (HASH) hash_add_agg(hist, hmask, hshift, b, &sh[1]);
+        else hist_add_agg<H16>(hist, b);
         if (a >= 0) path = bk::path_put(path, t++, a);
       });
     }
     nvalid += valid ? 1 : 0;
-    rays[pk * 64 + l] = rec;
-    paths[pk * 64 + l] = path;
+    A_.rays[pk * 64 + l] = rec;
+    A_.paths[pk * 64 + l] = path;
   }
   __syncthreads();
-  uint32_t* const pc = pose_cnt + (size_t)pw * bg.nbricks;
+  if (HASH && sh[1]) {  // table full: k_bk_rays_recover redoes this workgroup
+    if (threadIdx.x == 0) A_.ovl[1 + atomicAdd(&A_.ovl[0], 1u)] = wg;
+    return;
+  }
+  uint32_t* const pc = A_.pose_cnt + (size_t)pw * bg.nbricks;
   // the workgroup's touched bricks: [count | uint16 brick ids] (pass B initialises only these)
-  uint32_t* const row = wg_list + (size_t)blockIdx.x * (size_t)wgl_stride;
+  uint32_t* const row = A_.wg_list + (size_t)wg * (size_t)A_.wgl_stride;
   uint16_t* const ids = (uint16_t*)(row + 1);
   unsigned long long mine = 0;
-  for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) {
-    const uint32_t n = H16 ? (hist[i >> 1] >> ((i & 1) << 4)) & 0xffffu : hist[i];
-    if (n) {
-      wg_base[(size_t)blockIdx.x * bg.nbricks + i] = atomicAdd(&pc[i], n);
-      ids[atomicAdd(&nlist, 1u)] = (uint16_t)i;
+  for (int i = threadIdx.x; i < nwords; i += blockDim.x) {
+    uint32_t b, n;
+    if constexpr (HASH) {
+      const uint32_t e = hist[i];
+      b = e >> 16;
+      n = e == kHashEmpty ? 0u : (e & 0xffffu);
+    } else {
+      // direct table: word i holds brick i (or bricks 2i, 2i + 1 when H16)
+      b = (uint32_t)i;
+      n = hist[i];
+    }
+    if (!HASH && H16) {
+      for (int hh = 0; hh < 2; ++hh) {
+        const uint32_t bb = 2u * (uint32_t)i + (uint32_t)hh, nn = (n >> (16 * hh)) & 0xffffu;
+        if (nn) {
+          A_.wg_base[(size_t)wg * bg.nbricks + bb] = atomicAdd(&pc[bb], nn);
+          ids[atomicAdd(&sh[0], 1u)] = (uint16_t)bb;
+          mine += nn;
+        }
+      }
+    } else if (n) {
+      A_.wg_base[(size_t)wg * bg.nbricks + b] = atomicAdd(&pc[b], n);
+      ids[atomicAdd(&sh[0], 1u)] = (uint16_t)b;
       mine += n;
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) row[0] = nlist;
+  if (threadIdx.x == 0) row[0] = sh[0];
   for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o, 64);
-  if (l == 0 && mine) atomicAdd(&pose_pairs[pw], mine);
+  if (l == 0 && mine) atomicAdd(&A_.pose_pairs[pw], mine);
   if (stats) wave_stats(stats, upd, nvalid, nhit);
+}
+
+template <bool H16>
+__global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays(BkRaysArgs a) {
+  extern __shared__ uint32_t hist[];
+  __shared__ uint32_t sh[2];
+  bk_rays_wg<H16, false>(a, blockIdx.x, hist, sh);
+}
+
+// Pass A with the hashed histogram (256-lane workgroups, 8 KB of LDS by default).
+__global__ __launch_bounds__(kBkPassThreads) void k_bk_rays_hash(BkRaysArgs a) {
+  extern __shared__ uint32_t tab[];
+  __shared__ uint32_t sh[2];
+  bk_rays_wg<true, true>(a, blockIdx.x, tab, sh);
+}
+
+// The workgroups whose hashed histogram overflowed, redone with the direct 16-bit table
+// (persistent: the grid strides over the list; exits at once when it is empty).
+__global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_rays_recover(BkRaysArgs a) {
+  extern __shared__ uint32_t hist[];
+  __shared__ uint32_t sh[2];
+  const uint32_t n = a.ovl[0];
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    bk_rays_wg<true, false>(a, a.ovl[1 + i], hist, sh);
+    __syncthreads();  // the next workgroup's table reset follows this one's flush
+  }
 }
 
 // Pose batches of a call by the pairs pass A counted (one workgroup): greedy over the poses
@@ -1571,6 +1671,7 @@ struct BkPlan {
   int64_t PBg = 0;            // poses per batch under the geometric bound (>= 1)
   int max_poses = 0;          // cap of poses per batch (DMF_KNOB_BATCH_POSES test hook; else PS)
   int ab_threads = 0, span = 0, wg_pose = 0, wgl_stride = 0;
+  int hash_log = 0;  // pass A's hashed histogram: log2 of its words (0 = the direct table)
   uint32_t part_max = kBkPartMax;  // pairs per part of phase F (DMF_KNOB_PART_MAX)
   size_t rec_bytes = 20;           // bytes per pair record: 16 (pa) + 4 (slab walk) or 16 + 8 (per-cell walk)
   size_t hist_bytes = 0;
@@ -1601,6 +1702,17 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   // histogram is small enough for 8 per wave: config 2 fusion 2.05 -> 2.02 ms, while 384^3
   // and 512^3 measured slower at 32 packets than at 64
   pl.span = std::max((pl.bg.nbricks <= 512 ? 8 : 16) * (pl.ab_threads / 64), (pl.bg.nbricks + 63) / 64);
+  // over kBkBigHist bricks pass A counts into a hashed histogram of 2048 words (8 KB: it runs
+  // beside phase F's box when calls are pipelined; the 64-KB direct table cannot) over spans
+  // of 128 packets (a few hundred touched bricks per workgroup at 1024^3)
+  if (kn[DMF_KNOB_A_HASH] > 0) {
+    int lg = 4;
+    while (lg < 16 && (1ll << lg) < kn[DMF_KNOB_A_HASH]) ++lg;
+    pl.hash_log = lg;
+  } else if (kn[DMF_KNOB_A_HASH] == 0 && pl.bg.nbricks > kBkBigHist) {
+    pl.hash_log = 11;
+    pl.span = 128;
+  }
   if (kn[DMF_KNOB_SPAN] > 0) pl.span = (int)std::max<int64_t>(4, std::min<int64_t>(kn[DMF_KNOB_SPAN], 4096));
   if (kn[DMF_KNOB_PART_MAX] > 0)
     pl.part_max = (uint32_t)std::max<int64_t>(1024, std::min<int64_t>(kn[DMF_KNOB_PART_MAX], kBkPartMax));
@@ -1646,6 +1758,8 @@ static int bk_attributes() {
     const int lds = (int)(sizeof(uint32_t) * 32768);
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays_recover, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays_hash, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_pairs<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set.store(true);
@@ -1666,6 +1780,7 @@ struct BkBufs {
   unsigned long long* ctl = nullptr;
   uint4* pra = nullptr;
   void* prb = nullptr;  // uint32 per pair (20-B records) or uint2 (24-B records)
+  uint32_t* ovl = nullptr;  // pass A's overflow list [count | workgroups]
 };
 
 // Allocates only when a slot is too small.  `slot` = 0 or 1: the two staging slots of
@@ -1687,6 +1802,9 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b, int slot) {
   DMF_TRY(scratch(v, slot ? kScBkPoseBase1 : kScBkPoseBase, pl.hist_bytes * PS, &pbase));
   DMF_TRY(scratch(v, slot ? kScBkBatch1 : kScBkBatch, sizeof(unsigned long long) * PS + sizeof(uint32_t) * (PS + 4),
                   &batch));
+  void* ovl;
+  DMF_TRY(scratch(v, slot ? kScBkOvf1 : kScBkOvf, sizeof(uint32_t) * (1 + (size_t)pl.wg_pose * PS), &ovl));
+  b.ovl = (uint32_t*)ovl;
   b.rays = (ulonglong2*)rays;
   b.paths = (uint64_t*)(b.rays + nrays);
   b.cnt = (uint32_t*)bricks;
@@ -1712,7 +1830,7 @@ static int bk_release(dmf_volume* v) {
   static const int kSlots[] = {kScBkRays, kScBkPairs, kScBkPairsB, kScBkBricks, kScBkWgBase, kScBkCtl, kScBkPoseCnt,
                                kScBkPoseBase, kScBkBatch, kScBkWgList, kScBkRays1, kScBkWgBase1, kScBkWgList1,
                                kScBkPoseCnt1, kScBkBatch1, kScBkBricks1, kScBkCtl1, kScBkPairs1, kScBkPairsB1,
-                               kScBkPoseBase1};
+                               kScBkPoseBase1, kScBkOvf, kScBkOvf1};
   if (v->stream) DMF_HIP(hipStreamSynchronize(v->stream));
   if (v->stage) DMF_HIP(hipStreamSynchronize(v->stage));
   for (int k : kSlots) {
@@ -1795,15 +1913,24 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     }
     DMF_HIP(hipMemsetAsync(b.pose_cnt, 0, pl.hist_bytes * (size_t)ps, sa));
     DMF_HIP(hipMemsetAsync(b.pose_pairs, 0, sizeof(unsigned long long) * (size_t)ps, sa));
-    if (a16)
+    BkRaysArgs ra{g, cp, d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
+                  pl.wg_pose, pl.span, bg, b.rays, b.paths, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs,
+                  st_a, b.ovl, 0};
+    if (a16 && pl.hash_log > 0) {
+      // hashed histogram (8 KB: beside phase F's box), then the overflowed workgroups (if any)
+      // with the direct table
+      ra.hash_log = pl.hash_log;
+      DMF_HIP(hipMemsetAsync(b.ovl, 0, sizeof(uint32_t), sa));
+      hipLaunchKernelGGL(k_bk_rays_hash, dim3(nwg), dim3(kBkPassThreads), sizeof(uint32_t) << pl.hash_log, sa, ra);
+      DMF_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_bk_rays_recover, dim3(nf), dim3(kBkPassThreadsBig), sizeof(uint32_t) * ((bg.nbricks + 1) / 2),
+                         sa, ra);
+    } else if (a16) {
       hipLaunchKernelGGL(k_bk_rays<true>, dim3(nwg), dim3(pl.ab_threads), sizeof(uint32_t) * ((bg.nbricks + 1) / 2), sa,
-                         g, cp, d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx,
-                         (int)pl.ppose, pl.wg_pose, pl.span, bg, b.rays, b.paths, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride,
-                         b.pose_pairs, st_a);
-    else
-      hipLaunchKernelGGL(k_bk_rays<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, g, cp,
-                         d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
-                         pl.wg_pose, pl.span, bg, b.rays, b.paths, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs, st_a);
+                         ra);
+    } else {
+      hipLaunchKernelGGL(k_bk_rays<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, ra);
+    }
     DMF_LAUNCH_CHECK();
     if (staged) {
       DMF_HIP(hipEventRecord(v->st_done[slot], sa));

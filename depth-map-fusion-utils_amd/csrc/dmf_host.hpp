@@ -60,7 +60,8 @@ enum ScratchSlot {
   // ... and, when pass B is staged as well, the second slot's brick layout and pair records
   kScBkBricks1, kScBkCtl1, kScBkPairs1, kScBkPairsB1, kScBkPoseBase1,
   kScOgP0, kScOgP1, kScOgFinal, kScOgOcc,  // OccupancyGrid reorganization (dmf_ogrid.hip)
-  kScRevItems  // reverseRayTraceFast's item-ordered (spatial order) result masks (dmf_trace.hip)
+  kScRevItems,  // reverseRayTraceFast's item-ordered (spatial order) result masks (dmf_trace.hip)
+  kScBkOvf, kScBkOvf1  // pass A's hashed-histogram overflow lists, per staging slot (dmf_fuse.hip)
 };
 
 // Striped statistics: kernels add into slot (block % kStatSlots) of a zeroed buffer

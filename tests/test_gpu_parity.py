@@ -718,6 +718,27 @@ def test_fuse_brick_vs_lds_box_full_size(dmf):
     assert int(c0[:nt].astype(np.int64).sum()) == int(s0[2])  # one hit per ray ending inside
 
 
+@pytest.mark.parametrize("n,slots", [(256, 2048), (256, 16), (96, 64)])
+def test_fuse_pass_a_hashed_histogram(oracle, dmf, n, slots):
+    """Pass A's hashed histogram (the default above 8192 bricks, forced here with
+    DMF_KNOB_A_HASH = slots words): 2048 words hold every workgroup's bricks; 16 / 64 words
+    overflow in most workgroups, which k_bk_rays_recover then redoes with the direct table
+    (the overflowed workgroups' first run writes ray records only).  Counters and statistics
+    equal the oracle's either way."""
+    from dmf_amd import _lib
+    poses, depth, _ = Hh.frames()
+    poses, depth = poses[:4], depth[:4]
+    ov = Hh.oracle_volume(oracle, n=n, clouds=[])
+    ho, mo, so = oracle.fuse_depth(ov, K, depth, poses, dmin=200, dmax=1000)
+    gv = Hh.gpu_volume(n=n, clouds=[])
+    _lib.set_variant(gv, 57)
+    _lib.set_knob(gv, "a_hash", slots)
+    eng = dmf.RayTracingEngine(dmf.Camera(K, H, W))
+    hg, mg, sg = eng.fuse_depth(gv, depth, poses, dmf.FuseParams(dmin_mm=200, dmax_mm=1000))
+    assert np.array_equal(so, sg), (so, sg)
+    assert np.array_equal(ho, hg) and np.array_equal(mo, mg)
+
+
 @pytest.mark.parametrize("mode", ["poses2", "paircap"])
 def test_fuse_brick_multi_batch(oracle, engine, dmf, mode):
     """The brick pipeline (57 = the production slab walk on 20-B records, 40 = per-cell walk)
