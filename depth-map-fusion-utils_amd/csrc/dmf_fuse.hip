@@ -1946,26 +1946,30 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     v->bk_last_bt = b.bt;
     const int64_t jm = pl.jmax(ps);
     for (int64_t j = 0; j < jm; ++j) {
-      // batch j reuses the slot's pair records and part queue: after batch j-1's phase F
-      if (staged && j > 0) DMF_HIP(hipStreamWaitEvent(sa, v->st_free[slot], 0));
-      DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sa));
-      hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sa, bg.nbricks,
+      // batch j > 0 reuses the slot's pair records and part queue, so it follows batch j-1's
+      // phase F: on the volume's stream (in order after it, no event).  The host launches
+      // jmax triples from the one-pose bound; those past the device's batch count exit at
+      // once, and on the volume's stream they no longer hold the staging stream -- and with
+      // it the next call's pass A -- behind this call's phase F (1024^3: jmax 7, one batch).
+      const hipStream_t sj = staged && j > 0 ? v->stream : sa;
+      DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sj));
+      hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sj, bg.nbricks,
                          (int)j, (const uint32_t*)b.bt, (const uint32_t*)b.pose_cnt, b.pose_base, b.cnt);
       DMF_LAUNCH_CHECK();
       if (bg.nbricks > 4096)
-        hipLaunchKernelGGL(k_bk_scan<true>, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off,
+        hipLaunchKernelGGL(k_bk_scan<true>, dim3(1), dim3(1024), 0, sj, bg.nbricks, (const uint32_t*)b.cnt, b.off,
                            b.part_pref, b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       else
-        hipLaunchKernelGGL(k_bk_scan<false>, dim3(1), dim3(1024), 0, sa, bg.nbricks, (const uint32_t*)b.cnt, b.off,
+        hipLaunchKernelGGL(k_bk_scan<false>, dim3(1), dim3(1024), 0, sj, bg.nbricks, (const uint32_t*)b.cnt, b.off,
                            b.part_pref, b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       DMF_LAUNCH_CHECK();
       if (slab)
-        hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,
+        hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sj, (int)pl.ppose,
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
                            (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb);
       else
-        hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, (int)pl.ppose,
+        hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sj, (int)pl.ppose,
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
                            (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb);
