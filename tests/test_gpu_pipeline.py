@@ -130,12 +130,16 @@ def _run(n, poses, depth, per_call, pipelined, variant=0, knobs=None):
         v.close()
 
 
-@pytest.mark.parametrize("case", ["calls", "super2", "super1_batches"])
+@pytest.mark.parametrize("case", ["calls", "super2", "super1_batches", "hash_overflow_batches"])
 def test_pipelined_equals_serial_256(case):
-    """256^3 (the default brick pipeline), 4 calls of 3 frames."""
+    """256^3 (the default brick pipeline), 4 calls of 3 frames.  hash_overflow_batches: pass
+    A's hashed histogram forced with 64 words (most workgroups overflow and are redone by
+    k_bk_rays_recover) and three device batches per super-batch (batches j > 0 on the
+    volume's stream)."""
     poses, depth = _frames(12)
     knobs = {"calls": {}, "super2": {"super_poses": 2},  # 3 frames -> super-batches of 2 + 1
-             "super1_batches": {"super_poses": 3, "batch_poses": 1}}[case]  # three device batches each
+             "super1_batches": {"super_poses": 3, "batch_poses": 1},  # three device batches each
+             "hash_overflow_batches": {"super_poses": 3, "batch_poses": 1, "a_hash": 64}}[case]
     hs, ms, ss = _run(256, poses, depth, 3, pipelined=False, knobs=knobs)
     hp, mp, sp = _run(256, poses, depth, 3, pipelined=True, knobs=knobs)
     assert ss[0] > 10 ** 7 and ss[3] == 0
