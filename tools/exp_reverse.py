@@ -2,7 +2,8 @@
 """A/B of reverseRayTraceFast work orders (DMF_KNOB_REVERSE_KERNEL 0 = spatial order, 3 =
 occupied_cells_ order) on bench.py's secondary workload: a 512^3 volume integrated from 16
 back-projected 640x480 frames, 128 poses per launch.  Prints ms per launch for each and
-checks the visibility / good masks are identical."""
+checks the visibility / good masks are identical (with a DMF_EXP_STATS library also the work
+queue's lane occupancy: busy lane-iterations / 64 x burst iterations)."""
 import ctypes as C
 import json
 import os
@@ -63,6 +64,9 @@ for kr in (3, 0, 3, 0):
     torch.cuda.synchronize(dev)
     out[f"ms_kernel{kr}"] = e0.elapsed_time(e1) / 5
     out[f"samples_kernel{kr}"] = int(st[0].item()) // 5
+    sv = st.cpu().numpy()
+    if sv[10] > 0:  # DMF_EXP_STATS build: burst iterations (per wave) and busy lane-iterations
+        out[f"lane_busy_kernel{kr}"] = float(sv[11]) / (64.0 * float(sv[10]))
     res[kr] = (vis.cpu().numpy(), good.cpu().numpy())
 out["masks_equal"] = bool(np.array_equal(res[0][0], res[3][0]) and np.array_equal(res[0][1], res[3][1]))
 print(json.dumps(out), flush=True)
