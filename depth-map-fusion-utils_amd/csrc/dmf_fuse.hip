@@ -1707,7 +1707,7 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   // of 128 packets (a few hundred touched bricks per workgroup at 1024^3)
   if (kn[DMF_KNOB_A_HASH] > 0) {
     int lg = 4;
-    while (lg < 16 && (1ll << lg) < kn[DMF_KNOB_A_HASH]) ++lg;
+    while (lg < 14 && (1ll << lg) < kn[DMF_KNOB_A_HASH]) ++lg;  // 16 .. 16384 words (64 KB)
     pl.hash_log = lg;
   } else if (kn[DMF_KNOB_A_HASH] == 0 && pl.bg.nbricks > kBkBigHist) {
     pl.hash_log = 11;

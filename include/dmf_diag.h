@@ -44,8 +44,8 @@ enum dmf_knob {
                                   field), 1 plain, 2 plain + brick skip, 3 queue in insertion order */
   DMF_KNOB_FWD_SKIP = 8,    /* forward march empty-space skipping: 0 default (on), -1 off */
   DMF_KNOB_A_HASH = 9,      /* pass A's histogram: 0 default (hashed, 2048 words, above 8192 bricks; direct
-                               below), -1 always direct, k > 0 always hashed with k words (power of two,
-                               16..65536; a workgroup whose table overflows is redone with the direct one) */
+                               below), -1 always direct, k > 0 always hashed with k words (rounded up to a
+                               power of two, 16..16384; a workgroup whose table overflows is redone with the direct one) */
   DMF_KNOB_COUNT = 10
 };
 int dmf_volume_set_knob(dmf_volume* v, int32_t knob, int64_t value);
