@@ -415,18 +415,29 @@ def main():
         e.record(rt.lanes[lane])
         ev.setdefault(i, {})[name] = e
 
-    S.run_steps(rt, args.warmup, 2, clear, fuse, merge)
+    # the merge (finalize / RCCL) and clear of step i wait for step i+1's phase F to begin
+    # (dmf_fuse_set_phase_event), so that they run beside the issue-bound phase F and not
+    # beside the next call's passes A / B (DMF_BENCH_PHASE=0: right after step i's fusion)
+    phase = None
+    if os.environ.get("DMF_BENCH_PHASE", "1") != "0":
+        fev = torch.cuda.Event()
+        fev.record(stream)  # creates the event
+        _lib.check(L.dmf_fuse_set_phase_event(vol._h, C.c_void_p(fev.cuda_event)))
+        phase = lambda i: fev  # noqa: E731  (re-recorded by each fusion call)
+    S.run_steps(rt, args.warmup, 2, clear, fuse, merge, phase=phase)
     torch.cuda.synchronize(dev)
     stats.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    S.run_steps(rt, args.steps, 2, clear, fuse, merge, marks=marks)
+    S.run_steps(rt, args.steps, 2, clear, fuse, merge, marks=marks, phase=phase)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if phase is not None:  # the event is the bench's: unregister it before it goes away
+        _lib.check(L.dmf_fuse_set_phase_event(vol._h, None))
     st = stats.cpu().numpy()
     ev = list(ev.values())
     nct = npad
@@ -441,6 +452,7 @@ def main():
                                 "torch": f"torch {'RCCL' if backend == 'nccl' else backend} all-reduce(sum) + finalize"}[merge_mode] if world > 1
                  else "finalize (no collective at N=1)",
                  "schedule": "merge of step i, then the zeroing of its buffer for step i+2, on the comm stream overlap fuse of step i+1 (2 counter buffers)"
+                             + ("; they wait for step i+1's phase F to begin (dmf_fuse_set_phase_event)" if phase else "")
                              + ("; pass A of fuse i+1 on libdmf's staging stream beside passes B and F of fuse i (the 'fuse' span is the "
                                 "compute stream's: batch cut, B and F after waiting for that pass A)" if pipe else "")}
     # grid-wide streaming passes, priced separately: clear writes the

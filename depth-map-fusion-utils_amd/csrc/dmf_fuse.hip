@@ -1974,10 +1974,11 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
                            (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb);
       DMF_LAUNCH_CHECK();
-      if (staged) {
+      if (staged && j == 0) {  // (batches j > 0 ran on the volume's stream)
         DMF_HIP(hipEventRecord(v->st_b[slot], sa));
         DMF_HIP(hipStreamWaitEvent(v->stream, v->st_b[slot], 0));
       }
+      if (v->f_event && s0 == 0 && j == 0) DMF_HIP(hipEventRecord(v->f_event, v->stream));  // the call's phase F begins
       if (slab)
         hipLaunchKernelGGL((k_bk_fuse_s<kBkRefill, kBkSpread, kBkUnroll>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,
                            (const uint4*)b.pra, (const uint32_t*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
@@ -2168,6 +2169,14 @@ int dmf_fuse_counters_to_linear_device(dmf_volume* v, const int32_t* d_tiled, in
   DMF_API_END
 }
 
+int dmf_fuse_set_phase_event(dmf_volume* v, void* event) {
+  DMF_API_BEGIN
+  if (!v) return fail(DMF_ERR_INVALID, "null volume");
+  v->f_event = (hipEvent_t)event;
+  return DMF_OK;
+  DMF_API_END
+}
+
 int dmf_fuse_set_input_stream(dmf_volume* v, void* stream) {
   DMF_API_BEGIN
   if (!v) return fail(DMF_ERR_INVALID, "null volume");
@@ -2206,6 +2215,7 @@ static int fuse_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_d
     DMF_TRY(fuse_bricks(v, cp, g, d_depth, tab, d_poses, P, prm, d_hits, d_misses, st, d_stats, staged, capturing));
   } else {
     const int pkx = (cp.W + 7) / 8;
+    if (v->f_event) DMF_HIP(hipEventRecord(v->f_event, v->stream));
     hipLaunchKernelGGL((k_fuse_l<12, 1280>), dim3((unsigned)(pkx * ((cp.H + 7) / 8)), (unsigned)P), dim3(64), 0,
                        v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, d_misses, st);
     DMF_LAUNCH_CHECK();

@@ -254,6 +254,7 @@ struct dmf_volume {
   hipEvent_t st_in = nullptr, st_done[2] = {nullptr, nullptr}, st_free[2] = {nullptr, nullptr};
   hipEvent_t st_b[2] = {nullptr, nullptr};  // pass B of the slot's batch enqueued (staged pass B)
   bool st_free_set[2] = {false, false};
+  hipEvent_t f_event = nullptr;  // caller's phase-F event (dmf_fuse_set_phase_event)
   int st_slot = 0;
   // diagnostic / A-B controls (include/dmf_diag.h): fusion implementation and knobs
   int fuse_variant = 0;

@@ -129,6 +129,7 @@ SIGNATURES = {
     "dmf_fuse_counters_to_linear_device": (C.c_int, [_vp, _p, _p]),
     "dmf_fuse_reserve": (C.c_int, [_vp, _p, _i32, C.c_uint64]),
     "dmf_fuse_set_input_stream": (C.c_int, [_vp, _vp]),
+    "dmf_fuse_set_phase_event": (C.c_int, [_vp, _vp]),
     "dmf_fuse_plan": (C.c_int, [_vp, _p, _i32, _p]),
     "dmf_grid_save": (C.c_int, [C.c_char_p, _p, _p]),
     "dmf_grid_load": (C.c_int, [C.c_char_p, _p, _p, _i64]),

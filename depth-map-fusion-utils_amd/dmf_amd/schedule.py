@@ -89,7 +89,7 @@ class SimRuntime:
                 arg.done = True
 
 
-def run_steps(rt, nsteps, nbuf, clear, fuse, merge, marks=None, reuse_wait=True):
+def run_steps(rt, nsteps, nbuf, clear, fuse, merge, marks=None, reuse_wait=True, phase=None):
     """Enqueue `nsteps` steps on runtime `rt` and wait for the last merge.
 
     clear(b), fuse(b, i), merge(b, i) enqueue (or, on the simulator, perform) the work of
@@ -97,13 +97,34 @@ def run_steps(rt, nsteps, nbuf, clear, fuse, merge, marks=None, reuse_wait=True)
     the step's phase boundaries (z0, z1 around the clear that prepares step i's buffer, on
     whichever lane runs it; c1, c2 around the fusion on compute; a0, a1 around the merge
     on comm) for timing.  reuse_wait=False drops the buffer-reuse dependency (tests show it
-    is needed)."""
+    is needed).
+
+    phase(i), if given, returns an event that fuse(b, i) recorded when its phase F begins
+    (dmf_fuse_set_phase_event): the merge of step i - 1 (and the clear behind it) then also
+    waits for it, so that this HBM-bound work runs beside step i's issue-bound phase F rather
+    than beside its passes A / B; the last step's merge follows its fusion."""
     def mark(i, name, lane):
         if marks:
             marks(i, name, lane)
 
     merged = [None] * nbuf
     last = None
+
+    def enqueue_merge(b, i, fused, after=None):
+        nonlocal last
+        rt.wait("comm", fused)
+        if after is not None:
+            rt.wait("comm", after)
+        mark(i, "a0", "comm")
+        rt.enqueue("comm", lambda b=b, i=i: merge(b, i))
+        mark(i, "a1", "comm")
+        if i + nbuf < nsteps:  # zero the buffer for step i + nbuf behind its merge
+            mark(i + nbuf, "z0", "comm")
+            rt.enqueue("comm", lambda b=b: clear(b))
+            mark(i + nbuf, "z1", "comm")
+        merged[b] = last = rt.record("comm")
+
+    pending = None  # (b, i, fused) of the step whose merge waits for the next phase F
     for i in range(nsteps):
         b = i % nbuf
         if reuse_wait and merged[b] is not None:
@@ -116,15 +137,15 @@ def run_steps(rt, nsteps, nbuf, clear, fuse, merge, marks=None, reuse_wait=True)
         rt.enqueue("compute", lambda b=b, i=i: fuse(b, i))
         mark(i, "c2", "compute")
         fused = rt.record("compute")
-        rt.wait("comm", fused)
-        mark(i, "a0", "comm")
-        rt.enqueue("comm", lambda b=b, i=i: merge(b, i))
-        mark(i, "a1", "comm")
-        if i + nbuf < nsteps:  # zero the buffer for step i + nbuf behind its merge
-            mark(i + nbuf, "z0", "comm")
-            rt.enqueue("comm", lambda b=b: clear(b))
-            mark(i + nbuf, "z1", "comm")
-        merged[b] = last = rt.record("comm")
+        if phase is None:
+            enqueue_merge(b, i, fused)
+        else:
+            ph = phase(i)
+            if pending is not None:
+                enqueue_merge(*pending, after=ph)
+            pending = (b, i, fused)
+    if pending is not None:
+        enqueue_merge(*pending)
     if last is not None:
         rt.wait("compute", last)
     rt.drain()

@@ -253,6 +253,14 @@ int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t m
  * serially, and so does the host form dmf_fuse_depth (a captured graph must not be launched
  * while pipelined calls of the same volume are in flight: it reads the serial slot). */
 int dmf_fuse_set_input_stream(dmf_volume* v, void* stream);
+/* Phase-F event: `event` (a hipEvent_t the caller created; NULL = off) is recorded on the
+ * volume's stream of every later fusion call right before its (first) phase F launch -- on
+ * the brick pipeline after the call's pass B, on k_fuse_l before that kernel.  A caller that
+ * pipelines its own steps makes the previous step's merge / finalize wait for it, so that
+ * this HBM-bound work runs beside the issue-bound phase F instead of beside the next call's
+ * passes A / B (bench.py).  The event is re-recorded by each call: wait on
+ * it after the call returns and before the next call. */
+int dmf_fuse_set_phase_event(dmf_volume* v, void* event);
 /* How a fusion call of P frames of `cam`'s size on this volume is executed (no GPU work,
  * no allocation): brick = 1 for the brick-owned pipeline (k_bk_*), 0 for k_fuse_l.  The
  * brick pipeline runs pass A over super-batches of super_batch_poses frames; the DEVICE cuts

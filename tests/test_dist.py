@@ -131,7 +131,7 @@ def test_sharded_visibility_gloo_world2(tmp_path, oracle):
 # restatement of dmf_fuse_merge_finalize_device.  Step i fuses frames {i, i+S} (one per
 # rank), so every step's merged log-odds differ and buffer mix-ups show.
 
-def _sched_worker(rank, world, port, K, depth, poses, n, nsteps, seeds, reuse_wait, out_dir):
+def _sched_worker(rank, world, port, K, depth, poses, n, nsteps, seeds, reuse_wait, out_dir, phase=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "depth-map-fusion-utils_amd")]
@@ -164,7 +164,11 @@ def _sched_worker(rank, world, port, K, depth, poses, n, nsteps, seeds, reuse_wa
             D.merge_finalize_gloo(bufs[b], dims, prm, logodds)
             out[i] = logodds[: n ** 3].clone().numpy()
 
-        S.run_steps(S.SimRuntime(seed), nsteps, 2, clear, fuse, merge, reuse_wait=reuse_wait)
+        rt = S.SimRuntime(seed)
+        # phase: step i-1's merge also waits for an event recorded on compute after step i's
+        # fusion (the simulator's stand-in for the phase-F event of dmf_fuse_set_phase_event)
+        S.run_steps(rt, nsteps, 2, clear, fuse, merge, reuse_wait=reuse_wait,
+                    phase=(lambda i: rt.record("compute")) if phase else None)
         results.append(np.stack([out[i] for i in range(nsteps)]))
     np.save(os.path.join(out_dir, f"sched{rank}.npy"), np.stack(results))
     dist.destroy_process_group()
@@ -190,15 +194,17 @@ def _sched_inputs():
     return K, depth, poses, nsteps
 
 
-def test_step_schedule_gloo_world2(tmp_path, oracle):
+@pytest.mark.parametrize("phase", [False, True])
+def test_step_schedule_gloo_world2(tmp_path, oracle, phase):
     """The pipelined schedule (merge of step i overlapping fuse of step i+1, two counter
-    buffers) on 2 ranks under random stream-consistent execution orders: every step's
+    buffers; phase: the merge of step i deferred behind step i+1's phase-F event, as the bench
+    runs it) on 2 ranks under random stream-consistent execution orders: every step's
     merged, finalized log-odds equal the single-rank fusion of that step's frames."""
     K, depth, poses, nsteps = _sched_inputs()
     n = 21  # odd: a partial last tile row, and 11 tile rows over 2 ranks (padding)
     exp = _sched_expected(oracle, K, depth, poses, n, nsteps)
     seeds = [1, 2, 3, 4]
-    mp.spawn(_sched_worker, args=(2, _free_port(), K, depth, poses, n, nsteps, seeds, True, str(tmp_path)),
+    mp.spawn(_sched_worker, args=(2, _free_port(), K, depth, poses, n, nsteps, seeds, True, str(tmp_path), phase),
              nprocs=2, join=True)
     for r in range(2):
         got = np.load(tmp_path / f"sched{r}.npy")
