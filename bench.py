@@ -415,11 +415,14 @@ def main():
         e.record(rt.lanes[lane])
         ev.setdefault(i, {})[name] = e
 
-    # the merge (finalize / RCCL) and clear of step i wait for step i+1's phase F to begin
+    # the merge (finalize) and clear of step i wait for step i+1's phase F to begin
     # (dmf_fuse_set_phase_event), so that they run beside the issue-bound phase F and not
-    # beside the next call's passes A / B (DMF_BENCH_PHASE=0: right after step i's fusion)
+    # beside the next call's passes A / B (DMF_BENCH_PHASE=0: right after step i's fusion).
+    # At N > 1 the merge is RCCL's reduce-scatter / all-gather, whose kernels may not fit
+    # beside phase F's persistent workgroups; it keeps the round-3 order unless
+    # DMF_BENCH_PHASE=1 asks for the deferral there too.
     phase = None
-    if os.environ.get("DMF_BENCH_PHASE", "1") != "0":
+    if os.environ.get("DMF_BENCH_PHASE", "1" if world == 1 else "0") != "0":
         fev = torch.cuda.Event()
         fev.record(stream)  # creates the event
         _lib.check(L.dmf_fuse_set_phase_event(vol._h, C.c_void_p(fev.cuda_event)))
