@@ -165,6 +165,19 @@ def test_config_full_poses(cfg):
     assert k0.startswith("dmf::k_bk_fuse_s")
 
 
+def test_config5_shard_bench_workload_golden():
+    """Config 5's per-GPU shard size as bench.py runs it at N = 1 (1280x720, 1024^3, the 256
+    poses of fibonacci_poses(256)): the default call -- the slab-walk brick pipeline with pass
+    A's hashed histogram (32768 bricks) -- equals the committed oracle digest of all 256
+    frames (tests/golden/gen_fusion_digests.py config5_shard_N1)."""
+    f = Fusion(1024, 1280, 720, 256)
+    c0, s0, k0 = f.run(0)
+    _invariants(f, c0, s0)
+    assert k0.startswith("dmf::k_bk_fuse_s")
+    g = GOLDEN["config5_shard_N1"]
+    assert f.digest(c0) == g["logodds_digest"] and int(s0[0]) == g["updates"]
+
+
 def test_config3_batches_equal_single_batch():
     """Config 3's frames through the brick pipeline in batches of 7 poses (48 frames: 7
     batches) == the default (one batch: the device's cut by the real pair count)."""
