@@ -64,7 +64,7 @@ if kernels:
             "per_kernel": per_kernel,
             "tcc_ea0_atomic_requests_per_launch": sum(per(k, "TCC_EA0_ATOMIC_sum") for k in kernels),
             "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
-            "kernel_ms_bench": bench["roofline"]["kernel_ms"],
+            "kernel_ms_bench": bench["roofline"].get("step_ms", bench["roofline"].get("kernel_ms")),
             "note": "traffic = sum over the pipeline's kernels of (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch; "
                     "FETCH doubled per MI355X_MICROARCH.md"}
     json.dump(summ, open(os.path.join(dst, "pmc_fuse_summary.json"), "w"), indent=1)
