@@ -259,7 +259,8 @@ int dmf_fuse_set_input_stream(dmf_volume* v, void* stream);
  * pipelines its own steps makes the previous step's merge / finalize wait for it, so that
  * this HBM-bound work runs beside the issue-bound phase F instead of beside the next call's
  * passes A / B (bench.py).  The event is re-recorded by each call: wait on
- * it after the call returns and before the next call. */
+ * it after the call returns and before the next call.  It must stay valid until it is
+ * unregistered (event = NULL) or the volume is destroyed. */
 int dmf_fuse_set_phase_event(dmf_volume* v, void* event);
 /* How a fusion call of P frames of `cam`'s size on this volume is executed (no GPU work,
  * no allocation): brick = 1 for the brick-owned pipeline (k_bk_*), 0 for k_fuse_l.  The
