@@ -686,13 +686,13 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
     const int64_t kr = v->knob[DMF_KNOB_REVERSE_KERNEL];
     // work-queue shape (items per wave, refill threshold, burst): 512 / 8 / 8 in enumeration
     // or insertion order; in spatial order smaller queues pay (neighbouring lanes agree, so
-    // the per-wave tail is the cost): 128 / 8 / 16 measured 5.92 ms vs 6.51 at 512 / 8 / 8
-    // (profiles/r04/reverse_queue_sweep.json)
+    // the per-wave tail is the cost): 64 / 8 / 16 measured 5.54 ms vs 5.94 at 128 / 8 / 16 and
+    // 6.51 at 512 / 8 / 8 (profiles/r04/reverse_queue_sweep.json)
     constexpr int kRevItems = 512, kRevRefill = 8, kRevBurst = 8;
 #if defined(DMF_EXP_REV_ITEMS)  // experiment builds: the spatial-order queue's shape
     constexpr int kSpItems = DMF_EXP_REV_ITEMS, kSpRefill = DMF_EXP_REV_REFILL, kSpBurst = DMF_EXP_REV_BURST;
 #else
-    constexpr int kSpItems = 128, kSpRefill = 8, kSpBurst = 16;
+    constexpr int kSpItems = 64, kSpRefill = 8, kSpBurst = 16;
 #endif
     const dim3 gridq((unsigned)((nelem + 4 * kRevItems - 1) / (4 * kRevItems)), (unsigned)P);
     const dim3 gridqs((unsigned)((nelem + 4 * kSpItems - 1) / (4 * kSpItems)), (unsigned)P);
