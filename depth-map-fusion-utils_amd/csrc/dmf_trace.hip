@@ -805,14 +805,21 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, co
                                                  unsigned long long* __restrict__ hazards,
                                                  unsigned long long* __restrict__ stats) {
   stats = stat_slot(stats);
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // a wave marches an 8x8 tile of lattice pixels (fwd_threads): neighbouring rays in both
+  // directions reach similar depths and read the same bitmask tiles (a row of 64 pixels
+  // spans 8x the angle); outputs stay row-major (idx)
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int tpr = (C + 7) >> 3, ln = (int)(t & 63);
+  const int64_t tile = t >> 6;
+  const int ri = (int)(tile / tpr) * 8 + (ln >> 3), ci = (int)(tile % tpr) * 8 + (ln & 7);
+  const int64_t idx = (int64_t)ri * C + ci;
   // grid.y = pose index of a batched launch (one pose: grid.y = 1)
   pose += blockIdx.y;
   k_out += (int64_t)blockIdx.y * R * C;
   slot_out += (int64_t)blockIdx.y * R * C;
   int64_t samples = 0;
-  if (idx < (int64_t)R * C) {
-    const int r = (int)(idx / C) * rdelta, c = (int)(idx % C) * cdelta;
+  if (ri < R && ci < C) {
+    const int r = ri * rdelta, c = ci * cdelta;
     int32_t kk = -1, sl = -1;
     const float* m = pose->f;
     // the exact line (double estimates) and the error-bound coefficients
@@ -937,6 +944,12 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, co
   if (stats) wave_add_u64(&stats[0], (unsigned long long)samples);
 }
 
+// threads of a k_forward launch per pose: whole 8x8 tiles of the R x C lattice
+static unsigned fwd_blocks(int R, int C) {
+  const int64_t threads = (int64_t)((R + 7) / 8) * ((C + 7) / 8) * 64;
+  return (unsigned)((threads + 255) / 256);
+}
+
 // DMF_KNOB_FWD_SKIP = -1 (dmf_diag.h) disables the forward march's empty-space skipping (A/B)
 static bool fwd_skip(const dmf_volume* v) { return v->knob[DMF_KNOB_FWD_SKIP] >= 0; }
 
@@ -1050,7 +1063,7 @@ static int run_forward(dmf_volume* v, const dmf_camera* cam, const float* pose, 
   const CamP cp = cam_params(cam);
   const Geom g = v->geom();
   const dim3 grid((unsigned)((RC + 255) / 256));
-  DMF_LAUNCH_FORWARD(grid, g, v->dev(), cp, tab, zstart, zdelta, rdelta, cdelta, R, C, (int32_t*)kb, (int32_t*)sb, hz,
+  DMF_LAUNCH_FORWARD(dim3(fwd_blocks(R, C)), g, v->dev(), cp, tab, zstart, zdelta, rdelta, cdelta, R, C, (int32_t*)kb, (int32_t*)sb, hz,
                      nullptr);
   DMF_LAUNCH_CHECK();
   unsigned long long* minkey = nullptr;
@@ -1369,13 +1382,12 @@ int dmf_forward_first_hits_device(dmf_volume* v, const dmf_camera* cam, const fl
   PoseX* tab;
   DMF_TRY(pose_table(v, d_poses, P, true, &tab));
   const int R = (cam->height + rdelta - 1) / rdelta, C = (cam->width + cdelta - 1) / cdelta;
-  const int64_t RC = (int64_t)R * C;
   void* aux;
   DMF_TRY(scratch(v, kScHost2, 64, &aux));
   DMF_HIP(hipMemsetAsync(aux, 0, 64, v->stream));
   unsigned long long* st = nullptr;
   if (d_stats) DMF_TRY(stats_begin(v, &st));
-  DMF_LAUNCH_FORWARD(dim3((unsigned)((RC + 255) / 256), (unsigned)P), v->geom(), v->dev(), cam_params(cam), tab,
+  DMF_LAUNCH_FORWARD(dim3(fwd_blocks(R, C), (unsigned)P), v->geom(), v->dev(), cam_params(cam), tab,
                      zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot, (unsigned long long*)aux, st);
   DMF_LAUNCH_CHECK();
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 1));
@@ -1401,7 +1413,7 @@ int dmf_forward_first_hits(dmf_volume* v, const dmf_camera* cam, const float* po
   DMF_TRY(scratch(v, kScHost2, 64, &aux));
   DMF_HIP(hipMemsetAsync(aux, 0, 64, v->stream));
   const dim3 grid((unsigned)((RC + 255) / 256));
-  DMF_LAUNCH_FORWARD(grid, v->geom(), v->dev(), cam_params(cam), tab, zstart, zdelta, rdelta, cdelta, R, C,
+  DMF_LAUNCH_FORWARD(dim3(fwd_blocks(R, C)), v->geom(), v->dev(), cam_params(cam), tab, zstart, zdelta, rdelta, cdelta, R, C,
                      (int32_t*)kb, (int32_t*)sb, (unsigned long long*)aux, nullptr);
   DMF_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_first_hit_hash, grid, dim3(256), 0, v->stream, (const int32_t*)sb, v->d_hash, RC,
