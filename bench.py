@@ -108,6 +108,49 @@ def cpu_baseline(K, poses, depth, n_frames, grid, threads=1):
     return float(st[0]) / dt, float(st[1]) / dt, dt
 
 
+def reference_fusion_baseline(K, poses, depth, n_frames, grid, budget_s=20.0):
+    """The reference's OWN fusion path on the host, timed on the same frames: per frame the
+    oracle's Camera::projectPoint + transformPoints back-projection (Camera.hpp:24-45, the
+    cloud a reference driver integrates) and VoxelVolume::integratePointCloud(cloud, normals)
+    (Volume.hpp:199-228) in the reference layout -- vector<vector<vector<Voxel*>>>, one `new
+    Voxel` per first touch, push_back of every point and normal -- single-threaded, as the
+    reference is.  The reference integrates each point into ONE voxel (no ray traversal), so
+    its ray-voxel updates are its points.  Frames run until `budget_s` is spent (at most
+    n_frames).  Normals are unit vectors (their values do not change the work)."""
+    from oracle import oracle as O
+    v = O.Volume()
+    v.setDimensions(-0.5, 0.5, -0.5, 0.5, -0.5, 0.5)
+    v.setVolumeSize(grid, grid, grid)
+    v.constructVolume()
+    t_bp = t_int = 0.0
+    npts = nfr = 0
+    for i in range(n_frames):
+        t0 = time.perf_counter()
+        xyz = O.backproject(K, depth[i], poses[i])
+        m = depth[i] > 0
+        pts = np.ascontiguousarray(xyz[m])
+        t1 = time.perf_counter()
+        nrm = np.zeros_like(pts)
+        nrm[:, 2] = 1.0
+        t2 = time.perf_counter()
+        v.integratePointCloud(pts, nrm)
+        t3 = time.perf_counter()
+        t_bp += t1 - t0
+        t_int += t3 - t2
+        npts += int(pts.shape[0])
+        nfr += 1
+        if t_bp + t_int > budget_s:
+            break
+    return {"value": npts / (t_bp + t_int), "unit": "ray-voxel updates/s (= points/s: one voxel per point)",
+            "cores": 1, "kind": "port",
+            "integrate_points_per_s": npts / t_int, "backproject_points_per_s": npts / t_bp,
+            "occupied_voxels": len(v.occupied_cells_),
+            "sample": f"oracle reference-layout back-projection + integratePointCloud(cloud, normals) of {nfr} of the "
+                      f"{len(poses)} frames ({npts} points, {grid}^3), {t_bp + t_int:.1f}s single-threaded "
+                      f"(integrate {t_int:.1f}s, back-projection {t_bp:.1f}s); the reference's own fusion, "
+                      "Volume.hpp:199-228"}
+
+
 # PMC passes of the live measurement (one rocprofv3 run each; FETCH_SIZE takes 3 of the 4
 # TCC slots and WRITE_SIZE 2, so they cannot share a pass: MI355X_MICROARCH.md §PMC slots)
 PMC_PASSES = (["FETCH_SIZE"], ["WRITE_SIZE"],
@@ -246,7 +289,9 @@ def expected_digest(grid, P_total):
 def host_cores():
     """The GPU box host's CPUs as the OS reports them (nproc / lscpu), beside the threads the
     CPU baselines used (the job's share, host_threads)."""
-    info = {"os_cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    info = {"os_cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "physical_cores_in_affinity": physical_cores_in_affinity(), "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
     try:
         out = subprocess.run(["lscpu"], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=10,
                              text=True).stdout
@@ -259,11 +304,94 @@ def host_cores():
     return info
 
 
-def host_threads():
-    """Threads for the multi-core CPU baseline: the job's CPU share (OMP_NUM_THREADS on
-    the GPU box), not the whole machine that os.cpu_count() reports there."""
-    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return max(1, min(n if n > 0 else (os.cpu_count() or 1), 16))
+def cgroup_cpu_quota():
+    """CPUs the job's cgroup may use (cpu.max quota / period), or None when unlimited."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, p = open(path).read().split()[:2]
+            if q != "max":
+                return float(q) / float(p)
+        except (OSError, ValueError):
+            pass
+    try:  # cgroup v1
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0 and p > 0:
+            return q / p
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def physical_cores_in_affinity():
+    """Distinct physical cores (socket, core id) among the CPUs this process may run on."""
+    cpus = sorted(os.sched_getaffinity(0))
+    seen = set()
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            seen.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            seen.add(("?", str(c)))
+    return len(seen)
+
+
+def host_threads(requested=0):
+    """Threads for the multi-core CPU baselines: the physical cores of the affinity mask (one
+    thread per core), bounded by the job's CPU share where the host enforces one -- a cgroup
+    quota, or OMP_NUM_THREADS (the GPU box exports its share there: 16 per GPU) -- since threads
+    beyond the share only time-slice.  `requested` > 0 overrides.  Returns (threads, reason)."""
+    if requested > 0:
+        return requested, "--cpu-threads"
+    cores = physical_cores_in_affinity()
+    quota = cgroup_cpu_quota()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    n, why = cores, f"physical cores in the affinity mask ({cores})"
+    if quota is not None and int(quota) < n:
+        n, why = max(1, int(quota)), f"cgroup cpu.max quota {quota:g} CPUs < {cores} physical cores"
+    if omp > 0 and omp < n:
+        n, why = omp, f"OMP_NUM_THREADS={omp} (the job's CPU share) < {cores} physical cores"
+    return max(1, n), why
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(args, argv):
+    """The torch.distributed.run command of `bench.py --gpus N` (N > 1, no WORLD_SIZE): one rank
+    per GPU of this node, rendezvous on 127.0.0.1, every bench argument forwarded unchanged
+    (--print-launch dropped)."""
+    fwd = [a for a in argv if a != "--print-launch"]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + fwd
+
+
+def launch_ranks(args, json_fd):
+    """Spawn the N ranks as a child process, relay rank 0's JSON line on the real stdout and
+    return the child's exit status.  The child's stderr passes through (progress, RCCL)."""
+    cmd = launch_command(args, sys.argv[1:])
+    if args.print_launch:
+        os.write(json_fd, (json.dumps({"launch": cmd}) + "\n").encode())
+        return 0
+    log(f"bench: starting {args.gpus} ranks: {' '.join(cmd)}")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL)
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env)
+    lines = [ln for ln in proc.stdout.decode(errors="replace").splitlines() if ln.strip()]
+    out = [ln for ln in lines if ln.lstrip().startswith("{") and '"metric"' in ln]
+    for ln in lines:
+        if ln not in out:
+            log(f"[ranks stdout] {ln}")
+    if out:
+        os.write(json_fd, (out[-1].strip() + "\n").encode())
+    elif proc.returncode == 0:
+        log("bench: the ranks exited 0 but rank 0 printed no JSON line")
+        return 1
+    return proc.returncode
 
 
 def main():
@@ -290,15 +418,27 @@ def main():
                     help="poses of the multi-core reverseRayTraceFast CPU sample (0 = skip both samples)")
     ap.add_argument("--image", default="640x480", choices=["640x480", "1280x720"],
                     help="depth frame size (BASELINE configs 1/2/4: 640x480; 3/5: 1280x720)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the multi-core CPU baselines (0 = the job's CPU share, host_threads())")
+    ap.add_argument("--print-launch", action="store_true",
+                    help="--gpus N > 1 without WORLD_SIZE: print the torch.distributed.run command the bench would "
+                         "spawn (JSON) and exit")
     args = ap.parse_args()
     global WIDTH, HEIGHT
     WIDTH, HEIGHT = (int(v) for v in args.image.split("x"))
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` starts its own N ranks: torch.distributed.run as a CHILD
+        # process (never exec: nothing here has touched the GPU yet, and nothing will in this
+        # parent), whose rank 0 prints the JSON line; the parent relays it and exits with the
+        # child's status
+        sys.exit(launch_ranks(args, json_fd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch N ranks with --gpus N "
+                         "(or run `python bench.py --gpus N` without a launcher: it starts the ranks itself)")
     # DMF_BENCH_BACKEND=gloo rehearses the N > 1 path with ranks sharing GPUs (no RCCL: the
     # merge falls back to torch's all-reduce + finalize); the driver's runs use nccl (= RCCL)
     backend = os.environ.get("DMF_BENCH_BACKEND", "nccl")
@@ -468,8 +608,9 @@ def main():
         fin_bytes = 10 * ncell
         streaming["finalize"] = {"ms": merge_ms, "bytes": fin_bytes, "GBps": fin_bytes / (merge_ms * 1e-3) / 1e9,
                                  "frac": fin_bytes / (merge_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
-    if st[3] != 0:
-        raise RuntimeError(f"DDA guard tripped {st[3]} times")
+    if st[3] != 0:  # pass B's device-side layout check (dmf_fuse_status): the counters are invalid
+        raise RuntimeError(f"fusion layout check failed {st[3]} times")
+    _lib.fuse_status(vol)  # raises DmfError(DMF_ERR_DEVICE_CHECK) if any call disagreed
     elapsed = D.max_over_ranks(elapsed, device=dev)
     updates, rays, hits = D.sum_over_ranks(st[:3], device=dev)
 
@@ -506,19 +647,23 @@ def main():
         secondary = {}
         if not args.no_secondary:
             secondary = secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses, depth,
-                                          cpu_poses=args.cpu_reverse_poses if world == 1 else 0)
-        cpu = cpu_mt = None
+                                          cpu_poses=args.cpu_reverse_poses if world == 1 else 0,
+                                          cpu_threads=args.cpu_threads, world=world)
+        cpu = cpu_mt = cpu_ref = None
         if args.cpu_frames > 0 and world == 1:
             ups, rps, dt = cpu_baseline(K, poses, depth, args.cpu_frames, grid)
             cpu = {"value": ups, "unit": "ray-voxel updates/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle fuse of {args.cpu_frames} of the {P} frames ({WIDTH}x{HEIGHT}, {grid}^3), "
+                   "sample": f"oracle 3D-DDA fuse (this engine's spec, DESIGN.md 4: the reference has no DDA) of "
+                             f"{args.cpu_frames} of the {P} frames ({WIDTH}x{HEIGHT}, {grid}^3), "
                              f"{dt:.1f}s single-threaded; Mrays/s {rps / 1e6:.3f}"}
-            nt = host_threads()
-            nf = min(P, 4 * args.cpu_frames)
+            nt, nt_why = host_threads(args.cpu_threads)
+            nf = min(P, max(4 * args.cpu_frames, nt))
             ups_mt, rps_mt, dt_mt = cpu_baseline(K, poses, depth, nf, grid, threads=nt)
             cpu_mt = {"value": ups_mt, "unit": "ray-voxel updates/s", "cores": nt, "kind": "port",
+                      "threads_basis": nt_why,
                       "sample": f"oracle fuse (OpenMP rows, atomic counters) of {nf} of the {P} frames, "
                                 f"{dt_mt:.1f}s on {nt} threads; Mrays/s {rps_mt / 1e6:.3f}"}
+            cpu_ref = reference_fusion_baseline(K, poses, depth, P, grid)
         kname = _lib.kernel_name(vol)
         if kname.startswith("dmf::k_bk_fuse"):
             # brick-owned pipeline: step_ms spans every launch of the call
@@ -590,6 +735,8 @@ def main():
                          "updates_per_launch": upd_launch, "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "cpu_baseline_multicore": cpu_mt,
+            # the reference's own fusion (integratePointCloud, one voxel per point) on the same frames
+            "cpu_baseline_reference": cpu_ref,
             "host_cores": host_cores(),
             "step_breakdown_ms": breakdown,
             "streaming": streaming,
@@ -686,9 +833,10 @@ def reverse_cpu_baseline(grid, K, poses, pts, nrm, n_threads, n_poses):
     V = len(ov.occupied_cells_)
     eng = O.Engine(K)
     t0 = time.perf_counter()
-    eng.reverseRayTraceFast(ov, poses[0], False, dead_work=True)
+    _, good0 = eng.reverseRayTraceFast(ov, poses[0], False, dead_work=True)
     dt1 = time.perf_counter() - t0
     out = {"value": V / dt1, "unit": "voxel-pose evaluations/s", "cores": 1, "kind": "port",
+           "_pose0_good": good0, "_occupied": ov.occupied_cells_,
            "sample": f"oracle reverseRayTraceFast (reference layout, dead getNeighborHashes kept) of 1 of the "
                      f"{len(poses)} poses over the same {V}-voxel volume, {dt1:.1f}s single-threaded"}
     if n_poses > 0 and n_threads > 1:
@@ -703,10 +851,38 @@ def reverse_cpu_baseline(grid, K, poses, pts, nrm, n_threads, n_poses):
     return out
 
 
-def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses_h, depth_h, n_int=16, cpu_poses=16):
+MARCH_GOLDEN = os.path.join(ROOT, "tests", "golden", "march_digests.json")
+
+
+def march_digest(a):
+    """sha256 of an array's bytes, first 16 hex digits (tests/golden/gen_march_digests.py)."""
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+def expected_march(grid, P, n_int, Vc, world):
+    """The oracle's digests of this run's secondary workload (tests/golden/gen_march_digests.py),
+    or None: only the N = 1 pose set (rank 0's poses at N > 1 are another shard) was generated."""
+    if world != 1:
+        return None
+    try:
+        table = json.load(open(MARCH_GOLDEN))
+    except (OSError, ValueError):
+        return None
+    for key, e in table.items():
+        if (e["grid"], e["image"], e["poses"], e["seed"], e["integrated_frames"], e["costmap_centres"]) == (
+                grid, f"{WIDTH}x{HEIGHT}", P, 1234, n_int, Vc):
+            return dict(e, key=key)
+    return None
+
+
+def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses_h, depth_h, n_int=16, cpu_poses=16,
+                      cpu_threads=0, world=1):
     """reverseRayTraceFast (RayTracingEngine.hpp:136-226) throughput for the same poses over a
     volume integrated from n_int back-projected frames (march samples/s, voxel-rays/s), with
-    the reference-layout CPU port timed beside it (cpu_poses > 0)."""
+    the reference-layout CPU port timed beside it (cpu_poses > 0), the forward march's first
+    hits and the run_tsp cost map; each output is checked against the oracle's digest of the
+    same workload (tests/golden/march_digests.json) and the reverse CPU leg's pose-0 list
+    against the GPU's."""
     import ctypes as C
     H, W = HEIGHT, WIDTH
     xyz = torch.empty((n_int, H, W, 3), dtype=torch.float32, device=dev)
@@ -780,11 +956,7 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses_h,
     # ordered pairs of 1024 camera centres on a 0.45 m sphere inside the volume (the
     # createCameraLocationsFromSphere layout), one launch
     Vc = 1024
-    rng = np.random.default_rng(11)
-    dirs = rng.normal(size=(Vc, 3))
-    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
-    cp = np.tile(np.eye(3, 4, dtype=np.float32).reshape(1, 12), (Vc, 1))
-    cp[:, 3::4] = (0.45 * dirs).astype(np.float32)
+    cp = scene.sphere_centres(Vc)
     d_cp = torch.from_numpy(cp).to(dev)
     cmap = torch.empty((Vc, Vc), dtype=torch.int32, device=dev)
 
@@ -800,13 +972,42 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses_h,
     torch.cuda.synchronize(dev)
     cm_ms = h0.elapsed_time(h1)
     collided = int((cmap == 0x7FFFFFFF).sum().item())
+    # exactness at the timed size: digests of the GPU outputs against the oracle's
+    # (tests/golden/gen_march_digests.py) -- the occupied list, the good masks (P x words
+    # uint64 over occupied_cells_ slots), the forward (k, slot) maps, the cost map
+    occ = vol.occupied_cells_
+    got = {"occupied_digest": march_digest(np.asarray(occ, np.uint64)),
+           "reverse_good_digest": march_digest(good.cpu().numpy().view(np.uint64).reshape(P, words)),
+           "forward_k_digest": march_digest(kbuf.cpu().numpy()),
+           "forward_slot_digest": march_digest(sbuf.cpu().numpy()),
+           "costmap_digest": march_digest(cmap.cpu().numpy())}
+    gold = expected_march(vol.dims[0], P, n_int, Vc, world)
+
+    def check(*keys):
+        d = {k: got[k] for k in keys}
+        d["digest_match"] = all(got[k] == gold[k] for k in keys) if gold else None
+        d["digest_source"] = (f"oracle (CPU restatement) on the same workload, tests/golden/march_digests.json"
+                              f"[{gold['key']}]") if gold else "no committed oracle digest for this workload"
+        return d
     rev_cpu = None
     if cpu_poses > 0:
         rev_cpu = reverse_cpu_baseline(vol.dims[0], K, poses_h, pts.cpu().numpy(), d_nrm.cpu().numpy(),
-                                       host_threads(), cpu_poses)
+                                       host_threads(cpu_threads)[0], cpu_poses)
+        # per-run check, for free: the CPU leg's pose-0 good list (the oracle on the volume it
+        # integrated from the same points) against the GPU's pose-0 mask, and the two
+        # occupied_cells_ lists
+        g0 = good[:words].cpu().numpy().view(np.uint64)
+        slots = np.nonzero(np.unpackbits(g0.view(np.uint8), bitorder="little")[:V])[0]
+        gpu_list = np.asarray(occ, np.uint64)[slots]
+        ref_occ = rev_cpu.pop("_occupied")
+        ref_list = np.asarray(rev_cpu.pop("_pose0_good"), np.uint64)
+        rev_cpu["pose0_list_match"] = bool(np.array_equal(gpu_list, ref_list) and
+                                           np.array_equal(np.asarray(occ, np.uint64), np.asarray(ref_occ, np.uint64)))
+        rev_cpu["pose0_good"] = int(ref_list.size)
+    forward.update(check("forward_k_digest", "forward_slot_digest"))
     return {"greedy_set_cover": {"candidates": P, "selected": int(nsel.value), "ms": cover_ms},
             "collision_cost_map": {"centres": Vc, "pairs": Vc * Vc, "collided_pairs": collided, "ms": cm_ms,
-                                   "pairs_per_s": Vc * Vc / (cm_ms * 1e-3)},
+                                   "pairs_per_s": Vc * Vc / (cm_ms * 1e-3), **check("costmap_digest")},
             "forward_first_hits": forward,
             "reverse_ray_trace_fast": {
         "occupied_voxels": int(V), "poses": P, "ms_per_batch": ms,
@@ -817,6 +1018,7 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses_h,
         "roofline": None,  # issue-bound pricing from the PMC passes (attach_pmc); the march reads an
                            # L2-resident bitmask, so SURVEY 8d's 2 B per sample is reported, not a bound:
         "algorithmic_bytes_per_launch": bytes_launch,
+        **check("occupied_digest", "reverse_good_digest"),
         **({"diagnostics": dict(zip(REV_DIAG, (float(x) for x in s[2:2 + len(REV_DIAG)])))} if s[2:].any() else {})}}
 
 

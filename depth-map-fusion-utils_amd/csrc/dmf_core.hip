@@ -118,17 +118,22 @@ int stats_begin(dmf_volume* v, unsigned long long** striped) {
   return DMF_OK;
 }
 
-__global__ void k_stats_reduce(const unsigned long long* __restrict__ s, int n, unsigned long long* __restrict__ out) {
+// fault (may be null): the volume's fault words; word 1 (faults not yet reported in a call's
+// statistics) is taken atomically into counter 3
+__global__ void k_stats_reduce(const unsigned long long* __restrict__ s, int n, unsigned long long* __restrict__ out,
+                               uint32_t* fault) {
   const int c = threadIdx.x;
   if (c >= n) return;
   unsigned long long t = 0;
   for (int k = 0; k < kStatSlots; ++k) t += s[k * kStatWidth + c];
+  if (c == 3 && fault) t += atomicExch(&fault[1], 0u);
   out[c] += t;
 }
 
-int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int n) {
+int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int n, uint32_t* fault) {
   if (!d_user) return DMF_OK;
-  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(64), 0, v->stream, striped, n, (unsigned long long*)d_user);
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(64), 0, v->stream, striped, n, (unsigned long long*)d_user,
+                     fault);
   DMF_LAUNCH_CHECK();
   return DMF_OK;
 }
@@ -672,7 +677,8 @@ static void free_state(dmf_volume* v) {
   auto f = [&](void* p) { if (p) (void)hipFree(p); };
   f(v->d_occ); f(v->d_brick); f(v->d_bdist); f(v->d_slot_of); f(v->d_hash); f(v->d_view); f(v->d_good);
   f(v->d_pts); f(v->d_pnrm); f(v->d_pslot); f(v->d_off); f(v->d_csr_nrm); f(v->d_csr_pts);
-  f(v->d_axes); f(v->d_enum); f(v->d_sorder);
+  f(v->d_axes); f(v->d_enum); f(v->d_sorder); f(v->d_fault);
+  v->d_fault = nullptr;
   v->d_sorder = nullptr;
   v->sorder_cap = 0;
   v->sorder_valid = false;
@@ -701,6 +707,7 @@ const char* dmf_status_string(int s) {
     case DMF_ERR_CAPACITY: return "output buffer too small";
     case DMF_ERR_RANGE: return "size out of range";
     case DMF_ERR_NO_DEVICE: return "no usable GPU";
+    case DMF_ERR_DEVICE_CHECK: return "device-side consistency check failed";
     default: return "unknown status";
   }
 }

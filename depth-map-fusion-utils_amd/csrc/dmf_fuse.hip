@@ -715,9 +715,11 @@ __device__ inline void bk_rays_wg(const BkRaysArgs& A_, unsigned wg, uint32_t* h
     return;
   }
   uint32_t* const pc = A_.pose_cnt + (size_t)pw * bg.nbricks;
-  // the workgroup's touched bricks: [count | uint16 brick ids] (pass B initialises only these)
+  // the workgroup's touched bricks: [count | uint16 brick ids | uint32 pair counts] (pass B
+  // initialises only these, and checks the slots it took per brick against the counts)
   uint32_t* const row = A_.wg_list + (size_t)wg * (size_t)A_.wgl_stride;
   uint16_t* const ids = (uint16_t*)(row + 1);
+  uint32_t* const cnts = row + 1 + (bg.nbricks + 1) / 2;
   unsigned long long mine = 0;
   for (int i = threadIdx.x; i < nwords; i += blockDim.x) {
     uint32_t b, n;
@@ -735,13 +737,17 @@ __device__ inline void bk_rays_wg(const BkRaysArgs& A_, unsigned wg, uint32_t* h
         const uint32_t bb = 2u * (uint32_t)i + (uint32_t)hh, nn = (n >> (16 * hh)) & 0xffffu;
         if (nn) {
           A_.wg_base[(size_t)wg * bg.nbricks + bb] = atomicAdd(&pc[bb], nn);
-          ids[atomicAdd(&sh[0], 1u)] = (uint16_t)bb;
+          const uint32_t k = atomicAdd(&sh[0], 1u);
+          ids[k] = (uint16_t)bb;
+          cnts[k] = nn;
           mine += nn;
         }
       }
     } else if (n) {
       A_.wg_base[(size_t)wg * bg.nbricks + b] = atomicAdd(&pc[b], n);
-      ids[atomicAdd(&sh[0], 1u)] = (uint16_t)b;
+      const uint32_t k = atomicAdd(&sh[0], 1u);
+      ids[k] = (uint16_t)b;
+      cnts[k] = n;
       mine += n;
     }
   }
@@ -986,13 +992,20 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
                                                          const uint32_t* __restrict__ wg_base,
                                                          const uint32_t* __restrict__ bt, int j,
                                                          const uint32_t* __restrict__ wg_list, int wgl_stride,
-                                                         uint4* __restrict__ pa, void* __restrict__ pbv) {
+                                                         uint4* __restrict__ pa, void* __restrict__ pbv,
+                                                         const unsigned long long* __restrict__ ctl,
+                                                         uint32_t* __restrict__ fault, int inject) {
   uint2* const pb = (uint2*)pbv;
   uint32_t* const pw = (uint32_t*)pbv;
   extern __shared__ uint32_t hist[];
+  __shared__ uint32_t s_inj;  // DMF_KNOB_FAULT_INJECT: the extra slots not yet taken
   // the workgroups of pass A (one pose each); only those of batch j's poses run
   const int pz = (int)(blockIdx.x / (unsigned)wg_pose);
   if ((uint32_t)j >= bt[0] || (uint32_t)pz < bt[1 + j] || (uint32_t)pz >= bt[2 + j]) return;
+  // the batch's pair records: a slot at or past `total` (passes A and B disagree) is never
+  // stored, and the end of the kernel checks the slots taken per brick against pass A
+  const uint32_t total = (uint32_t)ctl[0];
+  if (threadIdx.x == 0) s_inj = (inject > 0 && j == 0 && blockIdx.x == 0) ? (uint32_t)inject : 0u;
   // this workgroup's range in brick i starts at off[i] + pose_base[p][i] + wg_base[wg][i]
   // (k_bk_scan, k_bk_batch_counts, pass A); only the bricks pass A counted for this
   // workgroup are initialised (1024^3: 32768 bricks, ~300 touched)
@@ -1073,6 +1086,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
       return bk_lds_word(x, y, z);
     };
     auto put = [&](uint32_t slot, uint4 e, uint32_t last, uint32_t steps, bool ends) {
+      if (slot >= total) return;  // only when A and B disagree (reported by the check below)
       if constexpr (SLAB) {
         uint32_t w[5];
         bk::pack20((int32_t)e.x, (int32_t)e.y, (int32_t)e.z, aM, a1, a2, e.w, last, steps, signs >> 22, (uint32_t)M,
@@ -1127,9 +1141,28 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
         ci1 = c[1];
         ci2 = c[2];
       }
-      slot = atomicAdd(&hist[b], 1u);
+      uint32_t take = 1u;
+      if (inject > 0 && s_inj) take += atomicExch(&s_inj, 0u);  // test hook only (uniform kernel argument)
+      slot = atomicAdd(&hist[b], take);
     });
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
+  }
+  // layout check: the slots taken in each touched brick must be pass A's count for it
+  __syncthreads();
+  {
+    const uint32_t* row = wg_list + (size_t)blockIdx.x * (size_t)wgl_stride;
+    const uint32_t nl = row[0];
+    const uint16_t* ids = (const uint16_t*)(row + 1);
+    const uint32_t* cnts = row + 1 + (bg.nbricks + 1) / 2;
+    uint32_t bad = 0;
+    for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x) {
+      const int i = ids[k];
+      bad += hist[i] != off[i] + pbz[i] + wb[i] + cnts[k] ? 1u : 0u;
+    }
+    if (bad) {
+      atomicAdd(&fault[0], bad);
+      atomicAdd(&fault[1], bad);
+    }
   }
 }
 
@@ -1719,7 +1752,8 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   pl.wg_pose = (int)((pl.ppose + pl.span - 1) / pl.span);
   pl.hist_bytes = sizeof(uint32_t) * (size_t)pl.bg.nbricks;
   // per pose: ray records, per-workgroup brick bases, pose counts and bases, pose pairs + batch table
-  pl.wgl_stride = 1 + (pl.bg.nbricks + 1) / 2;  // touched-brick list per workgroup: count + uint16 ids
+  // touched-brick list per workgroup: count + uint16 ids + uint32 pair counts (pass B's layout check)
+  pl.wgl_stride = 1 + (pl.bg.nbricks + 1) / 2 + pl.bg.nbricks;
   pl.per_pose_bytes = (uint64_t)rays_pose * (sizeof(ulonglong2) + sizeof(uint64_t)) + (uint64_t)pl.wg_pose * pl.hist_bytes +
                       (uint64_t)pl.wg_pose * sizeof(uint32_t) * (uint64_t)pl.wgl_stride + 2 * (uint64_t)pl.hist_bytes +
                       sizeof(unsigned long long) + sizeof(uint32_t);
@@ -1873,6 +1907,18 @@ static int stage_init(dmf_volume* v) {
   return DMF_OK;
 }
 
+// The volume's two fault words (dmf_fuse_status), zeroed once when first needed (the volume's
+// stream is synchronised then: every stream that later reads them is ordered after it).
+static int fault_words(dmf_volume* v) {
+  if (v->d_fault) return DMF_OK;
+  void* p = nullptr;
+  DMF_HIP(hipMalloc(&p, 2 * sizeof(uint32_t)));
+  v->d_fault = (uint32_t*)p;
+  DMF_HIP(hipMemsetAsync(p, 0, 2 * sizeof(uint32_t), v->stream));
+  DMF_HIP(hipStreamSynchronize(v->stream));
+  return DMF_OK;
+}
+
 static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint16_t* d_depth, const PoseX* tab,
                        const float* d_poses, int P, const dmf_fuse_params* prm, int32_t* d_hits, int32_t* d_misses,
                        unsigned long long* st, uint64_t* d_user, bool staged, bool capturing) {
@@ -1880,6 +1926,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   DMF_TRY(bk_plan(v, cp, g, P, pl));
   const BkGeom& bg = pl.bg;
   DMF_TRY(bk_attributes());
+  DMF_TRY(fault_words(v));
   BkBufs b;
   if (staged) DMF_TRY(stage_init(v));
   const bool slab = v->fuse_variant != DMF_FUSE_CELL_WALK;
@@ -1967,12 +2014,14 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sj, (int)pl.ppose,
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
-                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb);
+                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb, (const unsigned long long*)b.ctl,
+                           v->d_fault, (int)std::min<int64_t>(v->knob[DMF_KNOB_FAULT_INJECT], 1 << 20));
       else
         hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sj, (int)pl.ppose,
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
-                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb);
+                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb, (const unsigned long long*)b.ctl,
+                           v->d_fault, (int)std::min<int64_t>(v->knob[DMF_KNOB_FAULT_INJECT], 1 << 20));
       DMF_LAUNCH_CHECK();
       if (staged && j == 0) {  // (batches j > 0 ran on the volume's stream)
         DMF_HIP(hipEventRecord(v->st_b[slot], sa));
@@ -2092,6 +2141,7 @@ int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t m
     BkPlan pl;
     DMF_TRY(bk_plan(v, cp, g, P, pl));
     DMF_TRY(bk_attributes());
+    DMF_TRY(fault_words(v));
     BkBufs set;
     DMF_TRY(bk_scratch(v, pl, set, 0));
     if (v->pipelined) {  // the second staging slot, the staging stream, slot pose tables and statistics
@@ -2221,9 +2271,29 @@ static int fuse_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_d
     DMF_LAUNCH_CHECK();
     v->last_kernel = kNameLds;
   }
-  if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth));
+  // (brick pipeline: the layout faults not yet reported go to d_stats[3])
+  if (d_stats) DMF_TRY(stats_end(v, st, d_stats, kStatWidth, brick ? v->d_fault : nullptr));
   DMF_LAUNCH_CHECK();
   return DMF_OK;
+}
+
+// Reads and clears the volume's layout-fault count (synchronises the volume's streams).
+static int take_faults(dmf_volume* v, uint64_t* faults) {
+  uint32_t f = 0;
+  if (v->d_fault) {
+    if (v->stage) DMF_HIP(hipStreamSynchronize(v->stage));
+    DMF_HIP(hipMemcpyAsync(&f, v->d_fault, sizeof(f), hipMemcpyDeviceToHost, v->stream));
+    DMF_HIP(hipStreamSynchronize(v->stream));
+    if (f) {
+      DMF_HIP(hipMemsetAsync(v->d_fault, 0, sizeof(uint32_t), v->stream));
+      DMF_HIP(hipStreamSynchronize(v->stream));
+    }
+  }
+  if (faults) *faults = f;
+  return f ? fail(DMF_ERR_DEVICE_CHECK,
+                  "brick pipeline layout check: %u workgroup-brick slot ranges disagreed with pass A (the fusion "
+                  "counters of the calls since the last check are invalid)", f)
+           : DMF_OK;
 }
 }  // namespace dmf
 
@@ -2278,9 +2348,19 @@ int dmf_fuse_depth(dmf_volume* v, const dmf_camera* cam, const uint16_t* depth, 
   DMF_HIP(hipMemcpyAsync(misses, lin, sizeof(int32_t) * v->ncell, hipMemcpyDeviceToHost, v->stream));
   DMF_HIP(hipMemcpyAsync(st, ds, sizeof(st), hipMemcpyDeviceToHost, v->stream));
   DMF_HIP(hipStreamSynchronize(v->stream));
+  DMF_TRY(take_faults(v, nullptr));
   if (stats)
     for (int k = 0; k < 3; ++k) stats[k] += (int64_t)st[k];
   return DMF_OK;
+  DMF_API_END
+}
+
+int dmf_fuse_status(dmf_volume* v, uint64_t* faults) {
+  DMF_API_BEGIN
+  if (faults) *faults = 0;
+  DMF_TRY(require_constructed(v));
+  DMF_TRY(activate(v));
+  return take_faults(v, faults);
   DMF_API_END
 }
 

@@ -73,7 +73,8 @@ constexpr int kStatSlots = 256, kStatWidth = 20;  // diagnostic builds: extra co
 constexpr int kStatSlots = 256, kStatWidth = 8;
 #endif
 int stats_begin(dmf_volume* v, unsigned long long** striped);
-int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int ncounters);
+int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int ncounters,
+              uint32_t* fault = nullptr);
 __device__ inline unsigned long long* stat_slot(unsigned long long* base) {
   return base ? base + kStatWidth * ((blockIdx.x + blockIdx.y * gridDim.x) & (kStatSlots - 1)) : nullptr;
 }

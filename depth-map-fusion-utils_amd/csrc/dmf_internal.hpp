@@ -256,6 +256,9 @@ struct dmf_volume {
   bool st_free_set[2] = {false, false};
   hipEvent_t f_event = nullptr;  // caller's phase-F event (dmf_fuse_set_phase_event)
   int st_slot = 0;
+  // device-side layout check of the brick pipeline (dmf_fuse_status): [0] disagreements since
+  // the last dmf_fuse_status, [1] those not yet added to a call's d_stats[3]
+  uint32_t* d_fault = nullptr;
   // diagnostic / A-B controls (include/dmf_diag.h): fusion implementation and knobs
   int fuse_variant = 0;
   const char* last_kernel = nullptr;  // the fusion kernel of the latest call

@@ -28,6 +28,7 @@ DMF_ERR_NOMEM = 4
 DMF_ERR_CAPACITY = 5
 DMF_ERR_RANGE = 6
 DMF_ERR_NO_DEVICE = 7
+DMF_ERR_DEVICE_CHECK = 8
 
 
 class DmfError(RuntimeError):
@@ -134,6 +135,7 @@ SIGNATURES = {
     "dmf_grid_save": (C.c_int, [C.c_char_p, _p, _p]),
     "dmf_grid_load": (C.c_int, [C.c_char_p, _p, _p, _i64]),
     "dmf_fuse_batches_used": (C.c_int, [_vp, _p]),
+    "dmf_fuse_status": (C.c_int, [_vp, _p]),
     "dmf_rccl_version": (C.c_int, [_p]),
     "dmf_comm_unique_id": (C.c_int, [_p]),
     "dmf_comm_init_rank": (C.c_int, [_p, _i32, _p, _i32, _i32]),
@@ -216,7 +218,15 @@ def declared_symbols():
 # include/dmf_diag.h: fusion implementations and per-volume knobs (diagnostics, A/B, tests)
 FUSE_DEFAULT, FUSE_LDS_BOX, FUSE_CELL_WALK, FUSE_SLAB = 0, 31, 40, 57
 KNOBS = {"super_poses": 1, "pair_cap": 2, "batch_poses": 3, "part_max": 4, "span": 5, "tail_split": 6,
-         "reverse_kernel": 7, "fwd_skip": 8, "a_hash": 9}
+         "reverse_kernel": 7, "fwd_skip": 8, "a_hash": 9, "fault_inject": 10}
+
+
+def fuse_status(vol):
+    """dmf_fuse_status: raises DmfError (DMF_ERR_DEVICE_CHECK) when a fusion call of this volume
+    since the last check failed the device-side pair-layout check; returns the fault count (0)."""
+    f = C.c_uint64(0)
+    check(load().dmf_fuse_status(getattr(vol, "_h", vol), C.addressof(f)))
+    return f.value
 
 
 def set_variant(vol, variant):

@@ -231,3 +231,15 @@ def render_frames(K, width, height, poses, dmin=DEPTH_MIN_MM, dmax=DEPTH_MAX_MM,
 def grid_bounds(n):
     """bounds [-0.5, 0.5]^3 with n cells per axis (exact binary deltas)."""
     return (-0.5, 0.5, -0.5, 0.5, -0.5, 0.5), (n, n, n)
+
+
+def sphere_centres(V=1024, radius=0.45, seed=11):
+    """(V, 12) float32 identity-rotation poses whose centres lie on a `radius` sphere inside
+    the volume (the createCameraLocationsFromSphere layout the run_tsp cost map is built over,
+    tests/CameraPathGen.cpp:310-331): bench.py's collision cost map workload."""
+    rng = np.random.default_rng(seed)
+    dirs = rng.normal(size=(V, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    cp = np.tile(np.eye(3, 4, dtype=np.float32).reshape(1, 12), (V, 1))
+    cp[:, 3::4] = (radius * dirs).astype(np.float32)
+    return cp

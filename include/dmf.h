@@ -43,7 +43,9 @@ enum dmf_status {
   DMF_ERR_NOMEM = 4,     /* device or host allocation failed                       */
   DMF_ERR_CAPACITY = 5,  /* output buffer too small: required size returned        */
   DMF_ERR_RANGE = 6,     /* grid too large for a packed field (hash / fixed point) */
-  DMF_ERR_NO_DEVICE = 7  /* no usable GPU                                          */
+  DMF_ERR_NO_DEVICE = 7, /* no usable GPU                                          */
+  DMF_ERR_DEVICE_CHECK = 8 /* a device-side consistency check failed: the results of the
+                              calls it covers are invalid (dmf_fuse_status)               */
 };
 
 typedef struct dmf_volume dmf_volume;
@@ -220,8 +222,10 @@ int dmf_fuse_depth(dmf_volume* v, const dmf_camera* cam, const uint16_t* depth, 
  * tiles of 16 int32 = one 64-B line, tiles x-major) of
  * dmf_fuse_counter_cells() elements each, ACCUMULATED; any elementwise sum of them
  * (e.g. an all-reduce across ranks) stays valid.  d_stats (may be NULL): 8 uint64
- * counters += {cell updates, rays, hits, 0, LDS rounds, direct rounds, flushed cell
- * atomics, 0}. */
+ * counters += {cell updates, rays, hits, layout faults, LDS rounds | pairs, direct rounds |
+ * parts, flushed cell atomics, 0}; layout faults (must stay 0) = the device-side check of
+ * the brick pipeline's pair layout (dmf_fuse_status) -- a non-zero count means the counters
+ * of that call are invalid. */
 int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_depth,
                           const float* d_poses, int32_t P, const dmf_fuse_params* prm, int32_t* d_hits,
                           int32_t* d_misses, uint64_t* d_stats);
@@ -284,6 +288,14 @@ int dmf_fuse_plan(const dmf_volume* v, const dmf_camera* cam, int32_t P, dmf_fus
 /* Diagnostic (synchronises the stream): the pose batches the device cut the latest
  * brick-pipeline super-batch of this volume into (0 before any brick-pipeline call). */
 int dmf_fuse_batches_used(dmf_volume* v, int32_t* batches);
+/* Device-side check of the brick pipeline (synchronises the volume's streams): pass B
+ * writes each (ray, brick) pair record into the slot range pass A counted for it; a store
+ * outside the call's pair records is dropped, and every workgroup compares the slots it took
+ * per brick with pass A's counts.  Returns DMF_ERR_DEVICE_CHECK (and clears the count) when
+ * any fusion call since the last dmf_fuse_status disagreed -- their counters are invalid --
+ * else DMF_OK; *faults (may be NULL) = the workgroup-brick disagreements seen.  The host
+ * form dmf_fuse_depth runs this check itself. */
+int dmf_fuse_status(dmf_volume* v, uint64_t* faults);
 /* Elements of one tiled counter array (>= xdim*ydim*zdim: dims padded to 2, 2, 4). */
 int dmf_fuse_counter_cells(const dmf_volume* v, int64_t* n);
 /* Tiled counters -> x-major int32 (xdim*ydim*zdim). */

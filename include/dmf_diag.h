@@ -2,7 +2,8 @@
  * dmf_diag.h — diagnostic, A/B and test controls of libdmf.so (not the product ABI).
  *
  * Nothing here changes a result: every fusion kernel and every knob value gives the same
- * integer counters, flags and lists (the GPU suite checks each against the oracle).  The
+ * integer counters, flags and lists (the GPU suite checks each against the oracle) -- except
+ * DMF_KNOB_FAULT_INJECT, the test hook of the device-side layout check (dmf_fuse_status).  The
  * controls are PER VOLUME (no process-global state, no environment variables read by the
  * library); a new volume starts with every control at its default.  Declared apart from
  * include/dmf.h so that callers of the product ABI never see them.
@@ -46,7 +47,11 @@ enum dmf_knob {
   DMF_KNOB_A_HASH = 9,      /* pass A's histogram: 0 default (hashed, 2048 words, above 8192 bricks; direct
                                below), -1 always direct, k > 0 always hashed with k words (rounded up to a
                                power of two, 16..16384; a workgroup whose table overflows is redone with the direct one) */
-  DMF_KNOB_COUNT = 10
+  DMF_KNOB_FAULT_INJECT = 10, /* test hook: k > 0 makes lane 0 of pass B's first workgroup take k extra slots
+                                  in its first brick, so that passes A and B disagree (the call's results are
+                                  then invalid; dmf_fuse_status reports it, and no store leaves the pair
+                                  buffers); 0 = off */
+  DMF_KNOB_COUNT = 11
 };
 int dmf_volume_set_knob(dmf_volume* v, int32_t knob, int64_t value);
 int dmf_volume_get_knob(const dmf_volume* v, int32_t knob, int64_t* value);

@@ -1,12 +1,17 @@
 """CPU, world_size 2 over gloo: the pose-sharded fusion merged with one all-reduce
 equals the single-rank fusion bit for bit (the CPU oracle stands in for the GPU
 kernel, which is exercised by the -m gpu tests and bench.py)."""
+import json
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
 import torch.multiprocessing as mp
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -278,3 +283,36 @@ def test_merge_partition_single_rank():
                 D.finalize_tiles_np(ht, mt, dims, 847, -405, -2000, 3511, out, r0 * tpr, r1 * tpr)
             assert np.array_equal(out[: exp.size], exp)
             assert npad >= ((dims[0] + 1) // 2) * tpr * 16
+
+
+def _bench(*args, env_extra=None):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], stdout=subprocess.PIPE,
+                          stderr=subprocess.PIPE, env=env, timeout=300, text=True)
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_spawns_its_ranks(n):
+    """`python bench.py --gpus N` (N > 1, no launcher) starts N ranks itself: a
+    torch.distributed.run child with one rank per GPU on 127.0.0.1, every argument forwarded
+    (--print-launch is the dry run: it prints the command and touches no GPU)."""
+    r = _bench("--gpus", str(n), "--steps", "7", "--warmup", "3", "--print-launch")
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    cmd = json.loads(lines[0])["launch"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and f"--nproc-per-node={n}" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert int(cmd[cmd.index("--master-port") + 1]) > 0
+    i = cmd.index(os.path.join(ROOT, "bench.py"))
+    assert cmd[i + 1:] == ["--gpus", str(n), "--steps", "7", "--warmup", "3"]
+
+
+def test_bench_rejects_world_mismatch():
+    """A launcher whose WORLD_SIZE differs from --gpus is an error, not a warning."""
+    r = _bench("--gpus", "4", "--steps", "1", env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr

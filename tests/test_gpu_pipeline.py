@@ -257,3 +257,47 @@ def test_timed_mode_config4_shape():
     (cs, ss), (cp, sp) = results["serial"], results["pipelined"]
     assert np.array_equal(ss[:5], sp[:5]) and int(ss[0]) == 3 * golden["updates"]
     assert results["serial"][0].equal(cp)
+
+
+@pytest.mark.parametrize("extra", [1, 1 << 20])
+def test_pass_b_layout_guard(extra):
+    """Pass B's record stores are guarded: with DMF_KNOB_FAULT_INJECT one
+    lane of pass B takes `extra` slots more than pass A counted.  The call must neither fault
+    nor store outside the pair records: the layout check reports the disagreement in
+    d_stats[3] and through dmf_fuse_status (DMF_ERR_DEVICE_CHECK), the host form returns that
+    status, and the volume is clean again afterwards (same counters as before, status ok).
+    extra = 1 shifts one workgroup's slots into its neighbour's range; 2^20 sends that lane's
+    later slots in the brick past the call's records (dropped stores)."""
+    from test_gpu_configs import Fusion
+    import dmf_amd
+    from dmf_amd import _lib
+    f = Fusion(256, 640, 480, 8)
+    c0, st0, name = f.run(0)
+    assert name.startswith("dmf::k_bk_fuse_s") and int(st0[3]) == 0
+    assert _lib.fuse_status(f.vol) == 0
+    for pipelined in (False, True):
+        inp = f.torch.cuda.Stream(f.dev)
+        if pipelined:
+            _lib.check(f.L.dmf_fuse_set_input_stream(f.vol._h, inp.cuda_stream))
+        _lib.set_knob(f.vol, "fault_inject", extra)
+        c1, st1, _ = f.run(0)
+        assert int(st1[3]) > 0
+        with pytest.raises(_lib.DmfError) as e:
+            _lib.fuse_status(f.vol)
+        assert e.value.status == _lib.DMF_ERR_DEVICE_CHECK
+        _lib.set_knob(f.vol, "fault_inject", 0)
+        c2, st2, _ = f.run(0)
+        assert int(st2[3]) == 0 and _lib.fuse_status(f.vol) == 0
+        assert f.torch.equal(c2, c0)
+        if pipelined:
+            _lib.check(f.L.dmf_fuse_set_input_stream(f.vol._h, None))
+    # the host form returns the status itself
+    eng = dmf_amd.RayTracingEngine(dmf_amd.Camera(f.K))
+    prm = dmf_amd.FuseParams(dmin_mm=200, dmax_mm=1000)
+    _lib.set_knob(f.vol, "fault_inject", extra)
+    with pytest.raises(_lib.DmfError) as e:
+        eng.fuse_depth(f.vol, f.depth, f.poses, prm)
+    assert e.value.status == _lib.DMF_ERR_DEVICE_CHECK
+    _lib.set_knob(f.vol, "fault_inject", 0)
+    eng.fuse_depth(f.vol, f.depth, f.poses, prm)
+    assert _lib.fuse_status(f.vol) == 0

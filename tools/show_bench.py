@@ -14,3 +14,12 @@ if s:
     print("reverse %.3f ms/batch  forward %.3f ms/batch  costmap %.3f ms" % (
         s["reverse_ray_trace_fast"]["ms_per_batch"], s["forward_first_hits"]["ms_per_batch"],
         s["collision_cost_map"]["ms"]))
+    for k, sub in (("reverse", s["reverse_ray_trace_fast"]), ("forward", s["forward_first_hits"]),
+                   ("costmap", s["collision_cost_map"])):
+        print("  %s digest_match %s" % (k, sub.get("digest_match")))
+    rc = (s["reverse_ray_trace_fast"].get("cpu_baseline") or {})
+    print("  reverse cpu pose0_list_match %s" % rc.get("pose0_list_match"))
+for k in ("cpu_baseline", "cpu_baseline_multicore", "cpu_baseline_reference"):
+    c = d.get(k)
+    if c:
+        print("%s: %.4e %s cores %s  %s" % (k, c["value"], c["unit"], c["cores"], c["sample"][:120]))
