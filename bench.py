@@ -611,6 +611,9 @@ def main():
     if st[3] != 0:  # pass B's device-side layout check (dmf_fuse_status): the counters are invalid
         raise RuntimeError(f"fusion layout check failed {st[3]} times")
     _lib.fuse_status(vol)  # raises DmfError(DMF_ERR_DEVICE_CHECK) if any call disagreed
+    # how the device cut the calls (the per-volume budget may split a call)
+    plan = _lib.fuse_plan(vol, cam, P)
+    plan["batches_used_last_call"] = _lib.fuse_batches_used(vol) if plan.get("brick") else 1
     elapsed = D.max_over_ranks(elapsed, device=dev)
     updates, rays, hits = D.sum_over_ranks(st[:3], device=dev)
 
@@ -712,6 +715,7 @@ def main():
                            else "")},
             "mrays_per_s": rays / elapsed / 1e6,
             "fuse_diagnostics": diagnostics,
+            "fuse_plan": plan,
             "updates_per_ray": updates / max(rays, 1.0),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,

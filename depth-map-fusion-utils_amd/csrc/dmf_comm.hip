@@ -256,12 +256,17 @@ int dmf_flags_allreduce(dmf_volume* v, void* comm, void* stream) {
   // collective leaves the view ids as they were on this rank, never INT32_MAX.
   hipLaunchKernelGGL(k_view_zero_to_max, dim3(nb), dim3(256), 0, st, v->d_view, n);
   DMF_LAUNCH_CHECK();
+  // the guard restores on error / exception exits only; the success path launches the restore
+  // itself and checks that launch
   struct Restore {
     int32_t* view;
     int64_t n;
     unsigned nb;
     hipStream_t st;
-    ~Restore() { hipLaunchKernelGGL(k_view_max_to_zero, dim3(nb), dim3(256), 0, st, view, n); }
+    bool armed = true;
+    ~Restore() {
+      if (armed) hipLaunchKernelGGL(k_view_max_to_zero, dim3(nb), dim3(256), 0, st, view, n);
+    }
   } restore{v->d_view, n, nb, st};
   {
     NcclGroup grp;
@@ -270,6 +275,9 @@ int dmf_flags_allreduce(dmf_volume* v, void* comm, void* stream) {
     DMF_NCCL(ncclAllReduce(v->d_good, v->d_good, (size_t)n, ncclUint8, ncclMax, (ncclComm_t)comm, st));
     DMF_NCCL(grp.end());
   }
+  restore.armed = false;
+  hipLaunchKernelGGL(k_view_max_to_zero, dim3(nb), dim3(256), 0, st, v->d_view, n);
+  DMF_LAUNCH_CHECK();
   return DMF_OK;
   DMF_API_END
 }

@@ -1005,7 +1005,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
   // the batch's pair records: a slot at or past `total` (passes A and B disagree) is never
   // stored, and the end of the kernel checks the slots taken per brick against pass A
   const uint32_t total = (uint32_t)ctl[0];
-  if (threadIdx.x == 0) s_inj = (inject > 0 && j == 0 && blockIdx.x == 0) ? (uint32_t)inject : 0u;
+  if (threadIdx.x == 0) s_inj = (inject > 0 && j == 0 && (uint32_t)pz == bt[1]) ? (uint32_t)inject : 0u;
   // this workgroup's range in brick i starts at off[i] + pose_base[p][i] + wg_base[wg][i]
   // (k_bk_scan, k_bk_batch_counts, pass A); only the bricks pass A counted for this
   // workgroup are initialised (1024^3: 32768 bricks, ~300 touched)
@@ -2027,7 +2027,9 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         DMF_HIP(hipEventRecord(v->st_b[slot], sa));
         DMF_HIP(hipStreamWaitEvent(v->stream, v->st_b[slot], 0));
       }
-      if (v->f_event && s0 == 0 && j == 0) DMF_HIP(hipEventRecord(v->f_event, v->stream));  // the call's phase F begins
+      // the call's phase F begins (not while capturing: the record would become a graph node
+      // and the caller's event would never be re-recorded by the graph's launches)
+      if (v->f_event && !capturing && s0 == 0 && j == 0) DMF_HIP(hipEventRecord(v->f_event, v->stream));
       if (slab)
         hipLaunchKernelGGL((k_bk_fuse_s<kBkRefill, kBkSpread, kBkUnroll>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,
                            (const uint4*)b.pra, (const uint32_t*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
@@ -2265,7 +2267,7 @@ static int fuse_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* d_d
     DMF_TRY(fuse_bricks(v, cp, g, d_depth, tab, d_poses, P, prm, d_hits, d_misses, st, d_stats, staged, capturing));
   } else {
     const int pkx = (cp.W + 7) / 8;
-    if (v->f_event) DMF_HIP(hipEventRecord(v->f_event, v->stream));
+    if (v->f_event && !capturing) DMF_HIP(hipEventRecord(v->f_event, v->stream));
     hipLaunchKernelGGL((k_fuse_l<12, 1280>), dim3((unsigned)(pkx * ((cp.H + 7) / 8)), (unsigned)P), dim3(64), 0,
                        v->stream, g, cp, d_depth, tab, prm->dmin_mm, prm->dmax_mm, pkx, d_hits, d_misses, st);
     DMF_LAUNCH_CHECK();

@@ -16,6 +16,7 @@
 #include <memory>
 #include <string>
 
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -102,12 +103,20 @@ int dmf_grid_save(const char* path, const dmf_grid_header* h, const int16_t* log
     if (h->dims[a] < 1 || h->dims[a] > (1 << 20)) return fail(DMF_ERR_INVALID, "bad dims");
   uint8_t head[kHeaderBytes];
   put_header(h, head);
-  // written to path.tmp, flushed to disk, then renamed over path: a crash or a full disk
-  // mid-write leaves the previous file intact
-  const std::string tmp = std::string(path) + ".tmp";
+  // written to a unique temporary file in the target's directory (mkstemp: two writers of one
+  // path never share it), flushed to disk, renamed over path, then the directory itself is
+  // synced so that the new entry survives a crash: a crash or a full disk mid-write leaves the
+  // previous file intact
+  std::string tmp = std::string(path) + ".XXXXXX";
+  const int fd = mkstemp(&tmp[0]);
+  if (fd < 0) return fail(DMF_ERR_INVALID, "cannot create a temporary file beside %s", path);
   File out;
-  out.f = fopen(tmp.c_str(), "wb");
-  if (!out.f) return fail(DMF_ERR_INVALID, "cannot open %s for writing", tmp.c_str());
+  out.f = fdopen(fd, "wb");
+  if (!out.f) {
+    close(fd);
+    unlink(tmp.c_str());
+    return fail(DMF_ERR_INVALID, "cannot open %s for writing", tmp.c_str());
+  }
   const size_t n = (size_t)cells_of(h->dims);
   uint32_t crc = crc32().update(0, head, sizeof(head));
   crc = crc32().update(crc, logodds, n * sizeof(int16_t));
@@ -124,6 +133,14 @@ int dmf_grid_save(const char* path, const dmf_grid_header* h, const int16_t* log
     unlink(tmp.c_str());
     return fail(DMF_ERR_INVALID, "cannot rename %s to %s", tmp.c_str(), path);
   }
+  std::string dir(path);
+  const size_t slash = dir.find_last_of('/');
+  dir = slash == std::string::npos ? std::string(".") : (slash == 0 ? std::string("/") : dir.substr(0, slash));
+  const int dfd = open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+  if (dfd < 0) return fail(DMF_ERR_INVALID, "cannot open directory %s to sync it", dir.c_str());
+  const bool synced = fsync(dfd) == 0;
+  close(dfd);
+  if (!synced) return fail(DMF_ERR_INVALID, "cannot sync directory %s", dir.c_str());
   return DMF_OK;
   DMF_API_END
 }

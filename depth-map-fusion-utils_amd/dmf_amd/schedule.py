@@ -124,6 +124,10 @@ def run_steps(rt, nsteps, nbuf, clear, fuse, merge, marks=None, reuse_wait=True,
             mark(i + nbuf, "z1", "comm")
         merged[b] = last = rt.record("comm")
 
+    if phase is not None and nbuf < 2:
+        # the deferred merge of step i is enqueued after fuse(i + 1), which would add into
+        # the same single buffer before the merge read it
+        raise ValueError("run_steps: a phase-deferred merge needs at least 2 counter buffers")
     pending = None  # (b, i, fused) of the step whose merge waits for the next phase F
     for i in range(nsteps):
         b = i % nbuf

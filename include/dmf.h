@@ -236,7 +236,11 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
  * the device's memory, ~130 GB on MI355X): serial calls use one slot of the whole budget,
  * pipelined calls (dmf_fuse_set_input_stream) two staging slots of half each.  A call whose
  * pairs exceed a slot's pair capacity is cut into pose batches on the device
- * (dmf_fuse_plan).  A new budget frees and re-plans the slots.  Synchronises the stream. */
+ * (dmf_fuse_plan).  A new budget frees and re-plans the slots.  Synchronises the stream.
+ * The budget is PER VOLUME: several volumes fusing on one device (or several processes
+ * sharing it) should each reserve their share explicitly, e.g. 0.9 x free memory / volumes;
+ * a call whose pairs exceed the share runs in more pose batches (dmf_fuse_batches_used),
+ * with identical results. */
 int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t max_scratch_bytes);
 /* Pipelined fusion (an extension, the reference fuses one frame at a time,
  * tests/Raytracing.cpp:70-76).  Declares that the device inputs (d_depth, d_poses) of later
@@ -264,7 +268,9 @@ int dmf_fuse_set_input_stream(dmf_volume* v, void* stream);
  * this HBM-bound work runs beside the issue-bound phase F instead of beside the next call's
  * passes A / B (bench.py).  The event is re-recorded by each call: wait on
  * it after the call returns and before the next call.  It must stay valid until it is
- * unregistered (event = NULL) or the volume is destroyed. */
+ * unregistered (event = NULL) or the volume is destroyed.  A call enqueued while the volume's
+ * stream is capturing a graph does not record it (a record inside a graph would not re-record
+ * the caller's event when the graph is launched): order captured work by the graph itself. */
 int dmf_fuse_set_phase_event(dmf_volume* v, void* event);
 /* How a fusion call of P frames of `cam`'s size on this volume is executed (no GPU work,
  * no allocation): brick = 1 for the brick-owned pipeline (k_bk_*), 0 for k_fuse_l.  The

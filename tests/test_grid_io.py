@@ -83,17 +83,55 @@ def test_huge_dims_rejected_before_allocation(tmp_path):
     assert e.value.status == _lib.DMF_ERR_INVALID
 
 
+def _save_under_fsize_limit(path, limit):
+    """Child process: dmf_grid_save of a 5x4x3 grid with RLIMIT_FSIZE = limit bytes (writes past
+    it fail with EFBIG, SIGXFSZ ignored); prints the DmfError status or 'ok'."""
+    import subprocess
+    import sys
+    code = f"""
+import resource, signal, sys
+sys.path[:0] = {sys.path!r}
+import numpy as np
+from dmf_amd import _lib
+signal.signal(signal.SIGXFSZ, signal.SIG_IGN)
+resource.setrlimit(resource.RLIMIT_FSIZE, ({limit}, {limit}))
+g = (np.arange(60, dtype=np.int16) * 7).reshape(5, 4, 3)
+try:
+    _lib.grid_save({str(path)!r}, g, g.shape, (0, 1, 0, 1, 0, 1))
+    print("ok")
+except _lib.DmfError as e:
+    print("err", e.status)
+"""
+    return subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, timeout=120).stdout.strip()
+
+
 def test_save_replaces_atomically(tmp_path):
-    """dmf_grid_save writes path.tmp and renames it over path: a save that fails
-    (here: an unwritable temporary) leaves the previous file intact and no temporary behind."""
+    """dmf_grid_save writes a unique temporary beside path (mkstemp), syncs it,
+    renames it over path and syncs the directory: a save that fails mid-write (here: a file
+    size limit) leaves the previous file intact and no temporary behind."""
     g = _grid((5, 4, 3), 3)
     path = tmp_path / "g.dmf"
     _lib.grid_save(path, g, g.shape, (0, 1, 0, 1, 0, 1))
     before = path.read_bytes()
-    assert not (tmp_path / "g.dmf.tmp").exists()
-    (tmp_path / "g.dmf.tmp").mkdir()  # fopen of the temporary fails
-    with pytest.raises(_lib.DmfError):
-        _lib.grid_save(path, _grid((5, 4, 3), 4), (5, 4, 3), (0, 1, 0, 1, 0, 1))
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["g.dmf"]
+    assert _save_under_fsize_limit(path, 64) == f"err {_lib.DMF_ERR_INVALID}"
     assert path.read_bytes() == before
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["g.dmf"]  # the temporary is gone
     g2, _, _ = _lib.grid_load(path)
     assert np.array_equal(g2, g)
+
+
+def test_concurrent_saves_never_tear(tmp_path):
+    """Two writers of one path use their own temporaries: the file is always one whole grid."""
+    from concurrent.futures import ThreadPoolExecutor
+    path = tmp_path / "g.dmf"
+    grids = [_grid((40, 30, 20), s) for s in (1, 2)]
+
+    def save(k):
+        for _ in range(20):
+            _lib.grid_save(path, grids[k], grids[k].shape, (0, 1, 0, 1, 0, 1))
+    with ThreadPoolExecutor(2) as ex:
+        list(ex.map(save, (0, 1)))
+    g, _, _ = _lib.grid_load(path)
+    assert any(np.array_equal(g, x) for x in grids)
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["g.dmf"]

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r05a
 mkdir -p $O
 { echo "nproc $(nproc)"; cat /sys/fs/cgroup/cpu.max 2>&1; python -c 'import os; print("affinity", len(os.sched_getaffinity(0)), "omp", os.environ.get("OMP_NUM_THREADS"))'; lscpu | head -20; } > $O/host.txt 2>&1
-timeout -k 10 400 python -u -m pytest tests/test_gpu_marches.py tests/test_gpu_pipeline.py -m gpu -x -v --timeout 240 --timeout-method thread -k "marches or layout_guard" > $O/new_tests.log 2>&1 || { echo NEWTESTFAIL; tail -40 $O/new_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_pipeline.py -m gpu -x -v --timeout 240 --timeout-method thread -k "layout_guard" > $O/new_tests.log 2>&1 || { echo NEWTESTFAIL; tail -40 $O/new_tests.log; exit 1; }
 tail -3 $O/new_tests.log
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo TESTFAIL; tail -40 $O/gpu_tests.log; exit 1; }
 tail -3 $O/gpu_tests.log
