@@ -811,10 +811,11 @@ def attach_pmc(result, pmc):
     rf["valu_issue_frac"] = rf["companion"]["frac"]
     rf["valu_lane_slots_per_update"] = valu * 64.0 / max(rf["updates_per_launch"], 1.0)
     sec = result.get("secondary") or {}
-    for name, prefix in (("reverse_ray_trace_fast", "dmf::k_reverse_q"), ("forward_first_hits", "dmf::k_forward")):
+    for name, prefixes in (("reverse_ray_trace_fast", ("dmf::k_reverse_x", "dmf::k_reverse_q")),
+                           ("forward_first_hits", ("dmf::k_forward",))):
         if name not in sec:
             continue
-        ks = [k for k in pmc if k == prefix or k.startswith(prefix + "<")]
+        ks = [k for p_ in prefixes for k in pmc if k == p_ or k.startswith(p_ + "<")]
         if ks:
             sec[name]["roofline"] = issue_roofline(pmc, ks[0], sec[name].get("kernel_ms") or sec[name]["ms_per_batch"])
 

@@ -10,6 +10,7 @@
 //  * z-buffer splat rayTraceVolume (:498-564) and the willCollide segment march
 //    (tests/CameraPathGen.cpp:128-156).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -313,31 +314,20 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
 // all visible).  The result bits are then in item order: vis_mask / good_mask receive
 // item-ordered words, which k_mask_to_slots permutes into occupied_cells_ order (the output
 // is a per-slot bitmask, so the processing order is free).
-template <bool kEnum, int kItems, int kRefill, int kBurst, bool kOrder = false>
-__global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses,
-                                                   int64_t nelem, EnumList el, const uint32_t* __restrict__ order,
-                                                   int depth0, int max_steps, float dstar, int viz, int normal_test,
-                                                   uint64_t* __restrict__ vis_mask, uint64_t* __restrict__ good_mask,
-                                                   int64_t words, unsigned long long* __restrict__ stats,
-                                                   int* __restrict__ found, unsigned long long* __restrict__ hazards) {
-  static_assert(kItems % 64 == 0, "whole mask words per wave");
-  static_assert(!(kEnum && kOrder), "spatial order: occupied_cells_ items only");
-  stats = stat_slot(stats);
-  __shared__ uint32_t lvis[4][kItems / 32], lgood[4][kItems / 32];
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  for (int i = l; i < kItems / 32; i += 64) { lvis[w][i] = 0; lgood[w][i] = 0; }
-  const int p = blockIdx.y;
-  const int64_t base = ((int64_t)blockIdx.x * 4 + w) * kItems;
-  const int nitems = (int)max<int64_t>(0, min<int64_t>(kItems, nelem - base));
-  const PoseX& T = poses[p];
-  int64_t samples = 0, rays = 0;
-  unsigned long long ncap = 0;
-  unsigned long long rst[kRevStatN] = {};
+// One wave's work queue over items [base, base + nitems) of pose T: result bits into the
+// wave's LDS words lvis / lgood (item-indexed, zeroed by the caller); returns the lane's "some
+// item visible".  Shared by k_reverse_q (a grid of (item chunk, pose)) and k_reverse_x (per-XCD
+// unit queues).
+template <bool kEnum, int kItems, int kRefill, int kBurst, bool kOrder>
+__device__ inline bool rev_wave(const Geom& g, const DevVol& vd, const CamP& cam, const PoseX& T, const EnumList& el,
+                                const uint32_t* __restrict__ order, int64_t base, int nitems, int depth0,
+                                int max_steps, float dstar, int viz, int normal_test, uint32_t* lvis, uint32_t* lgood,
+                                int64_t& samples, int64_t& rays, unsigned long long& ncap, unsigned long long* rst) {
+  [[maybe_unused]] const int l = threadIdx.x & 63;  // (diagnostic-build statistics)
   bool any_vis = false;
   RevLane L;
   L.item = -1;
   int next = 0;  // wave-uniform queue head
-  __syncthreads();
   while (true) {
     const uint64_t idle = __builtin_amdgcn_ballot_w64(L.item < 0);
     const int nidle = __builtin_popcountll(idle);
@@ -428,8 +418,8 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
             good = true;
           }
         }
-        atomicOr(&lvis[w][L.item >> 5], 1u << (L.item & 31));
-        if (good) atomicOr(&lgood[w][L.item >> 5], 1u << (L.item & 31));
+        atomicOr(&lvis[L.item >> 5], 1u << (L.item & 31));
+        if (good) atomicOr(&lgood[L.item >> 5], 1u << (L.item & 31));
         if (viz) {
           vd.view[L.slot] = 1;
           if (good) vd.good[L.slot] = 1;
@@ -438,6 +428,32 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
       L.item = -1;
     }
   }
+  return any_vis;
+}
+
+template <bool kEnum, int kItems, int kRefill, int kBurst, bool kOrder = false>
+__global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses,
+                                                   int64_t nelem, EnumList el, const uint32_t* __restrict__ order,
+                                                   int depth0, int max_steps, float dstar, int viz, int normal_test,
+                                                   uint64_t* __restrict__ vis_mask, uint64_t* __restrict__ good_mask,
+                                                   int64_t words, unsigned long long* __restrict__ stats,
+                                                   int* __restrict__ found, unsigned long long* __restrict__ hazards) {
+  static_assert(kItems % 64 == 0, "whole mask words per wave");
+  static_assert(!(kEnum && kOrder), "spatial order: occupied_cells_ items only");
+  stats = stat_slot(stats);
+  __shared__ uint32_t lvis[4][kItems / 32], lgood[4][kItems / 32];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int i = l; i < kItems / 32; i += 64) { lvis[w][i] = 0; lgood[w][i] = 0; }
+  const int p = blockIdx.y;
+  const int64_t base = ((int64_t)blockIdx.x * 4 + w) * kItems;
+  const int nitems = (int)max<int64_t>(0, min<int64_t>(kItems, nelem - base));
+  int64_t samples = 0, rays = 0;
+  unsigned long long ncap = 0;
+  unsigned long long rst[kRevStatN] = {};
+  __syncthreads();
+  const bool any_vis = rev_wave<kEnum, kItems, kRefill, kBurst, kOrder>(
+      g, vd, cam, poses[p], el, order, base, nitems, depth0, max_steps, dstar, viz, normal_test, lvis[w], lgood[w],
+      samples, rays, ncap, rst);
   __syncthreads();
   const int64_t w0 = base >> 6;
   for (int i = l; i < kItems / 64; i += 64) {
@@ -449,6 +465,86 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
     }
   }
   if (__builtin_amdgcn_ballot_w64(any_vis) != 0 && l == 0) atomicOr(&found[p], 1);
+  for (int o = 32; o > 0; o >>= 1) ncap += __shfl_down(ncap, o, 64);
+  if (l == 0 && ncap) atomicAdd(hazards, ncap);
+  if (stats) {
+    wave_add_u64(&stats[0], (unsigned long long)samples);
+    wave_add_u64(&stats[1], (unsigned long long)rays);
+#if defined(DMF_EXP_STATS)
+#pragma unroll
+    for (int i = 0; i < kRevStatN; ++i) wave_add_u64(&stats[2 + i], rst[i]);
+#endif
+  }
+}
+
+// reverseRayTraceFast with per-XCD work queues (spatial order only).  A unit is one wave's
+// 64 consecutive items of the Morton order for one pose.  The Morton range is cut into 8
+// contiguous eighths, one queue per eighth, units pose-major inside it; workgroup b serves the
+// queue of its XCD group b % 8 (blocks b and b + 8 share an XCD's L2 under the observed
+// round-robin placement -- a speed choice only, any placement gives the same bits), so the
+// waves resident on one XCD march rays from one region of the surface toward one camera at a
+// time and share its L2 lines of the occupancy bitmask and distance field.  A wave whose queue
+// is empty takes units from the next groups' queues (work stealing at the tail), so uneven
+// march work per eighth cannot idle an XCD; every wave exits once all 8 queues are drained.
+// heads[8]: the queues' unit counters (zeroed before the launch).
+// kWg: a unit is the workgroup's 4 consecutive waves' worth of items (256, as one workgroup of
+// k_reverse_q), taken by the workgroup together: its waves share the CU's L1 lines as in
+// k_reverse_q, at the price of a barrier per unit; else one wave's 64 items per unit.
+template <int kItems, int kRefill, int kBurst, bool kWg>
+__global__ __launch_bounds__(256) void k_reverse_x(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses, int P,
+                                                   int64_t nelem, const uint32_t* __restrict__ order, int depth0,
+                                                   int max_steps, float dstar, int viz, uint64_t* __restrict__ vis_mask,
+                                                   uint64_t* __restrict__ good_mask, int64_t words,
+                                                   unsigned int* __restrict__ heads,
+                                                   unsigned long long* __restrict__ stats, int* __restrict__ found,
+                                                   unsigned long long* __restrict__ hazards) {
+  static_assert(kItems == 64, "one mask word per wave and unit");
+  stats = stat_slot(stats);
+  __shared__ uint32_t lvis[4][2], lgood[4][2];
+  __shared__ uint32_t s_unit;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int grp = (int)(blockIdx.x & 7u);
+  const EnumList el{};
+  int64_t samples = 0, rays = 0;
+  unsigned long long ncap = 0;
+  unsigned long long rst[kRevStatN] = {};
+  constexpr int kPer = kWg ? 4 : 1;  // mask words per unit
+  const int64_t nwu = (words + kPer - 1) / kPer;
+  for (int q = 0; q < 8; ++q) {
+    const int gq = (grp + q) & 7;
+    const int64_t c0 = nwu * gq / 8, nch = nwu * (gq + 1) / 8 - c0;
+    const uint32_t nunits = (uint32_t)(nch * P);
+    for (;;) {
+      uint32_t u = 0;
+      if (kWg) {
+        if (threadIdx.x == 0) s_unit = atomicAdd(&heads[gq], 1u);
+        __syncthreads();
+        u = s_unit;
+        __syncthreads();  // every wave has read it before the next unit's write
+      } else {
+        if (l == 0) u = atomicAdd(&heads[gq], 1u);
+        u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
+      }
+      if (u >= nunits) break;
+      const int p = (int)(u / (uint32_t)nch);
+      const int64_t c = (c0 + (int64_t)(u - (uint32_t)p * (uint32_t)nch)) * kPer + (kWg ? w : 0);
+      if (l < 2) { lvis[w][l] = 0; lgood[w][l] = 0; }
+      __builtin_amdgcn_wave_barrier();
+      const int64_t base = c * kItems;
+      const int nitems = (int)max<int64_t>(0, min<int64_t>(kItems, nelem - base));
+      const bool any_vis = rev_wave<false, kItems, kRefill, kBurst, true>(
+          g, vd, cam, poses[p], el, order, base, nitems, depth0, max_steps, dstar, viz, 1, lvis[w], lgood[w],
+          samples, rays, ncap, rst);
+      __builtin_amdgcn_wave_barrier();
+      if (l == 0 && c < words) {
+        const uint64_t vb = (uint64_t)lvis[w][0] | ((uint64_t)lvis[w][1] << 32);
+        const uint64_t gb = (uint64_t)lgood[w][0] | ((uint64_t)lgood[w][1] << 32);
+        if (vis_mask) vis_mask[(int64_t)p * words + c] = vb;
+        if (good_mask) good_mask[(int64_t)p * words + c] = gb;
+      }
+      if (__builtin_amdgcn_ballot_w64(any_vis) != 0 && l == 0) atomicOr(&found[p], 1);
+    }
+  }
   for (int o = 32; o > 0; o >>= 1) ncap += __shfl_down(ncap, o, 64);
   if (l == 0 && ncap) atomicAdd(hazards, ncap);
   if (stats) {
@@ -681,8 +777,10 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
     const dim3 grid((unsigned)((nelem + 255) / 256), (unsigned)P);
     const int depth0 = enumerate ? 1 : 50;  // :81 vs :172
     // DMF_KNOB_REVERSE_KERNEL (dmf_diag.h): 0 = default (the work-queue march with the brick
-    // distance field, items in spatial order for reverseRayTraceFast), 1 = lane per (voxel,
-    // pose), 2 = the same with brick skipping, 3 = the work queue in occupied_cells_ order
+    // distance field, items in spatial order for reverseRayTraceFast, per-XCD unit queues),
+    // 1 = lane per (voxel, pose), 2 = the same with brick skipping, 3 = the work queue in
+    // occupied_cells_ order, 4 = per-XCD queues of per-wave units, 5 = the spatial-order work
+    // queue on a (chunk, pose) grid (the default until round 5)
     const int64_t kr = v->knob[DMF_KNOB_REVERSE_KERNEL];
     // work-queue shape (items per wave, refill threshold, burst): 512 / 8 / 8 in enumeration
     // or insertion order; in spatial order smaller queues pay (neighbouring lanes agree, so
@@ -725,12 +823,39 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
       } else {
         DMF_TRY(ensure_spatial_order(v));
         void* items;
-        DMF_TRY(scratch(v, kScRevItems, sizeof(uint64_t) * (size_t)(2 * P * words), &items));
+        // item-ordered masks, then 8 queue heads (k_reverse_x)
+        DMF_TRY(scratch(v, kScRevItems, sizeof(uint64_t) * (size_t)(2 * P * words) + 64, &items));
         uint64_t* vis_i = (uint64_t*)items;
         uint64_t* good_i = vis_i + P * words;
-        hipLaunchKernelGGL((k_reverse_q<false, kSpItems, kSpRefill, kSpBurst, true>), gridqs, dim3(256), 0, v->stream, g, dv, cp, tab,
-                           nelem, el, (const uint32_t*)v->d_sorder, depth0, ms, v->dstar, viz, 1, vis_i, good_i, words,
-                           st, found, hz);
+        if (kr != 5) {
+          // default: per-XCD unit queues (persistent: as many workgroups as the device holds at
+          // once), a unit = the workgroup's 256 items (kr 4: a wave's 64) -- 5.30 vs 5.56 ms per
+          // 128 poses (k_reverse_q's (chunk, pose) grid, kr 5), L2 hit rate 0.56 -> 0.83, beyond-L2
+          // bytes 8.1 -> 3.3 GB; per-wave units 10.3 ms (the CU's waves no longer share L1 lines:
+          // L2 requests x1.6).  DESIGN.md §5.5, profiles/r05b/
+          unsigned int* heads = (unsigned int*)(good_i + P * words);
+          DMF_HIP(hipMemsetAsync(heads, 0, 8 * sizeof(unsigned int), v->stream));
+          const bool wg_units = kr != 4;
+          const void* kfn = wg_units ? (const void*)k_reverse_x<kSpItems, kSpRefill, kSpBurst, true>
+                                     : (const void*)k_reverse_x<kSpItems, kSpRefill, kSpBurst, false>;
+          int per_cu = 0;
+          DMF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, 0));
+          int ncu = 0;
+          DMF_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, v->device));
+          const unsigned nwg = (unsigned)(std::max(ncu, 8) * std::max(per_cu, 1));
+          if (wg_units)
+            hipLaunchKernelGGL((k_reverse_x<kSpItems, kSpRefill, kSpBurst, true>), dim3(nwg), dim3(256), 0, v->stream, g,
+                               dv, cp, tab, P, nelem, (const uint32_t*)v->d_sorder, depth0, ms, v->dstar, viz, vis_i,
+                               good_i, words, heads, st, found, hz);
+          else
+            hipLaunchKernelGGL((k_reverse_x<kSpItems, kSpRefill, kSpBurst, false>), dim3(nwg), dim3(256), 0, v->stream,
+                               g, dv, cp, tab, P, nelem, (const uint32_t*)v->d_sorder, depth0, ms, v->dstar, viz, vis_i,
+                               good_i, words, heads, st, found, hz);
+        } else {
+          hipLaunchKernelGGL((k_reverse_q<false, kSpItems, kSpRefill, kSpBurst, true>), gridqs, dim3(256), 0, v->stream, g,
+                             dv, cp, tab, nelem, el, (const uint32_t*)v->d_sorder, depth0, ms, v->dstar, viz, 1, vis_i,
+                             good_i, words, st, found, hz);
+        }
         DMF_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_mask_to_slots, dim3((unsigned)((words * 64 + 255) / 256)), dim3(256), 0, v->stream,
                            (const uint64_t*)vis_i, (const uint64_t*)good_i, (const uint32_t*)(v->d_sorder + v->sorder_cap),

@@ -41,8 +41,10 @@ enum dmf_knob {
   DMF_KNOB_SPAN = 5,        /* 8x8 packets per pass-A/B workgroup (4..4096) */
   DMF_KNOB_TAIL_SPLIT = 6,  /* phase F's queue tail split: -1 off, k > 0 = the last k x CUs parts quartered
                                (default: 2 for serial calls, off for pipelined ones) */
-  DMF_KNOB_REVERSE_KERNEL = 7, /* reverseRayTraceFast march: 0 default (queue in spatial order + distance
-                                  field), 1 plain, 2 plain + brick skip, 3 queue in insertion order */
+  DMF_KNOB_REVERSE_KERNEL = 7, /* reverseRayTraceFast march: 0 default (wave queues in spatial order + distance
+                                  field, workgroup units from per-XCD queues: k_reverse_x), 1 plain, 2 plain +
+                                  brick skip, 3 queue in insertion order, 4 per-XCD queues of wave units, 5 the
+                                  spatial-order queues on a (chunk, pose) grid (k_reverse_q) */
   DMF_KNOB_FWD_SKIP = 8,    /* forward march empty-space skipping: 0 default (on), -1 off */
   DMF_KNOB_A_HASH = 9,      /* pass A's histogram: 0 default (hashed, 2048 words, above 8192 bricks; direct
                                below), -1 always direct, k > 0 always hashed with k words (rounded up to a

@@ -94,11 +94,13 @@ def _flags(v_or, v_gpu):
     return ov, og, gview, ggood
 
 
-@pytest.mark.parametrize("kernel", [0, 3, 1, 2])
+@pytest.mark.parametrize("kernel", [0, 4, 5, 3, 1, 2])
 def test_reverse_fast_parity(oracle, engine, oeng, kernel):
     """reverseRayTraceFast (RayTracingEngine.hpp:136-226) over 12 poses, every march kernel
     (DMF_KNOB_REVERSE_KERNEL): 0 = the default work queue in spatial (Morton) item order with
-    the item -> slot mask permutation, 3 = the work queue in occupied_cells_ order, 1 / 2 =
+    the item -> slot mask permutation, its workgroup units taken from per-XCD queues with work
+    stealing (k_reverse_x), 4 = the same with per-wave units, 5 = the spatial-order queue on a
+    (chunk, pose) grid (k_reverse_q), 3 = the work queue in occupied_cells_ order, 1 / 2 =
     one lane per (voxel, pose) without / with brick skipping: lists (order included), found
     and view / good flags equal the oracle's."""
     from dmf_amd import _lib

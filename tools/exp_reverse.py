@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""A/B of reverseRayTraceFast work orders (DMF_KNOB_REVERSE_KERNEL 0 = spatial order, 3 =
-occupied_cells_ order) on bench.py's secondary workload: a 512^3 volume integrated from 16
+"""A/B of reverseRayTraceFast kernels (DMF_KNOB_REVERSE_KERNEL 0 = spatial order, 3 =
+occupied_cells_ order, 4 = per-XCD unit queues; argv[1] = comma-separated list, alternated) on bench.py's secondary workload: a 512^3 volume integrated from 16
 back-projected 640x480 frames, 128 poses per launch.  Prints ms per launch for each and
 checks the visibility / good masks are identical (with a DMF_EXP_STATS library also the work
 queue's lane occupancy: busy lane-iterations / 64 x burst iterations)."""
@@ -44,7 +44,8 @@ V = vol.info()["num_occupied"]
 words = (V + 63) // 64
 out = {"voxels": int(V), "poses": P}
 res = {}
-for kr in (3, 0, 3, 0):
+KS = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [3, 0, 3, 0]
+for kr in KS:
     _lib.set_knob(vol, "reverse_kernel", kr)
     vis = torch.zeros(P * words, dtype=torch.int64, device=dev)
     good = torch.zeros(P * words, dtype=torch.int64, device=dev)
@@ -68,5 +69,6 @@ for kr in (3, 0, 3, 0):
     if sv[10] > 0:  # DMF_EXP_STATS build: burst iterations (per wave) and busy lane-iterations
         out[f"lane_busy_kernel{kr}"] = float(sv[11]) / (64.0 * float(sv[10]))
     res[kr] = (vis.cpu().numpy(), good.cpu().numpy())
-out["masks_equal"] = bool(np.array_equal(res[0][0], res[3][0]) and np.array_equal(res[0][1], res[3][1]))
+k0 = KS[0]
+out["masks_equal"] = bool(all(np.array_equal(res[k0][0], r[0]) and np.array_equal(res[k0][1], r[1]) for r in res.values()))
 print(json.dumps(out), flush=True)
