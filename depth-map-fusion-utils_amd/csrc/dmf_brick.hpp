@@ -34,7 +34,11 @@
 namespace dmf {
 namespace brick {
 
+#if defined(DMF_EXP_BRICK_LOG)  // experiment builds (tools/build_exp.sh): another brick edge, e.g. 4 = 16^3
+constexpr int kLog = DMF_EXP_BRICK_LOG;
+#else
 constexpr int kLog = 5;                 // bricks of 32^3 cells
+#endif
 constexpr int kB = 1 << kLog;
 constexpr int kCells = kB * kB * kB;    // 32768 LDS counters (128 KiB)
 constexpr int kMaxBricks = 32768;       // per-WG LDS histograms of pass A/B (grids <= 1024^3)

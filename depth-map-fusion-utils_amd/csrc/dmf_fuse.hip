@@ -504,7 +504,9 @@ struct BkGeom {
   int nbricks;
 };
 
-constexpr int kBkThreads = 1024;
+// phase F's workgroup: 1024 lanes over a 32^3 brick (one per CU by LDS); an experiment build
+// with 16^3 bricks (DMF_EXP_BRICK_LOG = 4) runs 256-lane workgroups, several per CU
+constexpr int kBkThreads = bk::kLog == 5 ? 1024 : 256;
 // passes A/B: 256-lane workgroups (several per CU) while the LDS brick histogram is small;
 // 1024 lanes when it is large (over 8192 bricks: one workgroup per CU by LDS)
 constexpr int kBkPassThreads = 256, kBkPassThreadsBig = 1024, kBkBigHist = 8192;
@@ -1517,13 +1519,32 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     }
     DMF_T(tf0);
     __syncthreads();
+    if constexpr (bk::kLog != 5) {
+      // (experiment builds with another brick edge: the generic mapping of k_bk_fuse)
+      for (int e = tid; e < bk::kCells; e += blockDim.x) {
+        const int tile = e >> 4, w16 = e & 15;
+        const int tx = tile >> (2 * bk::kLog - 3), ty = (tile >> (bk::kLog - 2)) & ((bk::kB >> 1) - 1),
+                  tz = tile & ((bk::kB >> 2) - 1);
+        const int lx = tx * 2 + (w16 >> 3), ly = ty * 2 + ((w16 >> 2) & 1), lz = tz * 4 + (w16 & 3);
+        const int li = lx * kBkSx + ly * kBkSy + lz;
+        const uint32_t v = box[li];
+        if (v) {
+          box[li] = 0;
+          const uint32_t ti = tiled_index(tl, lo0 + lx, lo1 + ly, lo2 + lz);
+          const int32_t mi = (int32_t)(v & 0xffffu), hv = (int32_t)(v >> 16);
+          if (mi) atomic_add_dev(&misses[ti], mi);
+          if (hv) atomic_add_dev(&hits[ti], hv);
+          ++nflush;
+        }
+      }
+    } else
     // flush (one device atomic per non-zero cell and counter): lane tid takes cells
     // e = tid + 1024 k of the brick in the tiled order (16 lanes per 64-B counter line).  The
     // cell's box word and its counter index inside the brick move by per-k constants, so
     // the index math is done once per part, not per cell (cell e: tile e >> 4 = (tx, ty, tz)
     // with tx = k >> 1, ty = 8 (k & 1) + (t0 >> 3), tz = t0 & 7 for t0 = tid >> 4).
     {
-      static_assert(bk::kLog == 5 && kBkThreads == 1024, "flush strides: 32^3-cell bricks, 1024 lanes");
+      static_assert(bk::kLog != 5 || kBkThreads == 1024, "flush strides: 32^3-cell bricks, 1024 lanes");
       const int t0 = tid >> 4, w16 = tid & 15;
       const int li0 = (w16 >> 3) * kBkSx + (2 * (t0 >> 3) + ((w16 >> 2) & 1)) * kBkSy + 4 * (t0 & 7) + (w16 & 3);
       const uint32_t ti0 = tile_base(tl, lo0 >> 1, lo1 >> 1, lo2 >> 2) +
@@ -1933,6 +1954,15 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   // pass A with 16-bit histogram counts (a workgroup's pairs per brick <= span * 64 rays)
   const bool a16 = (int64_t)pl.span * 64 <= 65535;
   const unsigned nf = (unsigned)cu_count(v->device);
+  // phase F's persistent workgroups: one per CU (32^3 bricks); an experiment build with
+  // smaller bricks holds as many per CU as fit
+  unsigned nfF = nf;
+  if constexpr (bk::kLog != 5) {
+    int per = 0;
+    DMF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per, (const void*)k_bk_fuse_s<kBkRefill, kBkSpread, kBkUnroll>, kBkThreads, 0));
+    nfF = nf * (unsigned)std::max(per, 1);
+  }
   for (int64_t s0 = 0; s0 < P; s0 += pl.PS) {
     const int64_t ps = std::min<int64_t>(pl.PS, P - s0);
     const unsigned nwg = (unsigned)(ps * pl.wg_pose);
@@ -2031,7 +2061,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       // and the caller's event would never be re-recorded by the graph's launches)
       if (v->f_event && !capturing && s0 == 0 && j == 0) DMF_HIP(hipEventRecord(v->f_event, v->stream));
       if (slab)
-        hipLaunchKernelGGL((k_bk_fuse_s<kBkRefill, kBkSpread, kBkUnroll>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg,
+        hipLaunchKernelGGL((k_bk_fuse_s<kBkRefill, kBkSpread, kBkUnroll>), dim3(nfF), dim3(kBkThreads), 0, v->stream, g, bg,
                            (const uint4*)b.pra, (const uint32_t*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
                            (const uint2*)b.order, pl.part_max, b.ctl, d_hits, d_misses, st);
       else

@@ -923,26 +923,13 @@ static int reverse_lists(dmf_volume* v, const dmf_camera* cam, const float* pose
 //    shrunk by eps and, the cube being convex, so do the exact points of every sample in
 //    between; those samples are therefore inside the cube: no hit, no hazard — jump to j.
 // j is estimated from the line and then verified by evaluating sample j exactly.
+// The march of lattice pixel (ri, ci) of one pose: k_out / slot_out [ri * C + ci].
 template <bool kSkip>
-__global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ pose,
-                                                 int zstart, int zdelta, int rdelta, int cdelta, int R, int C,
-                                                 int32_t* __restrict__ k_out, int32_t* __restrict__ slot_out,
-                                                 unsigned long long* __restrict__ hazards,
-                                                 unsigned long long* __restrict__ stats) {
-  stats = stat_slot(stats);
-  // a wave marches an 8x8 tile of lattice pixels (fwd_threads): neighbouring rays in both
-  // directions reach similar depths and read the same bitmask tiles (a row of 64 pixels
-  // spans 8x the angle); outputs stay row-major (idx)
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int tpr = (C + 7) >> 3, ln = (int)(t & 63);
-  const int64_t tile = t >> 6;
-  const int ri = (int)(tile / tpr) * 8 + (ln >> 3), ci = (int)(tile % tpr) * 8 + (ln & 7);
+__device__ inline void fwd_ray(const Geom& g, const DevVol& vd, const CamP& cam, const PoseX* __restrict__ pose,
+                               int zstart, int zdelta, int rdelta, int cdelta, int R, int C, int ri, int ci,
+                               int32_t* __restrict__ k_out, int32_t* __restrict__ slot_out,
+                               unsigned long long* __restrict__ hazards, int64_t& samples) {
   const int64_t idx = (int64_t)ri * C + ci;
-  // grid.y = pose index of a batched launch (one pose: grid.y = 1)
-  pose += blockIdx.y;
-  k_out += (int64_t)blockIdx.y * R * C;
-  slot_out += (int64_t)blockIdx.y * R * C;
-  int64_t samples = 0;
   if (ri < R && ci < C) {
     const int r = ri * rdelta, c = ci * cdelta;
     int32_t kk = -1, sl = -1;
@@ -1065,6 +1052,68 @@ __global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, co
     }
     k_out[idx] = kk;
     slot_out[idx] = sl;
+  }
+}
+
+template <bool kSkip>
+__global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ pose,
+                                                 int zstart, int zdelta, int rdelta, int cdelta, int R, int C,
+                                                 int32_t* __restrict__ k_out, int32_t* __restrict__ slot_out,
+                                                 unsigned long long* __restrict__ hazards,
+                                                 unsigned long long* __restrict__ stats) {
+  stats = stat_slot(stats);
+  // a wave marches an 8x8 tile of lattice pixels (fwd_threads): neighbouring rays in both
+  // directions reach similar depths and read the same bitmask tiles (a row of 64 pixels
+  // spans 8x the angle); outputs stay row-major (idx)
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int tpr = (C + 7) >> 3, ln = (int)(t & 63);
+  const int64_t tile = t >> 6;
+  const int ri = (int)(tile / tpr) * 8 + (ln >> 3), ci = (int)(tile % tpr) * 8 + (ln & 7);
+  // grid.y = pose index of a batched launch (one pose: grid.y = 1)
+  int64_t samples = 0;
+  fwd_ray<kSkip>(g, vd, cam, pose + blockIdx.y, zstart, zdelta, rdelta, cdelta, R, C, ri, ci,
+                 k_out + (int64_t)blockIdx.y * R * C, slot_out + (int64_t)blockIdx.y * R * C, hazards, samples);
+  if (stats) wave_add_u64(&stats[0], (unsigned long long)samples);
+}
+
+// The batched forward march with per-XCD unit queues (as k_reverse_x): a unit is one
+// workgroup's 4 consecutive 8x8 tiles (row-major tile order) of one pose; the tile range is
+// cut into 8 contiguous bands of rows, one queue per band, units pose-major inside it, and
+// workgroup b serves the queue of its XCD group b % 8 first (a speed choice: the waves of one
+// XCD then march one slab of one frustum at a time and share its L2 lines of the occupancy
+// bitmask and distance field), then steals from the other queues.  heads[8] zeroed before.
+template <bool kSkip>
+__global__ __launch_bounds__(256) void k_forward_x(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ pose, int P,
+                                                   int zstart, int zdelta, int rdelta, int cdelta, int R, int C,
+                                                   int32_t* __restrict__ k_out, int32_t* __restrict__ slot_out,
+                                                   unsigned int* __restrict__ heads,
+                                                   unsigned long long* __restrict__ hazards,
+                                                   unsigned long long* __restrict__ stats) {
+  stats = stat_slot(stats);
+  __shared__ uint32_t s_unit;
+  const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int tpr = (C + 7) >> 3;
+  const int64_t ntiles = (int64_t)((R + 7) >> 3) * tpr, nwu = (ntiles + 3) / 4;
+  const int grp = (int)(blockIdx.x & 7u);
+  int64_t samples = 0;
+  for (int q = 0; q < 8; ++q) {
+    const int gq = (grp + q) & 7;
+    const int64_t u0 = nwu * gq / 8, nch = nwu * (gq + 1) / 8 - u0;
+    const uint32_t nunits = (uint32_t)(nch * P);
+    for (;;) {
+      if (threadIdx.x == 0) s_unit = atomicAdd(&heads[gq], 1u);
+      __syncthreads();
+      const uint32_t u = s_unit;
+      __syncthreads();  // every wave has read it before the next unit's write
+      if (u >= nunits) break;
+      const int p = (int)(u / (uint32_t)nch);
+      const int64_t tile = (u0 + (int64_t)(u - (uint32_t)p * (uint32_t)nch)) * 4 + w;
+      if (tile < ntiles) {
+        const int ri = (int)(tile / tpr) * 8 + (ln >> 3), ci = (int)(tile % tpr) * 8 + (ln & 7);
+        fwd_ray<kSkip>(g, vd, cam, pose + p, zstart, zdelta, rdelta, cdelta, R, C, ri, ci,
+                       k_out + (int64_t)p * R * C, slot_out + (int64_t)p * R * C, hazards, samples);
+      }
+    }
   }
   if (stats) wave_add_u64(&stats[0], (unsigned long long)samples);
 }
@@ -1512,8 +1561,26 @@ int dmf_forward_first_hits_device(dmf_volume* v, const dmf_camera* cam, const fl
   DMF_HIP(hipMemsetAsync(aux, 0, 64, v->stream));
   unsigned long long* st = nullptr;
   if (d_stats) DMF_TRY(stats_begin(v, &st));
-  DMF_LAUNCH_FORWARD(dim3(fwd_blocks(R, C), (unsigned)P), v->geom(), v->dev(), cam_params(cam), tab,
-                     zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot, (unsigned long long*)aux, st);
+  if (v->knob[DMF_KNOB_FWD_KERNEL] == 1) {
+    // per-XCD unit queues (k_forward_x; persistent: the workgroups the device holds at once)
+    unsigned int* heads = (unsigned int*)aux + 8;
+    const bool skip = fwd_skip(v);
+    if (skip) DMF_TRY(ensure_brick_dist(v));
+    const void* kfn = skip ? (const void*)k_forward_x<true> : (const void*)k_forward_x<false>;
+    int per_cu = 0, ncu = 0;
+    DMF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, 0));
+    DMF_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, v->device));
+    const dim3 grid((unsigned)(std::max(ncu, 8) * std::max(per_cu, 1)));
+    if (skip)
+      hipLaunchKernelGGL(k_forward_x<true>, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab, P,
+                         zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot, heads, (unsigned long long*)aux, st);
+    else
+      hipLaunchKernelGGL(k_forward_x<false>, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab,
+                         P, zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot, heads, (unsigned long long*)aux, st);
+  } else {
+    DMF_LAUNCH_FORWARD(dim3(fwd_blocks(R, C), (unsigned)P), v->geom(), v->dev(), cam_params(cam), tab,
+                       zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot, (unsigned long long*)aux, st);
+  }
   DMF_LAUNCH_CHECK();
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 1));
   return DMF_OK;

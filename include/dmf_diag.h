@@ -53,7 +53,9 @@ enum dmf_knob {
                                   first pose take k extra slots, so that passes A and B disagree (the results are
                                   then invalid; dmf_fuse_status reports it, and no store leaves the pair
                                   buffers); 0 = off */
-  DMF_KNOB_COUNT = 11
+  DMF_KNOB_FWD_KERNEL = 11,  /* batched forward first hits (dmf_forward_first_hits_device): 0 default (a grid of
+                                (tile block, pose): k_forward), 1 per-XCD unit queues (k_forward_x) */
+  DMF_KNOB_COUNT = 12
 };
 int dmf_volume_set_knob(dmf_volume* v, int32_t knob, int64_t value);
 int dmf_volume_get_knob(const dmf_volume* v, int32_t knob, int64_t* value);

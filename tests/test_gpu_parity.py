@@ -558,12 +558,17 @@ def test_golden_config1_gpu(dmf):
     assert np.array_equal(sha(eng.fuse_finalize(vf, hits, misses)), z["fuse_logodds_sha"])
 
 
-def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf):
-    """dmf_forward_first_hits_device over P poses in one launch == the oracle per pose."""
+@pytest.mark.parametrize("fwd_kernel", [0, 1])
+def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf, fwd_kernel):
+    """dmf_forward_first_hits_device over P poses in one launch == the oracle per pose (both
+    batched kernels, DMF_KNOB_FWD_KERNEL: 0 = the (tile block, pose) grid, 1 = per-XCD unit
+    queues)."""
     import ctypes as C
     from dmf_amd import _lib
     ov = Hh.oracle_volume(oracle, n=100)
     gv = Hh.gpu_volume(n=100)
+    from dmf_amd import _lib as _l
+    _l.set_knob(gv, "fwd_kernel", fwd_kernel)
     poses = Hh.all_poses()[:5].astype(np.float32)
     P, rd, cd = len(poses), 3, 2
     R, Cc = (H + rd - 1) // rd, (W + cd - 1) // cd
