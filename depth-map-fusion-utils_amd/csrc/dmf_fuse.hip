@@ -864,24 +864,21 @@ __global__ __launch_bounds__(256) void k_bk_batch_counts(int nbricks, int j, con
 // BIG (over 4096 bricks): the counts are staged in LDS (128 KiB); otherwise they are read
 // from memory (4 per lane at 512^3) and the kernel's ~12 KiB of LDS fit beside phase F's box
 // (pipelined calls).
+// The scan's body (one 1024-lane workgroup): `cnt` = the batch's pair counts per brick, in
+// memory or in LDS (s_cnt_in non-null).  Also zeroes ctl[2] / ctl[3] (phase F's queue head),
+// so no memset precedes it.
 template <bool BIG>
-__global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* __restrict__ cnt,
-                                                  uint32_t* __restrict__ off,
-                                                  uint32_t* __restrict__ part_pref,
-                                                  unsigned long long* __restrict__ ctl,
-                                                  uint2* __restrict__ order, uint32_t part_max,
-                                                  const uint32_t* __restrict__ bt, int j, int split_cu) {
-  if ((uint32_t)j >= bt[0]) {  // a batch the call does not need: no pairs, no parts
-    if (threadIdx.x == 0) ctl[0] = ctl[1] = 0;
-    return;
-  }
+__device__ inline void bk_scan_body(int nbricks, const uint32_t* __restrict__ cnt, const uint32_t* s_cnt_in,
+                                    uint32_t* __restrict__ off, uint32_t* __restrict__ part_pref,
+                                    unsigned long long* __restrict__ ctl, uint2* __restrict__ order, uint32_t part_max,
+                                    int split_cu) {
   __shared__ unsigned long long s_pairs[1024];
   __shared__ uint32_t s_parts[1024];
   __shared__ uint32_t s_cls[64];
   // the counts, loaded once with coalesced reads (the brick path has <= 32^3 bricks): the
   // per-thread brick ranges below then read LDS, not dependent HBM loads (1024^3: 0.18 ms)
   __shared__ uint32_t s_cnt_lds[BIG ? kBkScanMax : 1];
-  const uint32_t* const s_cnt = BIG ? s_cnt_lds : cnt;
+  const uint32_t* const s_cnt = BIG ? s_cnt_lds : (s_cnt_in ? s_cnt_in : cnt);
   const int t = threadIdx.x;
   if (t < 64) s_cls[t] = 0;
   if constexpr (BIG)
@@ -957,7 +954,98 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
     part_pref[nbricks] = NP;
     ctl[0] = s_pairs[1023];
     ctl[1] = NP + 3 * S;
+    ctl[2] = 0;
+    ctl[3] = 0;
   }
+}
+
+template <bool BIG>
+__global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* __restrict__ cnt,
+                                                  uint32_t* __restrict__ off,
+                                                  uint32_t* __restrict__ part_pref,
+                                                  unsigned long long* __restrict__ ctl,
+                                                  uint2* __restrict__ order, uint32_t part_max,
+                                                  const uint32_t* __restrict__ bt, int j, int split_cu) {
+  if ((uint32_t)j >= bt[0]) {  // a batch the call does not need: no pairs, no parts
+    if (threadIdx.x == 0) ctl[0] = ctl[1] = ctl[2] = ctl[3] = 0;
+    return;
+  }
+  bk_scan_body<BIG>(nbricks, cnt, nullptr, off, part_pref, ctl, order, part_max, split_cu);
+}
+
+// Small grids (nbricks <= kBkLayout1Bricks, super-batch <= kBkLayout1Poses): the batch cut
+// (k_bk_batches, batch 0's launch only), the batch's brick counts (k_bk_batch_counts) and the
+// scan (k_bk_scan) in ONE workgroup: one launch instead of three on the chain between pass A
+// and pass B of a pipelined call (config 2: 512 bricks, 64 poses; the chain's launch gaps
+// and three kernels ~47 us of a 1.7-ms call).
+constexpr int kBkLayout1Bricks = 1024, kBkLayout1Poses = 256;
+__global__ __launch_bounds__(1024) void k_bk_layout1(int P, const unsigned long long* __restrict__ pose_pairs,
+                                                     unsigned long long cap, int max_poses, uint32_t* __restrict__ bt,
+                                                     int nbricks, int j, const uint32_t* __restrict__ pose_cnt,
+                                                     uint32_t* __restrict__ pose_base, uint32_t* __restrict__ cnt,
+                                                     uint32_t* __restrict__ off, uint32_t* __restrict__ part_pref,
+                                                     unsigned long long* __restrict__ ctl, uint2* __restrict__ order,
+                                                     uint32_t part_max, int split_cu) {
+  __shared__ uint32_t s_bt[kBkLayout1Poses + 2];
+  __shared__ uint32_t s_cnt[kBkLayout1Bricks];
+  __shared__ unsigned long long s_pp[kBkLayout1Poses];
+  const int t = threadIdx.x;
+  if (j == 0) {  // pose pair counts staged in LDS (one coalesced load; the cut below is serial)
+    for (int p = t; p < P; p += blockDim.x) s_pp[p] = pose_pairs[p];
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (j == 0) {  // the batch cut of k_bk_batches (serial over <= 256 poses)
+      uint32_t J = 0;
+      unsigned long long sum = 0;
+      int n = 0;
+      for (int p = 0; p < P; ++p) {
+        const unsigned long long c = s_pp[p];
+        if (n == 0 || sum + c > cap || n >= max_poses) {
+          s_bt[1 + J] = (uint32_t)p;
+          ++J;
+          sum = 0;
+          n = 0;
+        }
+        sum += c;
+        ++n;
+      }
+      s_bt[1 + J] = (uint32_t)P;
+      s_bt[0] = J;
+      for (uint32_t k = 0; k <= J + 1; ++k) bt[k] = s_bt[k];
+    }
+  }
+  if (j > 0) {  // the table batch 0's launch wrote (same stream, earlier)
+    const uint32_t J = bt[0];
+    for (uint32_t k = t; k <= J + 1 && k < kBkLayout1Poses + 2; k += blockDim.x) s_bt[k] = bt[k];
+  }
+  __syncthreads();
+  if ((uint32_t)j >= s_bt[0]) {
+    if (t == 0) ctl[0] = ctl[1] = ctl[2] = ctl[3] = 0;
+    return;
+  }
+  const int p0 = (int)s_bt[1 + j], p1 = (int)s_bt[2 + j];
+  for (int b = t; b < nbricks; b += blockDim.x) {  // k_bk_batch_counts
+    uint32_t acc = 0;
+    int p = p0;
+    for (; p + 4 <= p1; p += 4) {  // four independent loads in flight
+      const uint32_t c0 = pose_cnt[(size_t)p * nbricks + b], c1 = pose_cnt[(size_t)(p + 1) * nbricks + b],
+                     c2 = pose_cnt[(size_t)(p + 2) * nbricks + b], c3 = pose_cnt[(size_t)(p + 3) * nbricks + b];
+      pose_base[(size_t)p * nbricks + b] = acc;
+      pose_base[(size_t)(p + 1) * nbricks + b] = acc + c0;
+      pose_base[(size_t)(p + 2) * nbricks + b] = acc + c0 + c1;
+      pose_base[(size_t)(p + 3) * nbricks + b] = acc + c0 + c1 + c2;
+      acc += c0 + c1 + c2 + c3;
+    }
+    for (; p < p1; ++p) {
+      pose_base[(size_t)p * nbricks + b] = acc;
+      acc += pose_cnt[(size_t)p * nbricks + b];
+    }
+    cnt[b] = acc;
+    s_cnt[b] = acc;
+  }
+  __syncthreads();
+  bk_scan_body<false>(nbricks, cnt, s_cnt, off, part_pref, ctl, order, part_max, split_cu);
 }
 
 // Pass B.  Same spans as pass A; the workgroup's range in each brick was laid out by pass A
@@ -979,6 +1067,11 @@ __global__ __launch_bounds__(1024) void k_bk_scan(int nbricks, const uint32_t* _
 // Slots: one LDS atomic per lane, whose return is consumed only by the pair's store at the
 // next brick boundary (its latency hides behind that boundary's count_at; B 1.92 -> 1.88 ms;
 // wave-aggregated and run-aggregated takes measured slower).
+// Pass B's store guard (experiment builds: 0 none, 1 a branch around the stores); the
+// default 2 clamps the slot onto a spare record
+#ifndef DMF_B_GUARD
+#define DMF_B_GUARD 2
+#endif
 __device__ inline uint32_t bk_e30(int32_t e) {
   const int32_t lim = (1 << 29) - 1;
   return (uint32_t)(e > lim ? lim : (e < -lim ? -lim : e)) & 0x3fffffffu;
@@ -1004,8 +1097,9 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
   // the workgroups of pass A (one pose each); only those of batch j's poses run
   const int pz = (int)(blockIdx.x / (unsigned)wg_pose);
   if ((uint32_t)j >= bt[0] || (uint32_t)pz < bt[1 + j] || (uint32_t)pz >= bt[2 + j]) return;
-  // the batch's pair records: a slot at or past `total` (passes A and B disagree) is never
-  // stored, and the end of the kernel checks the slots taken per brick against pass A
+  // the batch's pair records: a slot at or past `total` (passes A and B disagree) never
+  // stores outside them, and the end of the kernel checks the slots taken per brick against
+  // pass A
   const uint32_t total = (uint32_t)ctl[0];
   if (threadIdx.x == 0) s_inj = (inject > 0 && j == 0 && (uint32_t)pz == bt[1]) ? (uint32_t)inject : 0u;
   // this workgroup's range in brick i starts at off[i] + pose_base[p][i] + wg_base[wg][i]
@@ -1088,7 +1182,14 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
       return bk_lds_word(x, y, z);
     };
     auto put = [&](uint32_t slot, uint4 e, uint32_t last, uint32_t steps, bool ends) {
+#if DMF_B_GUARD == 1
       if (slot >= total) return;  // only when A and B disagree (reported by the check below)
+#elif DMF_B_GUARD == 2
+      // a slot at or past the batch's records (only when A and B disagree, reported by the
+      // check below) goes to the spare record at index `total` (pair_cap + 1 are reserved),
+      // which phase F never reads: one v_min instead of a branch around the stores
+      slot = min(slot, total);
+#endif
       if constexpr (SLAB) {
         uint32_t w[5];
         bk::pack20((int32_t)e.x, (int32_t)e.y, (int32_t)e.z, aM, a1, a2, e.w, last, steps, signs >> 22, (uint32_t)M,
@@ -1150,6 +1251,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }
   // layout check: the slots taken in each touched brick must be pass A's count for it
+#if DMF_B_GUARD != 0
   __syncthreads();
   {
     const uint32_t* row = wg_list + (size_t)blockIdx.x * (size_t)wgl_stride;
@@ -1166,6 +1268,7 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
       atomicAdd(&fault[1], bad);
     }
   }
+#endif
 }
 
 // Pair order inside a part: lane-adjacent picks come from S_ORDER far-apart regions of
@@ -1851,8 +1954,10 @@ static int bk_scratch(dmf_volume* v, const BkPlan& pl, BkBufs& b, int slot) {
   DMF_TRY(scratch(v, slot ? kScBkWgBase1 : kScBkWgBase, pl.hist_bytes * (size_t)pl.wg_pose * PS, &wgb));
   DMF_TRY(scratch(v, slot ? kScBkWgList1 : kScBkWgList,
                   sizeof(uint32_t) * (size_t)pl.wgl_stride * (size_t)pl.wg_pose * PS, &wgl));
-  DMF_TRY(scratch(v, slot ? kScBkPairs1 : kScBkPairs, sizeof(uint4) * (size_t)pl.pair_cap, &pra));
-  DMF_TRY(scratch(v, slot ? kScBkPairsB1 : kScBkPairsB, (pl.rec_bytes - sizeof(uint4)) * (size_t)pl.pair_cap, &prb));
+  // pair records: pair_cap, plus the spare record pass B's store guard writes to
+  DMF_TRY(scratch(v, slot ? kScBkPairs1 : kScBkPairs, sizeof(uint4) * ((size_t)pl.pair_cap + 1), &pra));
+  DMF_TRY(scratch(v, slot ? kScBkPairsB1 : kScBkPairsB, (pl.rec_bytes - sizeof(uint4)) * ((size_t)pl.pair_cap + 1),
+                  &prb));
   DMF_TRY(scratch(v, slot ? kScBkPoseCnt1 : kScBkPoseCnt, pl.hist_bytes * PS, &pcnt));
   DMF_TRY(scratch(v, slot ? kScBkPoseBase1 : kScBkPoseBase, pl.hist_bytes * PS, &pbase));
   DMF_TRY(scratch(v, slot ? kScBkBatch1 : kScBkBatch, sizeof(unsigned long long) * PS + sizeof(uint32_t) * (PS + 4),
@@ -2017,9 +2122,13 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         DMF_TRY(stats_end(v, st_a, d_user, kStatWidth));
       }
     }
-    hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sa, (int)ps, (const unsigned long long*)b.pose_pairs,
-                       (unsigned long long)pl.pair_cap, pl.max_poses, b.bt);
-    DMF_LAUNCH_CHECK();
+    // small grids: batch cut, brick counts and scan in one launch per batch (k_bk_layout1)
+    const bool layout1 = bg.nbricks <= kBkLayout1Bricks && ps <= kBkLayout1Poses;
+    if (!layout1) {
+      hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sa, (int)ps, (const unsigned long long*)b.pose_pairs,
+                         (unsigned long long)pl.pair_cap, pl.max_poses, b.bt);
+      DMF_LAUNCH_CHECK();
+    }
     v->bk_last_bt = b.bt;
     const int64_t jm = pl.jmax(ps);
     for (int64_t j = 0; j < jm; ++j) {
@@ -2029,11 +2138,19 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       // once, and on the volume's stream they no longer hold the staging stream -- and with
       // it the next call's pass A -- behind this call's phase F (1024^3: jmax 7, one batch).
       const hipStream_t sj = staged && j > 0 ? v->stream : sa;
-      DMF_HIP(hipMemsetAsync(b.ctl, 0, sizeof(unsigned long long) * 4, sj));
-      hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sj, bg.nbricks,
-                         (int)j, (const uint32_t*)b.bt, (const uint32_t*)b.pose_cnt, b.pose_base, b.cnt);
-      DMF_LAUNCH_CHECK();
-      if (bg.nbricks > 4096)
+      // (the scan zeroes phase F's queue head: no memset of ctl)
+      if (layout1) {
+        hipLaunchKernelGGL(k_bk_layout1, dim3(1), dim3(1024), 0, sj, (int)ps, (const unsigned long long*)b.pose_pairs,
+                           (unsigned long long)pl.pair_cap, pl.max_poses, b.bt, bg.nbricks, (int)j,
+                           (const uint32_t*)b.pose_cnt, b.pose_base, b.cnt, b.off, b.part_pref, b.ctl, b.order,
+                           pl.part_max, pl.split_cu);
+      } else {
+        hipLaunchKernelGGL(k_bk_batch_counts, dim3((unsigned)((bg.nbricks + 255) / 256)), dim3(256), 0, sj,
+                           bg.nbricks, (int)j, (const uint32_t*)b.bt, (const uint32_t*)b.pose_cnt, b.pose_base, b.cnt);
+        DMF_LAUNCH_CHECK();
+      }
+      if (layout1) {
+      } else if (bg.nbricks > 4096)
         hipLaunchKernelGGL(k_bk_scan<true>, dim3(1), dim3(1024), 0, sj, bg.nbricks, (const uint32_t*)b.cnt, b.off,
                            b.part_pref, b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       else
