@@ -1072,6 +1072,9 @@ __global__ __launch_bounds__(1024) void k_bk_layout1(int P, const unsigned long 
 #ifndef DMF_B_GUARD
 #define DMF_B_GUARD 2
 #endif
+// pass B's slot cursor of a brick pass A did not count for the workgroup: every slot taken
+// from it lies at or past any batch's records (pair capacity < the sentinel, bk_plan)
+constexpr uint32_t kBkSlotSentinel = 0xF0000000u;
 __device__ inline uint32_t bk_e30(int32_t e) {
   const int32_t lim = (1 << 29) - 1;
   return (uint32_t)(e > lim ? lim : (e < -lim ? -lim : e)) & 0x3fffffffu;
@@ -1088,12 +1091,11 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
                                                          const uint32_t* __restrict__ bt, int j,
                                                          const uint32_t* __restrict__ wg_list, int wgl_stride,
                                                          uint4* __restrict__ pa, void* __restrict__ pbv,
-                                                         const unsigned long long* __restrict__ ctl,
+                                                         unsigned long long* __restrict__ ctl,
                                                          uint32_t* __restrict__ fault, int inject) {
   uint2* const pb = (uint2*)pbv;
   uint32_t* const pw = (uint32_t*)pbv;
   extern __shared__ uint32_t hist[];
-  __shared__ uint32_t s_inj;  // DMF_KNOB_FAULT_INJECT: the extra slots not yet taken
   // the workgroups of pass A (one pose each); only those of batch j's poses run
   const int pz = (int)(blockIdx.x / (unsigned)wg_pose);
   if ((uint32_t)j >= bt[0] || (uint32_t)pz < bt[1 + j] || (uint32_t)pz >= bt[2 + j]) return;
@@ -1101,7 +1103,9 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
   // stores outside them, and the end of the kernel checks the slots taken per brick against
   // pass A
   const uint32_t total = (uint32_t)ctl[0];
-  if (threadIdx.x == 0) s_inj = (inject > 0 && j == 0 && (uint32_t)pz == bt[1]) ? (uint32_t)inject : 0u;
+  // DMF_KNOB_FAULT_INJECT: the first pair of thread 0 of the first pose's workgroups takes
+  // `inject` extra slots (a register, not LDS: nothing is read per pair for the test hook)
+  uint32_t extra = (inject > 0 && j == 0 && (uint32_t)pz == bt[1] && threadIdx.x == 0) ? (uint32_t)inject : 0u;
   // this workgroup's range in brick i starts at off[i] + pose_base[p][i] + wg_base[wg][i]
   // (k_bk_scan, k_bk_batch_counts, pass A); only the bricks pass A counted for this
   // workgroup are initialised (1024^3: 32768 bricks, ~300 touched)
@@ -1111,12 +1115,18 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
     const uint32_t* row = wg_list + (size_t)blockIdx.x * (size_t)wgl_stride;
     const uint32_t nl = row[0];
     const uint16_t* ids = (const uint16_t*)(row + 1);
+#if DMF_B_GUARD != 0
+    // bricks pass A did not count here: any slot taken from them is out of range (checked)
+    for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = kBkSlotSentinel;
+    __syncthreads();
+#endif
     for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x) {
       const int i = ids[k];
       hist[i] = off[i] + pbz[i] + wb[i];
     }
   }
   __syncthreads();
+  uint32_t over = 0;  // one past the lane's largest slot (the layout check; 0 = no pair)
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int q0 = (int)(blockIdx.x - (unsigned)pz * (unsigned)wg_pose) * span;
   const int64_t pk0 = (int64_t)pz * packets_pose + q0, pk1 = (int64_t)pz * packets_pose + min(packets_pose, q0 + span);
@@ -1183,11 +1193,15 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
     };
     auto put = [&](uint32_t slot, uint4 e, uint32_t last, uint32_t steps, bool ends) {
 #if DMF_B_GUARD == 1
-      if (slot >= total) return;  // only when A and B disagree (reported by the check below)
+      if (slot >= total) {  // only when A and B disagree (reported by the check below)
+        over = slot + 1u;
+        return;
+      }
 #elif DMF_B_GUARD == 2
       // a slot at or past the batch's records (only when A and B disagree, reported by the
       // check below) goes to the spare record at index `total` (pair_cap + 1 are reserved),
-      // which phase F never reads: one v_min instead of a branch around the stores
+      // which phase F never reads: a v_max and a v_min instead of a branch around the stores
+      over = max(over, slot + 1u);
       slot = min(slot, total);
 #endif
       if constexpr (SLAB) {
@@ -1244,9 +1258,8 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
         ci1 = c[1];
         ci2 = c[2];
       }
-      uint32_t take = 1u;
-      if (inject > 0 && s_inj) take += atomicExch(&s_inj, 0u);  // test hook only (uniform kernel argument)
-      slot = atomicAdd(&hist[b], take);
+      slot = atomicAdd(&hist[b], 1u + extra);
+      extra = 0;
     });
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }
@@ -1258,14 +1271,23 @@ __global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose
     const uint32_t nl = row[0];
     const uint16_t* ids = (const uint16_t*)(row + 1);
     const uint32_t* cnts = row + 1 + (bg.nbricks + 1) / 2;
-    uint32_t bad = 0;
+    uint32_t bad = over > total ? 1u : 0u;  // a slot past the records (or from an uncounted brick)
+#if defined(DMF_EXP_LAYOUT_DEBUG)
+    if (bad) printf("B over: wg %u j %d lane %u over %u total %u\n", blockIdx.x, j, threadIdx.x, over, total);
+#endif
     for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x) {
       const int i = ids[k];
       bad += hist[i] != off[i] + pbz[i] + wb[i] + cnts[k] ? 1u : 0u;
+#if defined(DMF_EXP_LAYOUT_DEBUG)
+      if (hist[i] != off[i] + pbz[i] + wb[i] + cnts[k])
+        printf("B count: wg %u j %d brick %d hist %u off %u pbz %u wb %u cnt %u total %u\n", blockIdx.x, j, i, hist[i],
+               off[i], pbz[i], wb[i], cnts[k], total);
+#endif
     }
     if (bad) {
       atomicAdd(&fault[0], bad);
       atomicAdd(&fault[1], bad);
+      atomicOr(&ctl[3], 1ull);  // phase F skips this batch: its records are not all in place
     }
   }
 #endif
@@ -1302,6 +1324,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
   uint32_t* sh = box + kBkBoxWords;
   stats = stat_slot(stats);
   const int tid = threadIdx.x, l = tid & 63;
+  if (ctl[3] != 0) return;  // pass B's layout check failed for this batch (as k_bk_fuse_s)
   for (int i = tid; i < kBkBoxWords; i += blockDim.x) box[i] = 0;
   const uint32_t nparts = (uint32_t)ctl[1];
   const Tiles tl = tiles_of(g.n);
@@ -1477,6 +1500,9 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
   }
   stats = stat_slot(stats);
   const int tid = threadIdx.x, l = tid & 63;
+  // pass B's layout check failed for this batch (dmf_fuse_status reports it): its pair
+  // records are not all in place, so none is walked
+  if (ctl[3] != 0) return;
   for (int i = tid; i < kBkBoxWords; i += blockDim.x) box[i] = 0;
   const uint32_t nparts = (uint32_t)ctl[1];
   const Tiles tl = tiles_of(g.n);
@@ -1887,8 +1913,9 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   pl.PS = std::min<int64_t>(P, (int64_t)(budget / 2 / pl.per_pose_bytes));
   if (kn[DMF_KNOB_SUPER_POSES] > 0) pl.PS = std::min<int64_t>(pl.PS, kn[DMF_KNOB_SUPER_POSES]);
   if (pl.PS < 1) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion budget (dmf_fuse_reserve)");
+  // (below pass B's slot sentinel: a slot taken from an uncounted brick is never in range)
   pl.pair_cap = std::min<uint64_t>({(budget - (uint64_t)pl.PS * pl.per_pose_bytes) / pl.rec_bytes,
-                                    (uint64_t)pl.PS * one_pose, (uint64_t)UINT32_MAX});
+                                    (uint64_t)pl.PS * one_pose, (uint64_t)kBkSlotSentinel - 1});
   if (pl.pair_cap < one_pose) return fail(DMF_ERR_RANGE, "one frame exceeds the brick fusion pair budget (dmf_fuse_reserve)");
   if (kn[DMF_KNOB_PAIR_CAP] > 0)  // test hook: the caller guarantees it holds any one pose's pairs
     pl.pair_cap = std::min<uint64_t>(pl.pair_cap, (uint64_t)kn[DMF_KNOB_PAIR_CAP]);
@@ -2161,13 +2188,13 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sj, (int)pl.ppose,
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
-                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb, (const unsigned long long*)b.ctl,
+                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb, b.ctl,
                            v->d_fault, (int)std::min<int64_t>(v->knob[DMF_KNOB_FAULT_INJECT], 1 << 20));
       else
         hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sj, (int)pl.ppose,
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
-                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb, (const unsigned long long*)b.ctl,
+                           (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb, b.ctl,
                            v->d_fault, (int)std::min<int64_t>(v->knob[DMF_KNOB_FAULT_INJECT], 1 << 20));
       DMF_LAUNCH_CHECK();
       if (staged && j == 0) {  // (batches j > 0 ran on the volume's stream)

@@ -49,8 +49,8 @@ enum dmf_knob {
   DMF_KNOB_A_HASH = 9,      /* pass A's histogram: 0 default (hashed, 2048 words, above 8192 bricks; direct
                                below), -1 always direct, k > 0 always hashed with k words (rounded up to a
                                power of two, 16..16384; a workgroup whose table overflows is redone with the direct one) */
-  DMF_KNOB_FAULT_INJECT = 10, /* test hook: k > 0 makes the first pair of every pass-B workgroup of the call's
-                                  first pose take k extra slots, so that passes A and B disagree (the results are
+  DMF_KNOB_FAULT_INJECT = 10, /* test hook: k > 0 makes the first pair of thread 0 of every pass-B workgroup of the
+                                  call's first pose take k extra slots, so that passes A and B disagree (the results are
                                   then invalid; dmf_fuse_status reports it, and no store leaves the pair
                                   buffers); 0 = off */
   DMF_KNOB_FWD_KERNEL = 11,  /* batched forward first hits (dmf_forward_first_hits_device): 0 default (a grid of

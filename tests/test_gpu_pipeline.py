@@ -262,8 +262,8 @@ def test_timed_mode_config4_shape():
 @pytest.mark.parametrize("extra", [1, 1 << 20])
 def test_pass_b_layout_guard(extra):
     """Pass B's record stores are guarded: with DMF_KNOB_FAULT_INJECT the
-    first pair of each pass-B workgroup of the first pose takes `extra` slots more than pass A
-    counted.  The call must neither fault
+    first pair of thread 0 of each pass-B workgroup of the first pose takes `extra` slots more
+    than pass A counted.  The call must neither fault
     nor store outside the pair records: the layout check reports the disagreement in
     d_stats[3] and through dmf_fuse_status (DMF_ERR_DEVICE_CHECK), the host form returns that
     status, and the volume is clean again afterwards (same counters as before, status ok).
