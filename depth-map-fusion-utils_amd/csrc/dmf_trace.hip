@@ -790,7 +790,9 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
 #if defined(DMF_EXP_REV_ITEMS)  // experiment builds: the spatial-order queue's shape
     constexpr int kSpItems = DMF_EXP_REV_ITEMS, kSpRefill = DMF_EXP_REV_REFILL, kSpBurst = DMF_EXP_REV_BURST;
 #else
-    constexpr int kSpItems = 64, kSpRefill = 8, kSpBurst = 16;
+    // (round 5, per-XCD queues: burst 32 5.24-5.25 ms vs 16 5.29-5.32, 24 5.25-5.26, 8 5.39-5.41;
+    // refill 4 / 12 / 16 at burst 16 within +-0.5 %: profiles/r05j/)
+    constexpr int kSpItems = 64, kSpRefill = 8, kSpBurst = 32;
 #endif
     const dim3 gridq((unsigned)((nelem + 4 * kRevItems - 1) / (4 * kRevItems)), (unsigned)P);
     const dim3 gridqs((unsigned)((nelem + 4 * kSpItems - 1) / (4 * kSpItems)), (unsigned)P);
