@@ -567,8 +567,21 @@ def main():
         fev.record(stream)  # creates the event
         _lib.check(L.dmf_fuse_set_phase_event(vol._h, C.c_void_p(fev.cuda_event)))
         phase = lambda i: fev  # noqa: E731  (re-recorded by each fusion call)
-    S.run_steps(rt, args.warmup, 2, clear, fuse, merge, phase=phase)
-    torch.cuda.synchronize(dev)
+    try:
+        S.run_steps(rt, args.warmup, 2, clear, fuse, merge, phase=phase)
+        torch.cuda.synchronize(dev)
+    except _lib.DmfError as ex:
+        # libdmf's RCCL merge failed on this node (every rank fails the same call): fall back to
+        # torch's all-reduce + finalize before anything is timed, and say so in the line
+        if comm_ptr is None:
+            raise
+        log(f"[rank {rank}] libdmf RCCL merge failed in warmup ({ex}); falling back to torch all_reduce")
+        comm_ptr, merge_mode = None, "torch"
+        rccl["fallback_reason"] = f"libdmf RCCL merge failed in warmup: {ex}"
+        rccl["merge"] = "fallback: torch.distributed all_reduce(sum) over RCCL + finalize of the world-padded grid"
+        torch.cuda.synchronize(dev)
+        S.run_steps(rt, max(args.warmup, 1), 2, clear, fuse, merge, phase=phase)
+        torch.cuda.synchronize(dev)
     stats.zero_()
     if world > 1:
         dist.barrier()

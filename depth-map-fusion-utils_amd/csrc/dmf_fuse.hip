@@ -667,6 +667,9 @@ __device__ inline void bk_rays_wg(const BkRaysArgs& A_, unsigned wg, uint32_t* h
   for (int i = threadIdx.x; i < nwords; i += blockDim.x) hist[i] = HASH ? kHashEmpty : 0u;
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+#if defined(DMF_EXP_A_PRIO)  // experiment builds: pass A's waves at a raised issue priority
+  __builtin_amdgcn_s_setprio(DMF_EXP_A_PRIO);
+#endif
   const int pw = (int)(wg / (unsigned)A_.wg_pose);
   const int q0 = (int)(wg - (unsigned)pw * (unsigned)A_.wg_pose) * A_.span;
   const int64_t pk0 = (int64_t)pw * A_.packets_pose + q0,
@@ -2184,6 +2187,9 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         hipLaunchKernelGGL(k_bk_scan<false>, dim3(1), dim3(1024), 0, sj, bg.nbricks, (const uint32_t*)b.cnt, b.off,
                            b.part_pref, b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       DMF_LAUNCH_CHECK();
+#if defined(DMF_EXP_B_AFTER_F)  // experiment builds: pass B of call i+1 never beside call i's phase F
+      if (staged && j == 0 && v->st_free_set[slot ^ 1]) DMF_HIP(hipStreamWaitEvent(sj, v->st_free[slot ^ 1], 0));
+#endif
       if (slab)
         hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sj, (int)pl.ppose,
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
