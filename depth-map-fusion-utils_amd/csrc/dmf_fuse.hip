@@ -1843,8 +1843,8 @@ static int cu_count(int device) {
 // into batches by the pairs they really make against the pair capacity (the rest of the
 // slot's budget, at most the geometric bound of the super-batch); the host launches jmax =
 // the batches the geometric bound rays x (1 + brick boundaries) would need, and the launches
-// past the device's batch count exit at once.  Budget (dmf_fuse_reserve): 45 % of the
-// device's HBM by default (~130 GB of MI355X's 288 GB), all of it for the one slot of serial
+// past the device's batch count exit at once.  Budget (dmf_fuse_reserve): 55 % of the
+// device's HBM by default (~158 GB of MI355X's 288 GB), all of it for the one slot of serial
 // calls, half of it for each of the two staging slots of pipelined calls: the 1024-pose
 // 512^3 anchor and the 256-pose 1024^3 shard each run as one batch either way.
 
