@@ -2295,6 +2295,14 @@ int dmf_fuse_get_variant(const dmf_volume* v, int32_t* variant) {
 int dmf_volume_set_knob(dmf_volume* v, int32_t knob, int64_t value) {
   if (!v) return fail(DMF_ERR_INVALID, "null volume");
   if (knob < 1 || knob >= DMF_KNOB_COUNT) return fail(DMF_ERR_INVALID, "unknown knob %d", knob);
+  if (knob == DMF_KNOB_BDIST_CAP) {
+    if (value < 0 || value > 255) return fail(DMF_ERR_INVALID, "brick distance cap %lld not in 1..255", (long long)value);
+    const int cap = value ? (int)value : kBrickDistCapDefault;
+    if (cap != v->brick_cap) {
+      v->brick_cap = cap;
+      v->bdist_valid = false;  // rebuilt at the next march
+    }
+  }
   v->knob[knob] = value;
   return DMF_OK;
 }

@@ -218,7 +218,8 @@ def declared_symbols():
 # include/dmf_diag.h: fusion implementations and per-volume knobs (diagnostics, A/B, tests)
 FUSE_DEFAULT, FUSE_LDS_BOX, FUSE_CELL_WALK, FUSE_SLAB = 0, 31, 40, 57
 KNOBS = {"super_poses": 1, "pair_cap": 2, "batch_poses": 3, "part_max": 4, "span": 5, "tail_split": 6,
-         "reverse_kernel": 7, "fwd_skip": 8, "a_hash": 9, "fault_inject": 10, "fwd_kernel": 11}
+         "reverse_kernel": 7, "fwd_skip": 8, "a_hash": 9, "fault_inject": 10, "fwd_kernel": 11,
+         "bdist_cap": 12}
 
 
 def fuse_status(vol):

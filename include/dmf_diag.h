@@ -55,7 +55,9 @@ enum dmf_knob {
                                   buffers); 0 = off */
   DMF_KNOB_FWD_KERNEL = 11,  /* batched forward first hits (dmf_forward_first_hits_device): 0 default (a grid of
                                 (tile block, pose): k_forward), 1 per-XCD unit queues (k_forward_x) */
-  DMF_KNOB_COUNT = 12
+  DMF_KNOB_BDIST_CAP = 12,   /* saturation of the brick distance field of the reverse / forward marches' empty-space
+                                jumps, in bricks (1..255; 0 = the default 63); rebuilt at the next march */
+  DMF_KNOB_COUNT = 13
 };
 int dmf_volume_set_knob(dmf_volume* v, int32_t knob, int64_t value);
 int dmf_volume_get_knob(const dmf_volume* v, int32_t knob, int64_t* value);

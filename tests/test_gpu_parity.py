@@ -136,10 +136,14 @@ def test_reverse_full_parity(oracle, engine, oeng):
     assert np.array_equal(a, c) and np.array_equal(b, d)
 
 
-def test_reverse_sparse_partial_bricks(oracle, engine, oeng):
+@pytest.mark.parametrize("cap", [0, 1, 2, 255])
+def test_reverse_sparse_partial_bricks(oracle, engine, oeng, cap):
     """Empty-space skipping stress: a sparse scatter of occupied cells in a grid whose
     dims are not multiples of the 8-cell brick and whose deltas are not powers of two;
-    cameras outside and inside the volume.  Lists and view/good flags must be exact."""
+    cameras outside and inside the volume; the brick distance field saturated at the default
+    (63), 1, 2 and 255 bricks (DMF_KNOB_BDIST_CAP: cubes of one brick up to cubes reaching past
+    the volume's faces, whose jumps may leave the volume at once).  Lists and view/good flags
+    must be exact."""
     rng = np.random.default_rng(21)
     bounds = (-0.45, 0.52, -0.4, 0.47, -0.33, 0.41)
     dims = (91, 77, 61)
@@ -156,6 +160,8 @@ def test_reverse_sparse_partial_bricks(oracle, engine, oeng):
     gv.setDimensions(*bounds)
     gv.setVolumeSize(*dims)
     gv.constructVolume()
+    from dmf_amd import _lib
+    _lib.set_knob(gv, "bdist_cap", cap)
     gv.integratePointCloud(pts, nn)
     assert np.array_equal(ov.occupied_cells_, gv.occupied_cells_)
     from dmf_amd import scene

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A/B of reverseRayTraceFast kernels (DMF_KNOB_REVERSE_KERNEL 0 = spatial order, 3 =
-occupied_cells_ order, 4 = per-XCD unit queues; argv[1] = comma-separated list, alternated) on bench.py's secondary workload: a 512^3 volume integrated from 16
+occupied_cells_ order, 4 = per-XCD unit queues; argv[1] = comma-separated list, alternated;
+argv[2] = comma-separated brick distance caps, DMF_KNOB_BDIST_CAP, 0 = default) on bench.py's secondary workload: a 512^3 volume integrated from 16
 back-projected 640x480 frames, 128 poses per launch.  Prints ms per launch for each and
 checks the visibility / good masks are identical (with a DMF_EXP_STATS library also the work
 queue's lane occupancy: busy lane-iterations / 64 x burst iterations)."""
@@ -45,7 +46,10 @@ words = (V + 63) // 64
 out = {"voxels": int(V), "poses": P}
 res = {}
 KS = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [3, 0, 3, 0]
-for kr in KS:
+CAPS = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
+for cap, kr in [(c, k) for c in CAPS for k in KS]:
+    tag = f"{kr}" if CAPS == [0] else f"{kr}_cap{cap}"
+    _lib.set_knob(vol, "bdist_cap", cap)
     _lib.set_knob(vol, "reverse_kernel", kr)
     vis = torch.zeros(P * words, dtype=torch.int64, device=dev)
     good = torch.zeros(P * words, dtype=torch.int64, device=dev)
@@ -54,8 +58,13 @@ for kr in KS:
     def run():
         _lib.check(L.dmf_reverse_visibility_device(vol._h, C.addressof(cam), d_poses.data_ptr(), P, 0, vis.data_ptr(),
                                                    good.data_ptr(), st.data_ptr()))
-    run()
     torch.cuda.synchronize(dev)
+    f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    f0.record(s)
+    run()  # the first call after a cap change rebuilds the distance field
+    f1.record(s)
+    torch.cuda.synchronize(dev)
+    out[f"first_ms_kernel{tag}"] = f0.elapsed_time(f1)
     st.zero_()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
@@ -63,12 +72,20 @@ for kr in KS:
         run()
     e1.record(s)
     torch.cuda.synchronize(dev)
-    out[f"ms_kernel{kr}"] = e0.elapsed_time(e1) / 5
-    out[f"samples_kernel{kr}"] = int(st[0].item()) // 5
+    out[f"ms_kernel{tag}"] = e0.elapsed_time(e1) / 5
+    out[f"samples_kernel{tag}"] = int(st[0].item()) // 5
     sv = st.cpu().numpy()
     if sv[10] > 0:  # DMF_EXP_STATS build: burst iterations (per wave) and busy lane-iterations
-        out[f"lane_busy_kernel{kr}"] = float(sv[11]) / (64.0 * float(sv[10]))
-    res[kr] = (vis.cpu().numpy(), good.cpu().numpy())
-k0 = KS[0]
+        out[f"lane_busy_kernel{tag}"] = float(sv[11]) / (64.0 * float(sv[10]))
+    res[tag] = (vis.cpu().numpy(), good.cpu().numpy())
+k0 = next(iter(res))
 out["masks_equal"] = bool(all(np.array_equal(res[k0][0], r[0]) and np.array_equal(res[k0][1], r[1]) for r in res.values()))
+# the committed oracle digest of every pose's good mask (tests/golden/march_digests.json)
+try:
+    import hashlib
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "march_digests.json")))["config4_shard_N1"]
+    out["good_digest_match"] = {t: hashlib.sha256(r[1].astype("<i8").tobytes()).hexdigest()[:16] for t, r in res.items()}
+    out["good_digest_expected"] = gold.get("reverse_good_digest")
+except (OSError, KeyError) as e:
+    out["good_digest_error"] = str(e)
 print(json.dumps(out), flush=True)
