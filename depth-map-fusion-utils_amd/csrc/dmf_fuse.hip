@@ -1084,8 +1084,14 @@ __device__ inline uint32_t bk_e30(int32_t e) {
 }
 
 
+// (experiment builds DMF_EXP_B_WAVES = n: the compiler keeps B's registers for n waves per SIMD)
+#if defined(DMF_EXP_B_WAVES)
+#define DMF_B_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_B_WAVES)))
+#else
+#define DMF_B_OCC
+#endif
 template <bool SLAB>
-__global__ __launch_bounds__(kBkPassThreadsBig) void k_bk_pairs(int packets_pose, int wg_pose, int span, BkGeom bg,
+__global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int packets_pose, int wg_pose, int span, BkGeom bg,
                                                          const ulonglong2* __restrict__ rays,
                                                          const uint64_t* __restrict__ paths,
                                                          const uint32_t* __restrict__ off,
