@@ -511,13 +511,25 @@ def main():
         elif not one_rccl_mapped():
             rccl["fallback_reason"] = "more than one librccl mapped: libdmf cannot use torch's communicator"
         if rccl["fallback_reason"] is None:
-            comm_ptr = D.torch_comm_ptr(device=dev)
-            nr, rk = C.c_int32(), C.c_int32()
-            _lib.check(L.dmf_comm_shape(comm_ptr, C.addressof(nr), C.addressof(rk)))
-            rccl["ranks"] = nr.value
-            if nr.value != world or rk.value != rank:
-                raise RuntimeError(f"RCCL communicator spans {nr.value} ranks (rank {rk.value}), world {world} "
-                                   f"rank {rank}")
+            try:
+                comm_ptr = D.torch_comm_ptr(device=dev)
+                nr, rk = C.c_int32(), C.c_int32()
+                _lib.check(L.dmf_comm_shape(comm_ptr, C.addressof(nr), C.addressof(rk)))
+                rccl["ranks"] = nr.value
+                if nr.value != world or rk.value != rank:
+                    raise RuntimeError(f"RCCL communicator spans {nr.value} ranks (rank {rk.value}), world {world} "
+                                       f"rank {rank}")
+            except (RuntimeError, AttributeError, TypeError, ValueError, _lib.DmfError) as ex:
+                comm_ptr = None
+                rccl["fallback_reason"] = f"torch's communicator not usable by libdmf: {ex}"
+        # every rank takes the same merge path: a rank alone in libdmf's collectives would hang
+        agree = torch.tensor([0 if comm_ptr is None else 1], dtype=torch.int32,
+                             device=dev if backend == "nccl" else torch.device("cpu"))
+        dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+        if int(agree.item()) == 0 and comm_ptr is not None:
+            comm_ptr = None
+            rccl["fallback_reason"] = "another rank cannot use torch's communicator from libdmf"
+        if comm_ptr is not None:
             rccl["merge"] = ("libdmf dmf_fuse_merge_finalize_device: RCCL ncclReduceScatter(hits, misses) + slab "
                              "finalize + ncclAllGather(int16) on torch's communicator")
         else:

@@ -319,6 +319,44 @@ __host__ __device__ inline int coarse_next(Coarse& w) {
   return s2 ? 2 : (s1 ? 1 : 0);
 }
 
+// coarse_next without its state: the axis of the next brick-boundary crossing of a ray now in
+// brick coordinates (b0, b1, b2).  On each moving axis the next boundary is fine crossing
+// k_a (into brick b_a + st_a); the earliest of those events in (T, axis) order (ev_before:
+// H_a |dq_b| against H_b |dq_a|, ties x < y < z) is the one coarse_next takes.  An axis
+// whose boundaries are all behind the ray's end never wins while crossings remain, so the
+// caller takes exactly coarse_total steps, as with coarse_next.  For pass B's rays past the
+// recorded path: no 64-bit walk state held across the replay.
+// (kept from being hoisted out of the replay loop: its operands are loop-invariant, and as
+// hoisted 64-bit values they would stay live across every ray's replay)
+__host__ __device__ inline int32_t pinned(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(x));
+#endif
+  return x;
+}
+__host__ __device__ inline int coarse_next_at(const QRay& r, int b0, int b1, int b2) {
+  int best = -1;
+  int64_t Hb = 0;
+  int32_t db = 0;
+  const int bc[3] = {b0, b1, b2};
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int32_t st = pinned(r.st[a]);
+    if (st == 0) continue;
+    const int32_t cs = pinned(r.cs[a]), da = pinned(r.adq[a]);
+    const int32_t nb = bc[a] + st;
+    const int32_t k = st > 0 ? nb * kB - cs - 1 : cs - nb * kB - kB;  // (nb may be -1: past the grid)
+    const int64_t H = (int64_t)pinned(r.h0[a]) + 2 * kQ * (int64_t)k;
+    // ev_before(r, a, H, best, Hb): H |dq_best| < Hb |dq_a| (a > best: ties keep best)
+    if (best < 0 || H * (int64_t)db < Hb * (int64_t)da) {
+      best = a;
+      Hb = H;
+      db = da;
+    }
+  }
+  return best;
+}
+
 // The coarse walk's crossing axes, 2 bits per brick boundary (step t at bits 2t, 2t + 1), for
 // the first kPathSteps boundaries: pass A records them with its walk so that pass B replays
 // the brick sequence without the 64-bit comparisons (a ray with more boundaries walks again).

@@ -547,20 +547,18 @@ __device__ inline void bk_coarse(const BkGeom& bg, const bk::QRay& R, F&& f) {
 }
 
 // Pass B's coarse walk: the brick sequence from the crossing axes pass A recorded (path, see
-// dmf_brick.hpp path_put), calling f exactly as bk_coarse does; a ray with more than
-// kPathSteps boundaries walks them again.
+// dmf_brick.hpp path_put), calling f exactly as bk_coarse does; past the path's kPathSteps
+// boundaries each next axis is recomputed from the current brick (coarse_next_at: no 64-bit
+// walk state lives across the replay, which held pass B at 116 VGPRs).
 template <class F>
 __device__ inline void bk_replay(const BkGeom& bg, const bk::QRay& R, uint64_t path, F&& f) {
   const int total = bk::coarse_total(R);
-  const bool walk = total > bk::kPathSteps;
-  bk::Coarse cw;
-  if (walk) bk::coarse_init(R, cw);
   int b0 = R.cs[0] >> bk::kLog, b1 = R.cs[1] >> bk::kLog, b2 = R.cs[2] >> bk::kLog;
   f(bk_index(bg, b0, b1, b2), -1, b0, b1, b2);
   for (int t = 0; t < total; ++t) {
     int a;
-    if (walk) a = bk::coarse_next(cw);  // (branch: skipped by the waves whose lanes all replay)
-    else a = bk::path_axis(path, t);
+    if (t < bk::kPathSteps) a = bk::path_axis(path, t);
+    else a = bk::coarse_next_at(R, b0, b1, b2);  // (branch: skipped by the waves whose lanes all replay)
     b0 += a == 0 ? R.st[0] : 0;
     b1 += a == 1 ? R.st[1] : 0;
     b2 += a == 2 ? R.st[2] : 0;

@@ -21,6 +21,19 @@
 
 namespace dmf {
 
+// (experiment builds DMF_EXP_REV_WAVES / DMF_EXP_FWD_WAVES = n: the compiler keeps the march
+// kernels' registers for n waves per SIMD)
+#if defined(DMF_EXP_REV_WAVES)
+#define DMF_REV_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_REV_WAVES)))
+#else
+#define DMF_REV_OCC
+#endif
+#if defined(DMF_EXP_FWD_WAVES)
+#define DMF_FWD_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_FWD_WAVES)))
+#else
+#define DMF_FWD_OCC
+#endif
+
 struct EnumList {
   const float* axes;  // xs | ys | zs (float-accumulated, RayTracingEngine.hpp:54-56)
   int32_t nax[3];
@@ -491,7 +504,7 @@ __global__ __launch_bounds__(256) void k_reverse_q(Geom g, DevVol vd, CamP cam, 
 // k_reverse_q), taken by the workgroup together: its waves share the CU's L1 lines as in
 // k_reverse_q, at the price of a barrier per unit; else one wave's 64 items per unit.
 template <int kItems, int kRefill, int kBurst, bool kWg>
-__global__ __launch_bounds__(256) void k_reverse_x(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses, int P,
+__global__ __launch_bounds__(256) DMF_REV_OCC void k_reverse_x(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ poses, int P,
                                                    int64_t nelem, const uint32_t* __restrict__ order, int depth0,
                                                    int max_steps, float dstar, int viz, uint64_t* __restrict__ vis_mask,
                                                    uint64_t* __restrict__ good_mask, int64_t words,
@@ -1058,7 +1071,7 @@ __device__ inline void fwd_ray(const Geom& g, const DevVol& vd, const CamP& cam,
 }
 
 template <bool kSkip>
-__global__ __launch_bounds__(256) void k_forward(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ pose,
+__global__ __launch_bounds__(256) DMF_FWD_OCC void k_forward(Geom g, DevVol vd, CamP cam, const PoseX* __restrict__ pose,
                                                  int zstart, int zdelta, int rdelta, int cdelta, int R, int C,
                                                  int32_t* __restrict__ k_out, int32_t* __restrict__ slot_out,
                                                  unsigned long long* __restrict__ hazards,

@@ -6,7 +6,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r05n
+O=${O_DIR:-gpurun_out/r05n}
 mkdir -p $O
 B=depth-map-fusion-utils_amd
 for rep in 1 2; do
