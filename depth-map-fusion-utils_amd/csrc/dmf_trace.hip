@@ -21,13 +21,14 @@
 
 namespace dmf {
 
-// (experiment builds DMF_EXP_REV_WAVES / DMF_EXP_FWD_WAVES = n: the compiler keeps the march
-// kernels' registers for n waves per SIMD)
-#if defined(DMF_EXP_REV_WAVES)
-#define DMF_REV_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_REV_WAVES)))
-#else
-#define DMF_REV_OCC
+// Register budgets of the march kernels: DMF_EXP_REV_WAVES / DMF_EXP_FWD_WAVES = n keeps their
+// registers for n waves per SIMD (experiment builds override them)
+// k_reverse_x at 7 waves per SIMD (72 VGPRs, no spill; 76 / 6 waves before: 5.19 vs 5.21 ms,
+// 8 waves spill and lose: 5.84 ms)
+#if !defined(DMF_EXP_REV_WAVES)
+#define DMF_EXP_REV_WAVES 7
 #endif
+#define DMF_REV_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_REV_WAVES)))
 #if defined(DMF_EXP_FWD_WAVES)
 #define DMF_FWD_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_FWD_WAVES)))
 #else
