@@ -273,6 +273,37 @@ def test_collision_cost_map(oracle, dmf):
     assert np.array_equal(dmf.collision_cost_map(gv, poses[:1]), np.zeros((1, 1), np.int32))
 
 
+def test_collision_cost_map_sparse(oracle, dmf):
+    """The cost map over a sparse scatter in a grid whose dims are not multiples of the brick and
+    whose deltas are not powers of two, with centres inside and outside the volume: equal to the
+    oracle's sequential willCollide."""
+    import dmf_amd
+    rng = np.random.default_rng(29)
+    bounds = (-0.45, 0.52, -0.4, 0.47, -0.33, 0.41)
+    dims = (91, 77, 61)
+    pts = rng.uniform([-0.44, -0.39, -0.32], [0.51, 0.46, 0.40], (150, 3)).astype(np.float32)
+    nn = np.tile(np.array([[0, 0, 1]], np.float32), (150, 1))
+    ov = oracle.Volume()
+    ov.setDimensions(*bounds)
+    ov.setVolumeSize(*dims)
+    ov.constructVolume()
+    ov.integratePointCloud(pts, nn)
+    gv = dmf_amd.VoxelVolume()
+    gv.setDimensions(*bounds)
+    gv.setVolumeSize(*dims)
+    gv.constructVolume()
+    gv.integratePointCloud(pts, nn)
+    V = 48
+    poses = np.tile(np.eye(3, 4, dtype=np.float32).reshape(1, 12), (V, 1))
+    lo, hi = np.array(bounds[0::2]), np.array(bounds[1::2])
+    poses[:, 3::4] = (lo + (hi - lo) * rng.uniform(-0.1, 1.1, (V, 3))).astype(np.float32)
+    got = dmf.collision_cost_map(gv, poses)
+    exp = oracle.collision_cost_map(ov, poses)
+    assert np.array_equal(got, exp)
+    coll = got == np.iinfo(np.int32).max
+    assert coll.any() and not coll.all()
+
+
 def test_collision_cost_map_device_invalid_centre(dmf):
     import ctypes as C
     import torch
