@@ -798,6 +798,26 @@ __global__ __launch_bounds__(1024) void k_bk_batches(int P, const unsigned long 
   // phase F, whose box leaves ~25 KiB of the CU's LDS)
   constexpr int kChunk = 1024;
   __shared__ unsigned long long spp[kChunk];
+  __shared__ unsigned long long s_tot;
+  // the common case, every pose in one batch: a parallel sum decides it (the greedy cut below
+  // is a serial loop of dependent LDS reads, ~10 us for 128 poses)
+  if (P <= max_poses) {
+    if (threadIdx.x == 0) s_tot = 0;
+    __syncthreads();
+    unsigned long long part = 0;
+    for (int i = (int)threadIdx.x; i < P; i += blockDim.x) part += pose_pairs[i];
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_down(part, o, 64);
+    if ((threadIdx.x & 63) == 0 && part) atomicAdd(&s_tot, part);
+    __syncthreads();
+    if (s_tot <= cap) {
+      if (threadIdx.x == 0) {
+        bt[0] = P > 0 ? 1u : 0u;
+        bt[1] = 0;
+        bt[2] = (uint32_t)P;
+      }
+      return;
+    }
+  }
   uint32_t J = 0;
   unsigned long long sum = 0;
   int n = 0;
@@ -826,6 +846,31 @@ __global__ __launch_bounds__(1024) void k_bk_batches(int P, const unsigned long 
   }
 }
 
+// pose_base[p][b] = brick b's pairs of poses p0 .. p-1 for p in [p0, p1); returns the total.
+// The loads of a brick's counts are independent: 16 in flight per round (the chain between
+// pass A and pass B is exposed in pipelined calls; 4 in flight took 21 us at 128 poses).
+__device__ inline uint32_t bk_pose_prefix(const uint32_t* __restrict__ pose_cnt, uint32_t* __restrict__ pose_base,
+                                          int nbricks, int b, int p0, int p1) {
+  constexpr int kF = 16;
+  uint32_t acc = 0;
+  int p = p0;
+  for (; p + kF <= p1; p += kF) {
+    uint32_t c[kF];
+#pragma unroll
+    for (int k = 0; k < kF; ++k) c[k] = pose_cnt[(size_t)(p + k) * nbricks + b];
+#pragma unroll
+    for (int k = 0; k < kF; ++k) {
+      pose_base[(size_t)(p + k) * nbricks + b] = acc;
+      acc += c[k];
+    }
+  }
+  for (; p < p1; ++p) {
+    pose_base[(size_t)p * nbricks + b] = acc;
+    acc += pose_cnt[(size_t)p * nbricks + b];
+  }
+  return acc;
+}
+
 // Brick lists of batch j (grid over bricks): cnt[b] = the batch's pairs in brick b, and
 // pose_base[p][b] = pairs of the batch's earlier poses in brick b (pass B places pose p's
 // pairs of brick b at off[b] + pose_base[p][b] + wg_base[wg][b] + slot).  Batches past
@@ -837,22 +882,7 @@ __global__ __launch_bounds__(256) void k_bk_batch_counts(int nbricks, int j, con
   const int b = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (b >= nbricks || (uint32_t)j >= bt[0]) return;
   const int p0 = (int)bt[1 + j], p1 = (int)bt[2 + j];
-  uint32_t acc = 0;
-  int p = p0;
-  for (; p + 4 <= p1; p += 4) {  // four independent loads in flight
-    const uint32_t c0 = pose_cnt[(size_t)p * nbricks + b], c1 = pose_cnt[(size_t)(p + 1) * nbricks + b],
-                   c2 = pose_cnt[(size_t)(p + 2) * nbricks + b], c3 = pose_cnt[(size_t)(p + 3) * nbricks + b];
-    pose_base[(size_t)p * nbricks + b] = acc;
-    pose_base[(size_t)(p + 1) * nbricks + b] = acc + c0;
-    pose_base[(size_t)(p + 2) * nbricks + b] = acc + c0 + c1;
-    pose_base[(size_t)(p + 3) * nbricks + b] = acc + c0 + c1 + c2;
-    acc += c0 + c1 + c2 + c3;
-  }
-  for (; p < p1; ++p) {
-    pose_base[(size_t)p * nbricks + b] = acc;
-    acc += pose_cnt[(size_t)p * nbricks + b];
-  }
-  cnt[b] = acc;
+  cnt[b] = bk_pose_prefix(pose_cnt, pose_base, nbricks, b, p0, p1);
 }
 
 // Scan of the brick counts (one workgroup): list offsets, write cursors, and the part
@@ -887,11 +917,28 @@ __device__ inline void bk_scan_body(int nbricks, const uint32_t* __restrict__ cn
   __syncthreads();
   const int per = (nbricks + 1023) / 1024;
   const int i0 = min(nbricks, t * per), i1 = min(nbricks, i0 + per);
+  // !BIG (<= 4096 bricks, <= 4 per lane): the lane's counts in registers, read once (the
+  // three passes below re-read them)
+  constexpr int kPer = 4;
+  uint32_t rc[kPer];
+  if constexpr (!BIG) {
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) rc[k] = i0 + k < i1 ? s_cnt[i0 + k] : 0u;
+  }
+  auto cnt_of = [&](int i) -> uint32_t {
+    if constexpr (BIG) return s_cnt[i];
+    else {
+      uint32_t r = rc[0];
+#pragma unroll
+      for (int k = 1; k < kPer; ++k) r = i - i0 == k ? rc[k] : r;
+      return r;
+    }
+  };
   unsigned long long sp = 0;
   uint32_t spt = 0;
   for (int i = i0; i < i1; ++i) {
-    sp += s_cnt[i];
-    spt += (s_cnt[i] + part_max - 1) / part_max;
+    sp += cnt_of(i);
+    spt += (cnt_of(i) + part_max - 1) / part_max;
   }
   s_pairs[t] = sp;
   s_parts[t] = spt;
@@ -911,10 +958,10 @@ __device__ inline void bk_scan_body(int nbricks, const uint32_t* __restrict__ cn
   for (int i = i0; i < i1; ++i) {
     off[i] = (uint32_t)base;
     part_pref[i] = pbase;
-    base += s_cnt[i];
-    const uint32_t np = (s_cnt[i] + part_max - 1) / part_max;
+    base += cnt_of(i);
+    const uint32_t np = (cnt_of(i) + part_max - 1) / part_max;
     pbase += np;
-    if (np) atomicAdd(&s_cls[size_class(s_cnt[i], np)], np);
+    if (np) atomicAdd(&s_cls[size_class(cnt_of(i), np)], np);
   }
   __syncthreads();
   if (t == 0) {  // class starts, largest class first
@@ -928,9 +975,9 @@ __device__ inline void bk_scan_body(int nbricks, const uint32_t* __restrict__ cn
   __syncthreads();
   pbase = pbase0;
   for (int i = i0; i < i1; ++i) {
-    const uint32_t np = (s_cnt[i] + part_max - 1) / part_max;
+    const uint32_t np = (cnt_of(i) + part_max - 1) / part_max;
     if (np) {
-      const uint32_t pos = atomicAdd(&s_cls[size_class(s_cnt[i], np)], np);
+      const uint32_t pos = atomicAdd(&s_cls[size_class(cnt_of(i), np)], np);
       for (uint32_t k = 0; k < np; ++k) order[pos + k] = make_uint2((uint32_t)i, k);  // (brick, part of it)
     }
     pbase += np;
@@ -991,11 +1038,30 @@ __global__ __launch_bounds__(1024) void k_bk_layout1(int P, const unsigned long 
   __shared__ uint32_t s_cnt[kBkLayout1Bricks];
   __shared__ unsigned long long s_pp[kBkLayout1Poses];
   const int t = threadIdx.x;
+  __shared__ unsigned long long s_tot;
+  bool one = false;  // every pose in one batch (decided by a parallel sum, as k_bk_batches)
   if (j == 0) {  // pose pair counts staged in LDS (one coalesced load; the cut below is serial)
-    for (int p = t; p < P; p += blockDim.x) s_pp[p] = pose_pairs[p];
+    if (t == 0) s_tot = 0;
     __syncthreads();
+    unsigned long long part = 0;
+    for (int p = t; p < P; p += blockDim.x) {
+      s_pp[p] = pose_pairs[p];
+      part += s_pp[p];
+    }
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_down(part, o, 64);
+    if ((t & 63) == 0 && part) atomicAdd(&s_tot, part);
+    __syncthreads();
+    one = P <= max_poses && s_tot <= cap;
+    if (one && t == 0) {
+      s_bt[0] = P > 0 ? 1u : 0u;
+      s_bt[1] = 0;
+      s_bt[2] = (uint32_t)P;
+      bt[0] = s_bt[0];
+      bt[1] = 0;
+      bt[2] = (uint32_t)P;
+    }
   }
-  if (t == 0) {
+  if (t == 0 && !one) {
     if (j == 0) {  // the batch cut of k_bk_batches (serial over <= 256 poses)
       uint32_t J = 0;
       unsigned long long sum = 0;
@@ -1027,21 +1093,7 @@ __global__ __launch_bounds__(1024) void k_bk_layout1(int P, const unsigned long 
   }
   const int p0 = (int)s_bt[1 + j], p1 = (int)s_bt[2 + j];
   for (int b = t; b < nbricks; b += blockDim.x) {  // k_bk_batch_counts
-    uint32_t acc = 0;
-    int p = p0;
-    for (; p + 4 <= p1; p += 4) {  // four independent loads in flight
-      const uint32_t c0 = pose_cnt[(size_t)p * nbricks + b], c1 = pose_cnt[(size_t)(p + 1) * nbricks + b],
-                     c2 = pose_cnt[(size_t)(p + 2) * nbricks + b], c3 = pose_cnt[(size_t)(p + 3) * nbricks + b];
-      pose_base[(size_t)p * nbricks + b] = acc;
-      pose_base[(size_t)(p + 1) * nbricks + b] = acc + c0;
-      pose_base[(size_t)(p + 2) * nbricks + b] = acc + c0 + c1;
-      pose_base[(size_t)(p + 3) * nbricks + b] = acc + c0 + c1 + c2;
-      acc += c0 + c1 + c2 + c3;
-    }
-    for (; p < p1; ++p) {
-      pose_base[(size_t)p * nbricks + b] = acc;
-      acc += pose_cnt[(size_t)p * nbricks + b];
-    }
+    const uint32_t acc = bk_pose_prefix(pose_cnt, pose_base, nbricks, b, p0, p1);
     cnt[b] = acc;
     s_cnt[b] = acc;
   }
