@@ -127,13 +127,14 @@ __global__ void k_stats_reduce(const unsigned long long* __restrict__ s, int n, 
   unsigned long long t = 0;
   for (int k = 0; k < kStatSlots; ++k) t += s[k * kStatWidth + c];
   if (c == 3 && fault) t += atomicExch(&fault[1], 0u);
-  out[c] += t;
+  if (t) atomicAdd(&out[c], t);
 }
 
-int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int n, uint32_t* fault) {
+int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int n, uint32_t* fault,
+              hipStream_t stream) {
   if (!d_user) return DMF_OK;
-  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(64), 0, v->stream, striped, n, (unsigned long long*)d_user,
-                     fault);
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(64), 0, stream ? stream : v->stream, striped, n,
+                     (unsigned long long*)d_user, fault);
   DMF_LAUNCH_CHECK();
   return DMF_OK;
 }
@@ -772,7 +773,7 @@ int dmf_volume_destroy(dmf_volume* v) {
   (void)hipDeviceSynchronize();
   free_state(v);
   if (v->switch_ev) (void)hipEventDestroy(v->switch_ev);
-  for (hipEvent_t e : {v->st_in, v->st_done[0], v->st_done[1], v->st_free[0], v->st_free[1], v->st_b[0], v->st_b[1]})
+  for (hipEvent_t e : {v->st_in, v->st_done[0], v->st_done[1], v->st_free[0], v->st_free[1], v->st_b[0], v->st_b[1], v->st_a[0], v->st_a[1]})
     if (e) (void)hipEventDestroy(e);
   if (v->stage) (void)hipStreamDestroy(v->stage);
   delete v;

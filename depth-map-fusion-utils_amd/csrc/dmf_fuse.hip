@@ -2094,13 +2094,13 @@ static int bk_release(dmf_volume* v) {
 // (k_bk_batch_counts, k_bk_scan), pass B and phase F; a launch past the device's batch
 // count exits at once.  Phase F reads its part count itself (its persistent workgroups exit
 // when the queue is empty).
-// Pipelined (staged): the pose table, pass A, the batch cut, the brick
-// layout and pass B of each super-batch run on the volume's staging stream into staging slot
-// s (alternating), after the caller's input stream and after the slot's previous reader
-// (event st_free[s]); phase F runs on the volume's stream after pass B's event; the input
-// stream waits for pass A (the inputs stay ordered before the caller's next writes).  Pass
-// A's statistics go to the slot's own striped buffer, summed into d_user on the volume's
-// stream.  Serial calls use slot 0 on the volume's stream; once the staging stream exists
+// Pipelined (staged): the pose table and pass A of each super-batch run on
+// the volume's staging stream into staging slot s (alternating), after the caller's input
+// stream and after the slot's previous reader (event st_free[s]), beside the previous call's
+// phase F; the batch cut, the brick layout, pass B and phase F run on the volume's stream
+// after pass A's event; the input stream waits for pass A (the inputs stay ordered before the
+// caller's next writes).  Pass A's statistics go to the slot's own striped buffer, summed into
+// d_user on the staging stream.  Serial calls use slot 0 on the volume's stream; once the staging stream exists
 // they record st_free[0] too, so that a later pipelined call on slot 0 waits for them.
 static int stage_init(dmf_volume* v) {
   if (v->stage) return DMF_OK;
@@ -2110,6 +2110,8 @@ static int stage_init(dmf_volume* v) {
     DMF_HIP(hipEventCreateWithFlags(&v->st_done[k], hipEventDisableTiming));
     DMF_HIP(hipEventCreateWithFlags(&v->st_free[k], hipEventDisableTiming));
     DMF_HIP(hipEventCreateWithFlags(&v->st_b[k], hipEventDisableTiming));
+    DMF_HIP(hipEventCreateWithFlags(&v->st_a[k], hipEventDisableTiming));
+    v->st_b_set[k] = false;
     v->st_free_set[k] = false;
   }
   // work already enqueued on the volume's stream (a serial call's slot 0 readers) precedes
@@ -2168,6 +2170,9 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       DMF_HIP(hipEventRecord(v->st_in, v->in_stream));
       DMF_HIP(hipStreamWaitEvent(sa, v->st_in, 0));
       if (v->st_free_set[slot]) DMF_HIP(hipStreamWaitEvent(sa, v->st_free[slot], 0));
+      // and after the previous call's pass B: this pass A then runs beside that call's phase F
+      // (launched at once, it would run beside pass B instead, and phase F alone)
+      if (v->st_b_set[slot ^ 1]) DMF_HIP(hipStreamWaitEvent(sa, v->st_b_ev[slot ^ 1], 0));
       void* t;
       DMF_TRY(scratch(v, slot ? kScStPoses1 : kScStPoses0, sizeof(PoseX) * (size_t)pl.PS, &t));
       DMF_TRY(pose_table_into(d_poses + (size_t)s0 * 12, (int)ps, (PoseX*)t, sa));
@@ -2201,17 +2206,25 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     }
     DMF_LAUNCH_CHECK();
     if (staged) {
+      // the layout, pass B and phase F on the volume's stream after pass A (event st_a): pass
+      // B follows the previous call's phase F in stream order (it never ran beside it: pass
+      // A's tail outlasts F), and phase F follows pass B with no cross-stream event (13 -> 7
+      // us per call).  Pass A's statistics are then summed here, on the staging stream
+      // (atomic sums: the previous call's are summed on the volume's stream meanwhile), off
+      // the chain to pass B; st_done (after them) orders the input stream, and the volume's
+      // stream after this call's phase F.
+      DMF_HIP(hipEventRecord(v->st_a[slot], sa));
+      DMF_HIP(hipStreamWaitEvent(v->stream, v->st_a[slot], 0));
+      if (st) DMF_TRY(stats_end(v, st_a, d_user, kStatWidth, nullptr, sa));
       DMF_HIP(hipEventRecord(v->st_done[slot], sa));
       DMF_HIP(hipStreamWaitEvent(v->in_stream, v->st_done[slot], 0));
-      if (st) {  // pass A's statistics, summed on the volume's stream after pass A
-        DMF_HIP(hipStreamWaitEvent(v->stream, v->st_done[slot], 0));
-        DMF_TRY(stats_end(v, st_a, d_user, kStatWidth));
-      }
     }
+    // everything after pass A: the volume's stream
+    const hipStream_t sl = v->stream;
     // small grids: batch cut, brick counts and scan in one launch per batch (k_bk_layout1)
     const bool layout1 = bg.nbricks <= kBkLayout1Bricks && ps <= kBkLayout1Poses;
     if (!layout1) {
-      hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sa, (int)ps, (const unsigned long long*)b.pose_pairs,
+      hipLaunchKernelGGL(k_bk_batches, dim3(1), dim3(1024), 0, sl, (int)ps, (const unsigned long long*)b.pose_pairs,
                          (unsigned long long)pl.pair_cap, pl.max_poses, b.bt);
       DMF_LAUNCH_CHECK();
     }
@@ -2219,11 +2232,9 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     const int64_t jm = pl.jmax(ps);
     for (int64_t j = 0; j < jm; ++j) {
       // batch j > 0 reuses the slot's pair records and part queue, so it follows batch j-1's
-      // phase F: on the volume's stream (in order after it, no event).  The host launches
-      // jmax triples from the one-pose bound; those past the device's batch count exit at
-      // once, and on the volume's stream they no longer hold the staging stream -- and with
-      // it the next call's pass A -- behind this call's phase F (1024^3: jmax 7, one batch).
-      const hipStream_t sj = staged && j > 0 ? v->stream : sa;
+      // phase F in stream order.  The host launches jmax triples from the one-pose bound;
+      // those past the device's batch count exit at once (1024^3: jmax 7, one batch).
+      const hipStream_t sj = sl;
       // (the scan zeroes phase F's queue head: no memset of ctl)
       if (layout1) {
         hipLaunchKernelGGL(k_bk_layout1, dim3(1), dim3(1024), 0, sj, (int)ps, (const unsigned long long*)b.pose_pairs,
@@ -2243,9 +2254,6 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
         hipLaunchKernelGGL(k_bk_scan<false>, dim3(1), dim3(1024), 0, sj, bg.nbricks, (const uint32_t*)b.cnt, b.off,
                            b.part_pref, b.ctl, b.order, pl.part_max, (const uint32_t*)b.bt, (int)j, pl.split_cu);
       DMF_LAUNCH_CHECK();
-#if defined(DMF_EXP_B_AFTER_F)  // experiment builds: pass B of call i+1 never beside call i's phase F
-      if (staged && j == 0 && v->st_free_set[slot ^ 1]) DMF_HIP(hipStreamWaitEvent(sj, v->st_free[slot ^ 1], 0));
-#endif
       if (slab)
         hipLaunchKernelGGL(k_bk_pairs<true>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sj, (int)pl.ppose,
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
@@ -2259,13 +2267,18 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                            (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb, b.ctl,
                            v->d_fault, (int)std::min<int64_t>(v->knob[DMF_KNOB_FAULT_INJECT], 1 << 20));
       DMF_LAUNCH_CHECK();
-      if (staged && j == 0) {  // (batches j > 0 ran on the volume's stream)
-        DMF_HIP(hipEventRecord(v->st_b[slot], sa));
-        DMF_HIP(hipStreamWaitEvent(v->stream, v->st_b[slot], 0));
-      }
       // the call's phase F begins (not while capturing: the record would become a graph node
       // and the caller's event would never be re-recorded by the graph's launches)
-      if (v->f_event && !capturing && s0 == 0 && j == 0) DMF_HIP(hipEventRecord(v->f_event, v->stream));
+      const bool fev = v->f_event && !capturing && s0 == 0 && j == 0;
+      if (fev) DMF_HIP(hipEventRecord(v->f_event, v->stream));
+      if (staged && j == 0) {
+        // pass B done: the next super-batch's pass A waits for it (the caller's phase event,
+        // recorded at the same point, serves when there is one: each record costs the chain
+        // to phase F a few us)
+        if (!fev) DMF_HIP(hipEventRecord(v->st_b[slot], sl));
+        v->st_b_ev[slot] = fev ? v->f_event : v->st_b[slot];
+        v->st_b_set[slot] = true;
+      }
       if (slab)
         hipLaunchKernelGGL((k_bk_fuse_s<kBkRefill, kBkSpread, kBkUnroll>), dim3(nfF), dim3(kBkThreads), 0, v->stream, g, bg,
                            (const uint4*)b.pra, (const uint32_t*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
@@ -2277,6 +2290,8 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       DMF_LAUNCH_CHECK();
       if (staged) DMF_HIP(hipEventRecord(v->st_free[slot], v->stream));  // batch j's phase F
     }
+    // pass A's statistics summed before the call's own (after phase F: off the chain)
+    if (staged) DMF_HIP(hipStreamWaitEvent(v->stream, v->st_done[slot], 0));
     if (staged || (v->stage && !capturing)) {  // the slot's last reader (phase F) is enqueued
       DMF_HIP(hipEventRecord(v->st_free[slot], v->stream));
       v->st_free_set[slot] = true;
@@ -2468,6 +2483,10 @@ int dmf_fuse_counters_to_linear_device(dmf_volume* v, const int32_t* d_tiled, in
 int dmf_fuse_set_phase_event(dmf_volume* v, void* event) {
   DMF_API_BEGIN
   if (!v) return fail(DMF_ERR_INVALID, "null volume");
+  // the next pass A no longer waits on the caller's old event (the wait only schedules it
+  // beside phase F: nothing depends on it, and the event may be destroyed after this)
+  for (int k = 0; k < 2; ++k)
+    if (v->st_b_ev[k] == v->f_event) v->st_b_set[k] = false;
   v->f_event = (hipEvent_t)event;
   return DMF_OK;
   DMF_API_END

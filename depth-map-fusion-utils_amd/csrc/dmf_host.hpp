@@ -73,8 +73,11 @@ constexpr int kStatSlots = 256, kStatWidth = 20;  // diagnostic builds: extra co
 constexpr int kStatSlots = 256, kStatWidth = 8;
 #endif
 int stats_begin(dmf_volume* v, unsigned long long** striped);
+// (on `stream`, the volume's stream by default; the sums are atomic: a pipelined call's
+// pass-A statistics are summed on the staging stream while the previous call's are on the
+// volume's)
 int stats_end(dmf_volume* v, const unsigned long long* striped, uint64_t* d_user, int ncounters,
-              uint32_t* fault = nullptr);
+              uint32_t* fault = nullptr, hipStream_t stream = nullptr);
 __device__ inline unsigned long long* stat_slot(unsigned long long* base) {
   return base ? base + kStatWidth * ((blockIdx.x + blockIdx.y * gridDim.x) & (kStatSlots - 1)) : nullptr;
 }

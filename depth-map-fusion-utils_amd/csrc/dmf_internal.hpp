@@ -252,8 +252,13 @@ struct dmf_volume {
   hipStream_t in_stream = nullptr;  // the caller's input stream
   hipStream_t stage = nullptr;      // staging stream (created on first use)
   hipEvent_t st_in = nullptr, st_done[2] = {nullptr, nullptr}, st_free[2] = {nullptr, nullptr};
-  hipEvent_t st_b[2] = {nullptr, nullptr};  // pass B of the slot's batch enqueued (staged pass B)
   bool st_free_set[2] = {false, false};
+  // pass B of the slot's call launched (the next call's pass A waits for it: it then runs beside
+  // that call's phase F)
+  hipEvent_t st_b[2] = {nullptr, nullptr};
+  hipEvent_t st_b_ev[2] = {nullptr, nullptr};  // the event that marks it (st_b, or the caller's phase event)
+  hipEvent_t st_a[2] = {nullptr, nullptr};  // the slot's pass A done (before its statistics' sum)
+  bool st_b_set[2] = {false, false};
   hipEvent_t f_event = nullptr;  // caller's phase-F event (dmf_fuse_set_phase_event)
   int st_slot = 0;
   // device-side layout check of the brick pipeline (dmf_fuse_status): [0] disagreements since
