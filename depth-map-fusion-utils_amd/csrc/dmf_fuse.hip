@@ -2170,9 +2170,6 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       DMF_HIP(hipEventRecord(v->st_in, v->in_stream));
       DMF_HIP(hipStreamWaitEvent(sa, v->st_in, 0));
       if (v->st_free_set[slot]) DMF_HIP(hipStreamWaitEvent(sa, v->st_free[slot], 0));
-      // and after the previous call's pass B: this pass A then runs beside that call's phase F
-      // (launched at once, it would run beside pass B instead, and phase F alone)
-      if (v->st_b_set[slot ^ 1]) DMF_HIP(hipStreamWaitEvent(sa, v->st_b_ev[slot ^ 1], 0));
       void* t;
       DMF_TRY(scratch(v, slot ? kScStPoses1 : kScStPoses0, sizeof(PoseX) * (size_t)pl.PS, &t));
       DMF_TRY(pose_table_into(d_poses + (size_t)s0 * 12, (int)ps, (PoseX*)t, sa));
@@ -2186,6 +2183,10 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     }
     DMF_HIP(hipMemsetAsync(b.pose_cnt, 0, pl.hist_bytes * (size_t)ps, sa));
     DMF_HIP(hipMemsetAsync(b.pose_pairs, 0, sizeof(unsigned long long) * (size_t)ps, sa));
+    // pass A after the previous super-batch's pass B: it then runs beside that super-batch's
+    // phase F (launched at once, it would run beside pass B instead, and phase F alone); the
+    // pose table and the zeroing above may run beside pass B
+    if (staged && v->st_b_set[slot ^ 1]) DMF_HIP(hipStreamWaitEvent(sa, v->st_b_ev[slot ^ 1], 0));
     BkRaysArgs ra{g, cp, d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
                   pl.wg_pose, pl.span, bg, b.rays, b.paths, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs,
                   st_a, b.ovl, 0};
