@@ -247,10 +247,11 @@ int dmf_fuse_reserve(dmf_volume* v, const dmf_camera* cam, int32_t P, uint64_t m
  * dmf_fuse_depth_device calls on this volume are ordered on `stream` (a hipStream_t the
  * caller writes them on) instead of on the volume's stream.  The brick pipeline then runs
  * each call's per-frame pass (pose table + pass A: back-projection, ray records, brick
- * counts), its device-side batch cut and brick layout and its pass B (pair records) on a
- * staging stream of the volume that waits only for `stream` and for its staging slot's
- * previous reader, so that they overlap the previous call's phase F; only phase F stays on
- * the volume's stream.  Two staging slots alternate between super-batches, each with its
+ * counts) on a staging stream of the volume that waits only for `stream`, for its staging
+ * slot's previous reader and (pass A itself) for the previous call's pass B, so that it
+ * overlaps the previous call's phase F; the device-side batch cut, brick layout, pass B
+ * (pair records) and phase F run on the volume's stream after pass A.  Two staging slots
+ * alternate between super-batches, each with its
  * own pair records and half of the fusion budget (dmf_fuse_reserve).  `stream` is made to
  * wait until the call's pass A has read the inputs, so inputs rewritten there afterwards
  * stay ordered.  Results are identical to the serial order, and serial and pipelined calls
