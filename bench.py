@@ -483,7 +483,7 @@ def main():
     pcam, pprm = C.addressof(cam), C.addressof(prm)
     # Pipelined fusion (DMF_BENCH_PIPE=0 = serial): the frames are resident and
     # never rewritten, so their input stream is an idle one; each call's pass A then runs on
-    # libdmf's staging stream beside the previous call's passes B and F.
+    # libdmf's staging stream beside the previous call's phase F.
     pipe = os.environ.get("DMF_BENCH_PIPE", "1") != "0"
     inp = torch.cuda.Stream(dev)
     torch.cuda.synchronize(dev)
@@ -621,7 +621,7 @@ def main():
                  else "finalize (no collective at N=1)",
                  "schedule": "merge of step i, then the zeroing of its buffer for step i+2, on the comm stream overlap fuse of step i+1 (2 counter buffers)"
                              + ("; they wait for step i+1's phase F to begin (dmf_fuse_set_phase_event)" if phase else "")
-                             + ("; pass A of fuse i+1 on libdmf's staging stream beside passes B and F of fuse i (the 'fuse' span is the "
+                             + ("; pass A of fuse i+1 on libdmf's staging stream beside phase F of fuse i (the 'fuse' span is the "
                                 "compute stream's: batch cut, B and F after waiting for that pass A)" if pipe else "")}
     # grid-wide streaming passes, priced separately: clear writes the
     # 2 tiled int32 counter arrays; finalize reads them and writes int16 log-odds
