@@ -223,6 +223,45 @@ def test_pipelined_then_serial_mixed():
     assert np.array_equal(hs, hp) and np.array_equal(ms, mp)
 
 
+def test_pipelined_with_phase_event():
+    """dmf_fuse_set_phase_event on a pipelined volume (what bench.py does): the caller's event
+    is recorded before every phase F and also marks the end of pass B for the next call's pass
+    A.  Pipelined calls with the event set, then with it replaced by a
+    second event and the first destroyed (the next pass A must not wait on it), then with none
+    equal the serial counters, and the events were recorded."""
+    poses, depth = _frames(12, seed=8)
+    hs, ms, ss = _run(256, poses, depth, 3, pipelined=False)
+    v = _Vol(256, 3)
+    torch = v.torch
+    d_depth = torch.from_numpy(depth.view(np.int16)).to(v.dev)
+    d_poses = torch.from_numpy(poses).to(v.dev)
+    torch.cuda.synchronize(v.dev)
+    ev1, ev2 = torch.cuda.Event(), torch.cuda.Event()
+    ev1.record(v.main)
+    ev2.record(v.main)
+    try:
+        v.pipelined(True)
+        v.reserve()
+        v._lib.check(v.L.dmf_fuse_set_phase_event(v.vol._h, C.c_void_p(ev1.cuda_event)))
+        v.call(d_depth[0:3], d_poses[0:3])
+        v.call(d_depth[3:6], d_poses[3:6])
+        v.inp.wait_event(ev1)  # what a caller does with it: its next work after phase F began
+        v._lib.check(v.L.dmf_fuse_set_phase_event(v.vol._h, C.c_void_p(ev2.cuda_event)))
+        ev1.synchronize()  # the second call's phase F has begun: the replaced event may go
+        del ev1            # (the next pass A no longer waits on it)
+        import gc
+        gc.collect()
+        v.call(d_depth[6:9], d_poses[6:9])
+        v._lib.check(v.L.dmf_fuse_set_phase_event(v.vol._h, None))
+        v.call(d_depth[9:12], d_poses[9:12])
+        hp, mp, sp = v.linear()
+        assert ev2.query()
+    finally:
+        v.close()
+    assert np.array_equal(ss[:5], sp[:5])
+    assert np.array_equal(hs, hp) and np.array_equal(ms, mp)
+
+
 def test_timed_mode_config4_shape():
     """The bench's timed mode at its own shape: 512^3, calls of the 128 frames of config 4's
     per-GPU shard (bench.py at N = 1), pipelined through an idle input stream exactly as
