@@ -192,15 +192,22 @@ __host__ __device__ inline void counts_at_sel(const QRay& r, int a, int32_t k, i
 // floor(X / Y) (X / Y < 2^12, relative error < 2^-51), and the remainder X - qY, exact by fma,
 // corrects it.  The tie rule of count_at (b > a: X - 1) is the same bias.  Checked against
 // counts_at by the brick self-test (check 7).
+// The reciprocal need not be correctly rounded: with X < 2^41 any inv within a few ulps of
+// 1 / Y puts X * inv within 2^-9 of X / Y, so q is within one of the floor and the remainder
+// step corrects it; the device takes v_rcp_f64 (the self-test checks inv perturbed by +-2 ulps).
 struct QRayF64 {
-  double adq[3], h[3], inv[3];  // |dq|, first-crossing numerator h0, RN(1 / (2Q |dq|)) (0: non-moving)
+  double adq[3], h[3], inv[3];  // |dq|, first-crossing numerator h0, ~1 / (2Q |dq|) (0: non-moving)
 };
 __host__ __device__ inline void qray_f64(const QRay& r, QRayF64& f) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     f.adq[a] = (double)r.adq[a];
     f.h[a] = (double)r.h0[a];
+#if defined(__HIP_DEVICE_COMPILE__)
+    f.inv[a] = r.adq[a] ? __builtin_amdgcn_rcp(2.0 * (double)kQ * (double)r.adq[a]) : 0.0;
+#else
     f.inv[a] = r.adq[a] ? 1.0 / (2.0 * (double)kQ * (double)r.adq[a]) : 0.0;
+#endif
   }
 }
 template <int A>

@@ -13,11 +13,12 @@
 //      R fits the record's 7 bits;
 //   5. the same walk from the 20-byte record (pack20 -> unpack20, scaled state beta);
 //   6. pass B's select-based counts_at_sel equals counts_at at the ray's crossing events;
-//   7. so does the double-arithmetic counts_at_f64;
+//   7. so does the double-arithmetic counts_at_f64 (also with its reciprocals 2 ulps off);
 //   8. pass B's replay of pass A's recorded crossing path (path_put / path_axis, the first
 //      kPathSteps boundaries; coarse_total = the walk's step count) lists the same bricks,
 //      and so does its replay past them by the stateless coarse_next_at (also over whole rays).
 // Build: make -C depth-map-fusion-utils_amd build/brick_selftest ; run: <exe> [rays] [seed]
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -294,6 +295,20 @@ int main(int argc, char** argv) {
           else counts_at_f64<2>(r, fd, k, c2);
           okc = c0[0] == c1[0] && c0[1] == c1[1] && c0[2] == c1[2] && c0[0] == c2[0] && c0[1] == c2[1] &&
                 c0[2] == c2[2];
+          // 7b. the same with the reciprocals 2 ulps off either way (the device's v_rcp_f64
+          //     need not be correctly rounded)
+          for (int dir = -1; dir <= 1 && okc; dir += 2) {
+            QRayF64 fp = fd;
+            for (int b = 0; b < 3; ++b)
+              if (fp.inv[b] != 0.0)
+                for (int u = 0; u < 2; ++u) fp.inv[b] = std::nextafter(fp.inv[b], dir < 0 ? 0.0 : 1.0);
+            int32_t c3[3];
+            if (a == 0) counts_at_f64<0>(r, fp, k, c3);
+            else if (a == 1) counts_at_f64<1>(r, fp, k, c3);
+            else counts_at_f64<2>(r, fp, k, c3);
+            okc = c0[0] == c3[0] && c0[1] == c3[1] && c0[2] == c3[2];
+            if (!okc) printf("ray %ld: counts_at_f64 with inv %+d ulps (%d, %d) differs\n", i, 2 * dir, a, k);
+          }
           if (!okc) printf("ray %ld: counts_at_sel / _f64(%d, %d) = %d %d %d / %d %d %d vs %d %d %d\n", i, a, k, c1[0],
                            c1[1], c1[2], c2[0], c2[1], c2[2], c0[0], c0[1], c0[2]);
           ++events;
