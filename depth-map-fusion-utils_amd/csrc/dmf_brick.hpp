@@ -152,6 +152,26 @@ __host__ __device__ inline int32_t opaque(int32_t x) {
   return x;
 }
 
+// a * b for |a|, |b| < 2^23: the low 32 bits of the product, as the plain 32-bit product gives
+// them.  On the device one v_mul_i32_i24 / v_mad_i32_i24, where the compiler's 32-bit integer
+// multiply is a v_mul_lo_u32 / v_mad_u64_u32 (passes A / B: step -0.2 %; the
+// experiment build -DDMF_EXP_MUL32 restores the 32-bit multiply).  The brick path's
+// operands are in range: brick coordinates and counts <= 1024, |dq| < 2^18 (<= 1024 cells per
+// axis, dmf_fuse.hip brick_path_ok).
+#if defined(__HIP_DEVICE_COMPILE__)
+// the LLVM intrinsic itself: HIP's __mul24 sign-extends its operands in IR, and when only some
+// low bits of a product are used (a cell coordinate & 31, a count times 2 kQ) the optimiser
+// drops that extension and selects the 32-bit multiply again
+extern "C" __device__ int32_t dmf_llvm_mul_i24(int32_t, int32_t) __asm("llvm.amdgcn.mul.i24");
+#endif
+__host__ __device__ inline int32_t mul24(int32_t a, int32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(DMF_EXP_MUL32)
+  return dmf_llvm_mul_i24(a, b);
+#else
+  return (int32_t)((uint32_t)a * (uint32_t)b);
+#endif
+}
+
 __host__ __device__ inline int32_t sel3(bool a0, bool a1, int32_t v0, int32_t v1, int32_t v2) {
   return a0 ? opaque(v0) : (a1 ? opaque(v1) : opaque(v2));
 }
@@ -459,9 +479,12 @@ __host__ __device__ inline uint32_t slab_rcode(int M, int32_t sb1, int32_t sb2, 
   const int32_t S = LM - pick3(cin[0], cin[1], cin[2], M);
   const uint32_t steps = (uint32_t)((cL[0] - cin[0]) + (cL[1] - cin[1]) + (cL[2] - cin[2]));
   // e = the state one M- and one minor crossing before the last cell's: within K_1 + K_M of a
-  // walk state (|b| < 2^29), so |e| < 2^30 and the wrapped 32-bit sum is exact
-  const int32_t e1 = (int32_t)((uint32_t)sb1 + (uint32_t)(LM - 1) * K1 - (uint32_t)(L1 - 1) * KM);
-  const int32_t e2 = (int32_t)((uint32_t)sb2 + (uint32_t)(LM - 1) * K2 - (uint32_t)(L2 - 1) * KM);
+  // walk state (|b| < 2^29), so |e| < 2^30 and the wrapped 32-bit sum is exact; (L - 1) K =
+  // 2 kQ (L - 1) |dq| mod 2^32 with 24-bit multiplies (K = 2 kQ |dq|)
+  const uint32_t k2 = (uint32_t)(2 * kQ);
+  const int32_t aM = (int32_t)(KM / k2), a1 = (int32_t)(K1 / k2), a2 = (int32_t)(K2 / k2);
+  const int32_t e1 = (int32_t)((uint32_t)sb1 + ((uint32_t)mul24(LM - 1, a1) - (uint32_t)mul24(L1 - 1, aM)) * k2);
+  const int32_t e2 = (int32_t)((uint32_t)sb2 + ((uint32_t)mul24(LM - 1, a2) - (uint32_t)mul24(L2 - 1, aM)) * k2);
   const uint32_t s = (L1 >= 1 && e1 < 0 ? 1u : 0u) + (L2 >= 1 && e2 < 0 ? 1u : 0u);
   return S == 0 ? steps : 3u * (uint32_t)S + s;
 }

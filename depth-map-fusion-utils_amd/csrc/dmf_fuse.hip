@@ -527,7 +527,9 @@ __host__ __device__ constexpr uint32_t bk_lds_off(uint32_t x, uint32_t y, uint32
 // word index of the same cell (< 33824: 16 bits in the pair record)
 __host__ __device__ constexpr uint32_t bk_lds_word(uint32_t x, uint32_t y, uint32_t z) { return x * kBkSx + y * kBkSy + z; }
 
-__device__ inline int bk_index(const BkGeom& bg, int x, int y, int z) { return (x * bg.nb[1] + y) * bg.nb[2] + z; }
+__device__ inline int bk_index(const BkGeom& bg, int x, int y, int z) {
+  return bk::mul24(bk::mul24(x, bg.nb[1]) + y, bg.nb[2]) + z;  // (24-bit multiplies, dmf_brick.hpp mul24)
+}
 
 // Coarse walk of one ray: calls f(brick index, axis of the boundary crossed to enter it
 // (-1 for the first brick), brick coordinates) for every brick it passes, in order.
@@ -1268,24 +1270,28 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
       if (SLAB) {  // b = b(0) + c_M K_m - c_m K_M;  b12 = b12(0) + c_1 K_2 - c_2 K_1
         const uint32_t cM = (uint32_t)bk::pick3(c[0], c[1], c[2], M), c1 = (uint32_t)bk::pick3(c[0], c[1], c[2], m1),
                        c2 = (uint32_t)bk::pick3(c[0], c[1], c[2], m2);
-        e.x = (uint32_t)sb1 + cM * Km1 - c1 * KM;
-        e.y = (uint32_t)sb2 + cM * Km2 - c2 * KM;
-        e.z = (uint32_t)sb12 + c1 * Km2 - c2 * Km1;
+        // c K = 2 kQ c |dq| mod 2^32: 24-bit multiplies (counts <= 1024, |dq| < 2^18)
+        constexpr uint32_t k2 = (uint32_t)(2 * bk::kQ);
+        auto m = [](uint32_t c, uint32_t a) { return (uint32_t)bk::mul24((int32_t)c, (int32_t)a); };
+        e.x = (uint32_t)sb1 + (m(cM, a1) - m(c1, aM)) * k2;
+        e.y = (uint32_t)sb2 + (m(cM, a2) - m(c2, aM)) * k2;
+        e.z = (uint32_t)sb12 + (m(c1, a2) - m(c2, a1)) * k2;
       } else {
         e.x = e01 + (uint32_t)c[0] * K1 - (uint32_t)c[1] * K0;
         e.y = e02 + (uint32_t)c[0] * K2 - (uint32_t)c[2] * K0;
         e.z = e12 + (uint32_t)c[1] * K2 - (uint32_t)c[2] * K1;
       }
-      const uint32_t x = (uint32_t)(R.cs[0] + R.st[0] * c[0]) & m5, y = (uint32_t)(R.cs[1] + R.st[1] * c[1]) & m5,
-                     z = (uint32_t)(R.cs[2] + R.st[2] * c[2]) & m5;
+      const uint32_t x = (uint32_t)(R.cs[0] + bk::mul24(R.st[0], c[0])) & m5,
+                     y = (uint32_t)(R.cs[1] + bk::mul24(R.st[1], c[1])) & m5,
+                     z = (uint32_t)(R.cs[2] + bk::mul24(R.st[2], c[2])) & m5;
       e.w = bk_lds_word(x, y, z);
       return e;
     };
     // brick-local word of the cell before the crossing (axis a) that produced counts c
     auto last_before = [&](const int32_t c[3], int a) {
-      const uint32_t x = (uint32_t)(R.cs[0] + R.st[0] * (c[0] - (a == 0))) & m5,
-                     y = (uint32_t)(R.cs[1] + R.st[1] * (c[1] - (a == 1))) & m5,
-                     z = (uint32_t)(R.cs[2] + R.st[2] * (c[2] - (a == 2))) & m5;
+      const uint32_t x = (uint32_t)(R.cs[0] + bk::mul24(R.st[0], c[0] - (a == 0))) & m5,
+                     y = (uint32_t)(R.cs[1] + bk::mul24(R.st[1], c[1] - (a == 1))) & m5,
+                     z = (uint32_t)(R.cs[2] + bk::mul24(R.st[2], c[2] - (a == 2))) & m5;
       return bk_lds_word(x, y, z);
     };
     auto put = [&](uint32_t slot, uint4 e, uint32_t last, uint32_t steps, bool ends) {
