@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import csv
+import datetime
 import ctypes as C
 import glob
 import hashlib
@@ -361,6 +362,11 @@ def free_port():
         return s.getsockname()[1]
 
 
+class MergeError(RuntimeError):
+    """libdmf's merge (dmf_fuse_merge_finalize_device) failed: the only error the warmup's RCCL
+    fallback takes."""
+
+
 def launch_command(args, argv):
     """The torch.distributed.run command of `bench.py --gpus N` (N > 1, no WORLD_SIZE): one rank
     per GPU of this node, rendezvous on 127.0.0.1, every bench argument forwarded unchanged
@@ -444,11 +450,17 @@ def main():
     backend = os.environ.get("DMF_BENCH_BACKEND", "nccl")
     local_rank = local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local_rank)
+    ctl_group = None
     if world > 1:
+        # torch's collectives time out instead of hanging for ever
+        tmo = datetime.timedelta(seconds=int(os.environ.get("DMF_BENCH_DIST_TIMEOUT_S", "600")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
+        # a CPU group for the ranks' agreement on the merge path (it must work whatever state
+        # the GPU communicator is in)
+        ctl_group = dist.new_group(backend="gloo", timeout=tmo)
 
     grid = args.grid
     P = args.poses_per_gpu
@@ -552,7 +564,10 @@ def main():
         c = bufs[b]
         if comm_ptr is not None or world == 1:
             # N = 1: no communicator, the finalize alone (on the comm stream, behind fuse(i+1))
-            D.merge_finalize_device(vol, c, pprm, logodds, comm_ptr, rt.lanes["comm"].cuda_stream)
+            try:
+                D.merge_finalize_device(vol, c, pprm, logodds, comm_ptr, rt.lanes["comm"].cuda_stream)
+            except _lib.DmfError as ex:  # only the merge's own failures may take the fallback
+                raise MergeError(str(ex)) from ex
         else:
             # fallback: torch's all-reduce (RCCL, or gloo), issued on the comm lane (the current
             # stream here); the finalize of every slab of the world-padded counters follows it on
@@ -579,14 +594,25 @@ def main():
         fev.record(stream)  # creates the event
         _lib.check(L.dmf_fuse_set_phase_event(vol._h, C.c_void_p(fev.cuda_event)))
         phase = lambda i: fev  # noqa: E731  (re-recorded by each fusion call)
+    failed = None
     try:
         S.run_steps(rt, args.warmup, 2, clear, fuse, merge, phase=phase)
         torch.cuda.synchronize(dev)
-    except _lib.DmfError as ex:
-        # libdmf's RCCL merge failed on this node (every rank fails the same call): fall back to
-        # torch's all-reduce + finalize before anything is timed, and say so in the line
+    except MergeError as ex:  # a fusion error (NOMEM, RANGE ...) is not a merge failure: it raises
         if comm_ptr is None:
             raise
+        failed = ex
+    if comm_ptr is not None and world > 1:
+        # the ranks agree on the fallback over the CPU group: one rank's failure moves every
+        # rank to torch's all-reduce (a rank alone in libdmf's collective would wait for ever)
+        flag = torch.tensor([0 if failed is None else 1], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=ctl_group)
+        if int(flag.item()) and failed is None:
+            failed = RuntimeError("another rank's libdmf RCCL merge failed in warmup")
+    if failed is not None:
+        # libdmf's RCCL merge failed: fall back to torch's all-reduce + finalize before anything
+        # is timed, and say so in the line
+        ex = failed
         log(f"[rank {rank}] libdmf RCCL merge failed in warmup ({ex}); falling back to torch all_reduce")
         comm_ptr, merge_mode = None, "torch"
         rccl["fallback_reason"] = f"libdmf RCCL merge failed in warmup: {ex}"
@@ -623,16 +649,51 @@ def main():
                              + ("; they wait for step i+1's phase F to begin (dmf_fuse_set_phase_event)" if phase else "")
                              + ("; pass A of fuse i+1 on libdmf's staging stream beside phase F of fuse i (the 'fuse' span is the "
                                 "compute stream's: batch cut, B and F after waiting for that pass A)" if pipe else "")}
+    # the merged grid of the timed steps (before the isolated re-timings below overwrite it)
+    digest = hashlib.sha256(logodds[:ncell].cpu().numpy().tobytes()).hexdigest()[:16]
     # grid-wide streaming passes, priced separately: clear writes the
-    # 2 tiled int32 counter arrays; finalize reads them and writes int16 log-odds
+    # 2 tiled int32 counter arrays; finalize reads them and writes int16 log-odds.  In the timed
+    # steps they run on the comm stream BESIDE the next call's phase F (by design), so their
+    # event spans there are spans, not kernel durations: the *_isolated entries below re-time
+    # each alone on the idle GPU after the timed region
     clear_bytes = 2 * 4 * nct
-    streaming = {
-        "clear": {"ms": clear_ms, "bytes": clear_bytes, "GBps": clear_bytes / (clear_ms * 1e-3) / 1e9,
-                  "frac": clear_bytes / (clear_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+    fin_bytes = 10 * ncell
+
+    def rate(ms_, nbytes, **kw):
+        return dict({"ms": ms_, "bytes": nbytes, "GBps": nbytes / (ms_ * 1e-3) / 1e9 if ms_ else None,
+                     "frac": nbytes / (ms_ * 1e-3) / 1e9 / HBM_PEAK_GBS if ms_ else None}, **kw)
+    streaming = {"clear_span_overlapped": rate(clear_ms, clear_bytes, note="event span on the comm stream beside "
+                                                                      "the next call's phase F (not a duration)")}
     if world == 1:
-        fin_bytes = 10 * ncell
-        streaming["finalize"] = {"ms": merge_ms, "bytes": fin_bytes, "GBps": fin_bytes / (merge_ms * 1e-3) / 1e9,
-                                 "frac": fin_bytes / (merge_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        streaming["finalize_span_overlapped"] = rate(merge_ms, fin_bytes, note="event span on the comm stream "
+                                                                             "beside the next call's phase F")
+    # isolated re-timing: each pass alone on the compute stream, GPU idle
+    torch.cuda.synchronize(dev)
+    niso = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        bufs[0].zero_()
+    e0.record(stream)
+    for _ in range(niso):
+        bufs[0].zero_()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    streaming["clear_isolated"] = rate(e0.elapsed_time(e1) / niso, clear_bytes,
+                                       kernel="torch zero_ of the [hits | misses] int32 counters, alone")
+
+    def fin_whole():
+        _lib.check(L.dmf_fuse_finalize_slab_device(vol._h, bufs[1].data_ptr(), pprm, logodds.data_ptr(), world, -1,
+                                                   stream.cuda_stream))
+    for _ in range(3):
+        fin_whole()
+    e0.record(stream)
+    for _ in range(niso):
+        fin_whole()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    streaming["finalize_isolated"] = rate(e0.elapsed_time(e1) / niso, fin_bytes,
+                                          kernel="dmf::k_finalize over the whole grid (2 x int32 read + int16 "
+                                                 "write per cell), alone")
     if st[3] != 0:  # pass B's device-side layout check (dmf_fuse_status): the counters are invalid
         raise RuntimeError(f"fusion layout check failed {st[3]} times")
     _lib.fuse_status(vol)  # raises DmfError(DMF_ERR_DEVICE_CHECK) if any call disagreed
@@ -667,7 +728,6 @@ def main():
     # are pipelined (they overlap: no per-call duration), the call's HIP-event span when serial
     step_ms = ms if pipe else fuse_ms
     achieved = bytes_launch / (step_ms * 1e-3) / 1e9
-    digest = hashlib.sha256(logodds[:ncell].cpu().numpy().tobytes()).hexdigest()[:16]
     golden = expected_digest(grid, P * world)
 
     result = None

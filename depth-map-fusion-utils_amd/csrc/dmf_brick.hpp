@@ -212,9 +212,11 @@ __host__ __device__ inline void counts_at_sel(const QRay& r, int a, int32_t k, i
 // floor(X / Y) (X / Y < 2^12, relative error < 2^-51), and the remainder X - qY, exact by fma,
 // corrects it.  The tie rule of count_at (b > a: X - 1) is the same bias.  Checked against
 // counts_at by the brick self-test (check 7).
-// The reciprocal need not be correctly rounded: with X < 2^41 any inv within a few ulps of
-// 1 / Y puts X * inv within 2^-9 of X / Y, so q is within one of the floor and the remainder
-// step corrects it; the device takes v_rcp_f64 (the self-test checks inv perturbed by +-2 ulps).
+// The reciprocal need not be correctly rounded: with X / Y < 2^12, an inv of relative error
+// eps puts X * inv within 2^12 eps of X / Y, so q stays within one of the floor -- which the
+// remainder step corrects -- while eps < 2^-12.  The device takes v_rcp_f64, whose documented
+// precision (2^29 ulps of a double) is a relative error near 2^-23; the self-test (check 7b)
+// runs the counts with inv perturbed by +-2 ulps and by relative errors of +-2^-22 and +-2^-14.
 struct QRayF64 {
   double adq[3], h[3], inv[3];  // |dq|, first-crossing numerator h0, ~1 / (2Q |dq|) (0: non-moving)
 };

@@ -753,13 +753,15 @@ int dmf_volume_create(dmf_volume** out, int32_t device) {
   auto* v = new dmf_volume();
   v->device = device;
   v->dstar = angle_threshold();
-  // brick-fusion scratch budget: 55 % of the device's HBM (~158 GB of MI355X's 288 GB; the
+  // brick-fusion scratch budget: 45 % of the device's HBM (~130 GB of MI355X's 288 GB; the
   // two staging slots of pipelined calls get half each), at least 8 GiB -- every pose batch a
   // smaller pair capacity forces costs its own passes and counter flushes (the device cuts
   // the batches by the pairs a call really makes).  Config 5's 1024^3 shard (2.85G pairs +
-  // 11.5 GB of per-pose tables per slot) needs 55 %: at 45 % it ran in two batches (round 5,
-  // 68.6 ms vs one batch).  A volume only allocates what its plan uses (dmf_fuse_plan).
-  v->bk_budget = std::max<uint64_t>(8ull << 30, (uint64_t)prop.totalGlobalMem / 20 * 11);
+  // the per-pose tables) runs as two batches per pipelined call at 45 %, in the same time as
+  // one batch at 55 % (round 5: 68.6 ms either way); the rest of the device
+  // stays free for a second volume or the caller.  A volume only allocates what
+  // its plan uses (dmf_fuse_plan); dmf_fuse_reserve sets another budget.
+  v->bk_budget = std::max<uint64_t>(8ull << 30, (uint64_t)prop.totalGlobalMem / 20 * 9);
   *out = v;
   return DMF_OK;
   DMF_API_END

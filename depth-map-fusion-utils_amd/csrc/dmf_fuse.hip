@@ -758,11 +758,10 @@ __device__ inline void bk_rays_wg(const BkRaysArgs& A_, unsigned wg, uint32_t* h
     return;
   }
   uint32_t* const pc = A_.pose_cnt + (size_t)pw * bg.nbricks;
-  // the workgroup's touched bricks: [count | uint16 brick ids | uint32 pair counts] (pass B
-  // initialises only these, and checks the slots it took per brick against the counts)
+  // the workgroup's touched bricks: [count | (brick id | pair count << 16) per brick] (pass B
+  // initialises only these, and checks the slots it took per brick against the counts; a
+  // workgroup makes at most span * 64 <= 65535 pairs in one brick, bk_plan)
   uint32_t* const row = A_.wg_list + (size_t)wg * (size_t)A_.wgl_stride;
-  uint16_t* const ids = (uint16_t*)(row + 1);
-  uint32_t* const cnts = row + 1 + (bg.nbricks + 1) / 2;
   unsigned long long mine = 0;
   for (int i = threadIdx.x; i < nwords; i += blockDim.x) {
     uint32_t b, n;
@@ -781,16 +780,14 @@ __device__ inline void bk_rays_wg(const BkRaysArgs& A_, unsigned wg, uint32_t* h
         if (nn) {
           A_.wg_base[(size_t)wg * bg.nbricks + bb] = atomicAdd(&pc[bb], nn);
           const uint32_t k = atomicAdd(&sh[0], 1u);
-          ids[k] = (uint16_t)bb;
-          cnts[k] = nn;
+          row[1 + k] = bb | nn << 16;
           mine += nn;
         }
       }
     } else if (n) {
       A_.wg_base[(size_t)wg * bg.nbricks + b] = atomicAdd(&pc[b], n);
       const uint32_t k = atomicAdd(&sh[0], 1u);
-      ids[k] = (uint16_t)b;
-      cnts[k] = n;
+      row[1 + k] = b | n << 16;
       mine += n;
     }
   }
@@ -1213,14 +1210,13 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
   {
     const uint32_t* row = wg_list + (size_t)blockIdx.x * (size_t)wgl_stride;
     const uint32_t nl = row[0];
-    const uint16_t* ids = (const uint16_t*)(row + 1);
 #if DMF_B_GUARD != 0
     // bricks pass A did not count here: any slot taken from them is out of range (checked)
     for (int i = threadIdx.x; i < bg.nbricks; i += blockDim.x) hist[i] = kBkSlotSentinel;
     __syncthreads();
 #endif
     for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x) {
-      const int i = ids[k];
+      const int i = (int)(row[1 + k] & 0xffffu);
       hist[i] = off[i] + pbz[i] + wb[i];
     }
   }
@@ -1385,19 +1381,18 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
   {
     const uint32_t* row = wg_list + (size_t)blockIdx.x * (size_t)wgl_stride;
     const uint32_t nl = row[0];
-    const uint16_t* ids = (const uint16_t*)(row + 1);
-    const uint32_t* cnts = row + 1 + (bg.nbricks + 1) / 2;
     uint32_t bad = over > total ? 1u : 0u;  // a slot past the records (or from an uncounted brick)
 #if defined(DMF_EXP_LAYOUT_DEBUG)
     if (bad) printf("B over: wg %u j %d lane %u over %u total %u\n", blockIdx.x, j, threadIdx.x, over, total);
 #endif
     for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x) {
-      const int i = ids[k];
-      bad += hist[i] != off[i] + pbz[i] + wb[i] + cnts[k] ? 1u : 0u;
+      const uint32_t e = row[1 + k];
+      const int i = (int)(e & 0xffffu);
+      bad += hist[i] != off[i] + pbz[i] + wb[i] + (e >> 16) ? 1u : 0u;
 #if defined(DMF_EXP_LAYOUT_DEBUG)
-      if (hist[i] != off[i] + pbz[i] + wb[i] + cnts[k])
+      if (hist[i] != off[i] + pbz[i] + wb[i] + (e >> 16))
         printf("B count: wg %u j %d brick %d hist %u off %u pbz %u wb %u cnt %u total %u\n", blockIdx.x, j, i, hist[i],
-               off[i], pbz[i], wb[i], cnts[k], total);
+               off[i], pbz[i], wb[i], e >> 16, total);
 #endif
     }
     if (bad) {
@@ -2012,14 +2007,17 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
     pl.hash_log = 11;
     pl.span = 128;
   }
-  if (kn[DMF_KNOB_SPAN] > 0) pl.span = (int)std::max<int64_t>(4, std::min<int64_t>(kn[DMF_KNOB_SPAN], 4096));
+  // (at most 1023 packets: a workgroup's pairs per brick, <= span * 64, fit the 16-bit counts
+  // of pass A's histogram and of its touched-brick list)
+  if (kn[DMF_KNOB_SPAN] > 0) pl.span = (int)std::max<int64_t>(4, std::min<int64_t>(kn[DMF_KNOB_SPAN], 1023));
   if (kn[DMF_KNOB_PART_MAX] > 0)
     pl.part_max = (uint32_t)std::max<int64_t>(1024, std::min<int64_t>(kn[DMF_KNOB_PART_MAX], kBkPartMax));
   pl.wg_pose = (int)((pl.ppose + pl.span - 1) / pl.span);
   pl.hist_bytes = sizeof(uint32_t) * (size_t)pl.bg.nbricks;
   // per pose: ray records, per-workgroup brick bases, pose counts and bases, pose pairs + batch table
-  // touched-brick list per workgroup: count + uint16 ids + uint32 pair counts (pass B's layout check)
-  pl.wgl_stride = 1 + (pl.bg.nbricks + 1) / 2 + pl.bg.nbricks;
+  // touched-brick list per workgroup: count + one word per touched brick (uint16 id | uint16
+  // pair count: pass B's layout check; ADVICE r5 -- 1.5 words per brick before)
+  pl.wgl_stride = 1 + pl.bg.nbricks;
   pl.per_pose_bytes = (uint64_t)rays_pose * (sizeof(ulonglong2) + sizeof(uint64_t)) + (uint64_t)pl.wg_pose * pl.hist_bytes +
                       (uint64_t)pl.wg_pose * sizeof(uint32_t) * (uint64_t)pl.wgl_stride + 2 * (uint64_t)pl.hist_bytes +
                       sizeof(unsigned long long) + sizeof(uint32_t);
@@ -2057,7 +2055,6 @@ static int bk_attributes() {
   static std::atomic<bool> attr_set{false};
   if (!attr_set.load()) {
     const int lds = (int)(sizeof(uint32_t) * 32768);
-    DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays_recover, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     DMF_HIP(hipFuncSetAttribute((const void*)k_bk_rays_hash, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -2201,8 +2198,9 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
   BkBufs b;
   if (staged) DMF_TRY(stage_init(v));
   const bool slab = v->fuse_variant != DMF_FUSE_CELL_WALK;
-  // pass A with 16-bit histogram counts (a workgroup's pairs per brick <= span * 64 rays)
-  const bool a16 = (int64_t)pl.span * 64 <= 65535;
+  // pass A with 16-bit histogram counts (a workgroup's pairs per brick <= span * 64 rays; the
+  // plan holds span <= 1023)
+  if ((int64_t)pl.span * 64 > 65535) return fail(DMF_ERR_RANGE, "pass A span %d exceeds 16-bit counts", pl.span);
   const unsigned nf = (unsigned)cu_count(v->device);
   // phase F's persistent workgroups: one per CU (32^3 bricks); an experiment build with
   // smaller bricks holds as many per CU as fit
@@ -2247,7 +2245,7 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
     BkRaysArgs ra{g, cp, d_depth + (size_t)s0 * cp.H * cp.W, tab_a, prm->dmin_mm, prm->dmax_mm, pl.pkx, (int)pl.ppose,
                   pl.wg_pose, pl.span, bg, b.rays, b.paths, b.pose_cnt, b.wgb, b.wgl, pl.wgl_stride, b.pose_pairs,
                   st_a, b.ovl, 0};
-    if (a16 && pl.hash_log > 0) {
+    if (pl.hash_log > 0) {
       // hashed histogram (8 KB: beside phase F's box), then the overflowed workgroups (if any)
       // with the direct table
       ra.hash_log = pl.hash_log;
@@ -2256,11 +2254,9 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       DMF_LAUNCH_CHECK();
       hipLaunchKernelGGL(k_bk_rays_recover, dim3(nf), dim3(kBkPassThreadsBig), sizeof(uint32_t) * ((bg.nbricks + 1) / 2),
                          sa, ra);
-    } else if (a16) {
+    } else {
       hipLaunchKernelGGL(k_bk_rays<true>, dim3(nwg), dim3(pl.ab_threads), sizeof(uint32_t) * ((bg.nbricks + 1) / 2), sa,
                          ra);
-    } else {
-      hipLaunchKernelGGL(k_bk_rays<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sa, ra);
     }
     DMF_LAUNCH_CHECK();
     if (staged) {
@@ -2425,7 +2421,7 @@ int dmf_volume_set_knob(dmf_volume* v, int32_t knob, int64_t value) {
   if (!v) return fail(DMF_ERR_INVALID, "null volume");
   if (knob < 1 || knob >= DMF_KNOB_COUNT) return fail(DMF_ERR_INVALID, "unknown knob %d", knob);
   if (knob == DMF_KNOB_BDIST_CAP) {
-    if (value < 0 || value > 255) return fail(DMF_ERR_INVALID, "brick distance cap %lld not in 1..255", (long long)value);
+    if (value < 0 || value > 255) return fail(DMF_ERR_INVALID, "brick distance cap %lld not in 0..255 (0 = default)", (long long)value);
     const int cap = value ? (int)value : kBrickDistCapDefault;
     if (cap != v->brick_cap) {
       v->brick_cap = cap;

@@ -110,6 +110,24 @@ int dmf_grid_save(const char* path, const dmf_grid_header* h, const int16_t* log
   std::string tmp = std::string(path) + ".XXXXXX";
   const int fd = mkstemp(&tmp[0]);
   if (fd < 0) return fail(DMF_ERR_INVALID, "cannot create a temporary file beside %s", path);
+  // mkstemp creates the file 0600; give it the mode a plain fopen would have (0666 less the
+  // umask), or the mode of the file it replaces
+  {
+    struct stat st;
+    mode_t mode;
+    if (stat(path, &st) == 0) {
+      mode = st.st_mode & 07777;
+    } else {
+      const mode_t um = umask(0);
+      umask(um);
+      mode = 0666 & ~um;
+    }
+    if (fchmod(fd, mode) != 0) {
+      close(fd);
+      unlink(tmp.c_str());
+      return fail(DMF_ERR_INVALID, "cannot set the mode of %s", tmp.c_str());
+    }
+  }
   File out;
   out.f = fdopen(fd, "wb");
   if (!out.f) {

@@ -232,8 +232,8 @@ int dmf_fuse_depth_device(dmf_volume* v, const dmf_camera* cam, const uint16_t* 
 /* Pre-allocate the fusion scratch for calls of up to P frames of `cam`'s size on this
  * volume, so that dmf_fuse_depth_device then neither allocates nor synchronises (e.g. for
  * hipGraph capture).  The brick pipeline fits its ray records, brick tables and (ray,
- * brick) pair records into max_scratch_bytes (0 = keep the current budget; default 55 % of
- * the device's memory, ~158 GB on MI355X): serial calls use one slot of the whole budget,
+ * brick) pair records into max_scratch_bytes (0 = keep the current budget; default 45 % of
+ * the device's memory, ~130 GB on MI355X): serial calls use one slot of the whole budget,
  * pipelined calls (dmf_fuse_set_input_stream) two staging slots of half each.  A call whose
  * pairs exceed a slot's pair capacity is cut into pose batches on the device
  * (dmf_fuse_plan).  A new budget frees and re-plans the slots.  Synchronises the stream.

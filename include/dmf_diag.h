@@ -38,7 +38,7 @@ enum dmf_knob {
   DMF_KNOB_PAIR_CAP = 2,    /* cap of the pair records a batch may hold (must hold any one frame's pairs) */
   DMF_KNOB_BATCH_POSES = 3, /* cap of the poses per device-cut pose batch */
   DMF_KNOB_PART_MAX = 4,    /* pairs per part of phase F's queue (1024..65535; default 65535) */
-  DMF_KNOB_SPAN = 5,        /* 8x8 packets per pass-A/B workgroup (4..4096) */
+  DMF_KNOB_SPAN = 5,        /* 8x8 packets per pass-A/B workgroup (4..1023) */
   DMF_KNOB_TAIL_SPLIT = 6,  /* phase F's queue tail split: -1 off, k > 0 = the last k x CUs parts quartered
                                (default: 2 for serial calls, off for pipelined ones) */
   DMF_KNOB_REVERSE_KERNEL = 7, /* reverseRayTraceFast march: 0 default (wave queues in spatial order + distance

@@ -13,8 +13,9 @@ are summed equals the oracle fusing all global poses (integer counters), so one 
 global pose set covers N = 1 and the N-GPU merge alike.  Digest = sha256 of the x-major
 int16 log-odds bytes, first 16 hex digits (bench.py logodds_digest).
 
-usage: python tests/golden/gen_fusion_digests.py [keys...]   (OpenMP oracle, all host cores;
-       config4 N = 1/2/4/8 take ~1-8 min each here)
+usage: python tests/golden/gen_fusion_digests.py [keys...]   (OpenMP oracle, all host cores or
+       DMF_GEN_THREADS; config4 N = 1/2/4/8 take ~1-8 min each here, config5_N8 (7.1e11 updates)
+       about two hours on 6 threads)
 """
 import hashlib
 import json
@@ -43,6 +44,9 @@ WORKLOADS = {
     "config2_N1": (256, 640, 480, 64),
     "config3_N1": (512, 1280, 720, 256),
     "config5_shard_N1": (1024, 1280, 720, 256),  # config 5's per-GPU shard size (256 of 2048 poses)
+    "config5_N8": (1024, 1280, 720, 2048),  # config 5's global set (8 GPUs x 256 poses)
+    # the one-GPU rehearsal of the 8-rank launch (bench.py --gpus 8 --grid 128 --poses-per-gpu 8)
+    "rehearsal_g128_N8": (128, 640, 480, 64),
 }
 
 
@@ -72,7 +76,7 @@ def oracle_digest(grid, W, H, P, threads):
 def main():
     keys = sys.argv[1:] or list(WORKLOADS)
     out = json.load(open(OUT)) if os.path.exists(OUT) else {}
-    threads = os.cpu_count() or 1
+    threads = int(os.environ.get("DMF_GEN_THREADS", "0")) or os.cpu_count() or 1
     for k in keys:
         t0 = time.time()
         out[k] = oracle_digest(*WORKLOADS[k], threads=threads)

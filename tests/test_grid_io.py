@@ -135,3 +135,25 @@ def test_concurrent_saves_never_tear(tmp_path):
     g, _, _ = _lib.grid_load(path)
     assert any(np.array_equal(g, x) for x in grids)
     assert sorted(p.name for p in tmp_path.iterdir()) == ["g.dmf"]
+
+
+def test_saved_file_mode(tmp_path):
+    """the mkstemp temporary (created 0600) gets the mode a plain fopen would give
+    (0666 less the umask) for a new file, and keeps the mode of a file it replaces."""
+    import os
+    import stat
+    g = _grid((4, 3, 2), 5)
+    old = os.umask(0o022)
+    try:
+        path = tmp_path / "new.dmf"
+        _lib.grid_save(path, g, g.shape, (0, 1, 0, 1, 0, 1))
+        assert stat.S_IMODE(os.stat(path).st_mode) == 0o644
+        os.umask(0o077)
+        path2 = tmp_path / "new2.dmf"
+        _lib.grid_save(path2, g, g.shape, (0, 1, 0, 1, 0, 1))
+        assert stat.S_IMODE(os.stat(path2).st_mode) == 0o600
+        os.chmod(path, 0o640)
+        _lib.grid_save(path, g, g.shape, (0, 1, 0, 1, 0, 1))
+        assert stat.S_IMODE(os.stat(path).st_mode) == 0o640
+    finally:
+        os.umask(old)

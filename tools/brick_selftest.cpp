@@ -13,7 +13,8 @@
 //      R fits the record's 7 bits;
 //   5. the same walk from the 20-byte record (pack20 -> unpack20, scaled state beta);
 //   6. pass B's select-based counts_at_sel equals counts_at at the ray's crossing events;
-//   7. so does the double-arithmetic counts_at_f64 (also with its reciprocals 2 ulps off);
+//   7. so does the double-arithmetic counts_at_f64 (also with its reciprocals 2 ulps and a
+//      relative 2^-22 / 2^-14 off);
 //   8. pass B's replay of pass A's recorded crossing path (path_put / path_axis, the first
 //      kPathSteps boundaries; coarse_total = the walk's step count) lists the same bricks,
 //      and so does its replay past them by the stateless coarse_next_at (also over whole rays).
@@ -295,19 +296,27 @@ int main(int argc, char** argv) {
           else counts_at_f64<2>(r, fd, k, c2);
           okc = c0[0] == c1[0] && c0[1] == c1[1] && c0[2] == c1[2] && c0[0] == c2[0] && c0[1] == c2[1] &&
                 c0[2] == c2[2];
-          // 7b. the same with the reciprocals 2 ulps off either way (the device's v_rcp_f64
-          //     need not be correctly rounded)
-          for (int dir = -1; dir <= 1 && okc; dir += 2) {
+          // 7b. the same with the reciprocals off either way, by 2 ulps and by a relative error
+          //     of 2^-22 (v_rcp_f64's documented precision is 2^29 ulps of a double, i.e. a
+          //     relative error near 2^-23) and of 2^-14 (the margin: the +-1 remainder step
+          //     holds while X / Y * eps < 1, X / Y < 2^12)
+          for (int pert = 0; pert < 6 && okc; ++pert) {
+            const int dir = pert & 1 ? 1 : -1;
             QRayF64 fp = fd;
-            for (int b = 0; b < 3; ++b)
-              if (fp.inv[b] != 0.0)
+            for (int b = 0; b < 3; ++b) {
+              if (fp.inv[b] == 0.0) continue;
+              if (pert < 2) {
                 for (int u = 0; u < 2; ++u) fp.inv[b] = std::nextafter(fp.inv[b], dir < 0 ? 0.0 : 1.0);
+              } else {
+                fp.inv[b] *= 1.0 + dir * std::ldexp(1.0, pert < 4 ? -22 : -14);
+              }
+            }
             int32_t c3[3];
             if (a == 0) counts_at_f64<0>(r, fp, k, c3);
             else if (a == 1) counts_at_f64<1>(r, fp, k, c3);
             else counts_at_f64<2>(r, fp, k, c3);
             okc = c0[0] == c3[0] && c0[1] == c3[1] && c0[2] == c3[2];
-            if (!okc) printf("ray %ld: counts_at_f64 with inv %+d ulps (%d, %d) differs\n", i, 2 * dir, a, k);
+            if (!okc) printf("ray %ld: counts_at_f64 with perturbed inv (%d) (%d, %d) differs\n", i, pert, a, k);
           }
           if (!okc) printf("ray %ld: counts_at_sel / _f64(%d, %d) = %d %d %d / %d %d %d vs %d %d %d\n", i, a, k, c1[0],
                            c1[1], c1[2], c2[0], c2[1], c2[2], c0[0], c0[1], c0[2]);
