@@ -491,6 +491,87 @@ __host__ __device__ inline uint32_t slab_rcode(int M, int32_t sb1, int32_t sb2, 
   return S == 0 ? steps : 3u * (uint32_t)S + s;
 }
 
+// Slab code of a pair (round 6: the record's 8-bit walk field, phase F's walk bound):
+//   code = S | s << 5 | e << 7
+// S = slabs the walk takes whole (the M-crossings between the pair's first cell and its last
+// cell L, <= 31 inside a 32-cell brick), s = cells of L's slab before L (0..2), and e = the
+// minor whose crossing entered L when s >= 1 (0: m1, 1: m2).  Phase F walks S whole slabs
+// with ONE ownership test per slab (every cell of slab k < S lies before L) and adds L's slab
+// at adoption from L itself: L - d_e (s >= 1) and L - d_1 - d_2 (s = 2, the slab's first
+// cell) -- instead of three per-cell thresholds in every slab (R = 3 S + s, slab_rcode).
+// e for s = 2: the later of the two minor crossings of L's slab; m1's (L1-th) and m2's
+// (L2-th) crossings are the next crossings at counts (L1 - 1, L2 - 1), where b_12 >= 0 says
+// m2's comes first (ties to m1): then m1 entered L (e = 0), else m2 (e = 1).  That b_12 is
+// a state the walk passes through (its start of L's slab), so the wrapped int32 sum is exact.
+__host__ __device__ inline uint32_t slab_code(int M, int32_t sb1, int32_t sb2, int32_t sb12, uint32_t KM, uint32_t K1,
+                                              uint32_t K2, const int32_t cin[3], const int32_t cL[3]) {
+  const int m1 = M == 0 ? 1 : 0, m2 = M == 2 ? 1 : 2;
+  const int32_t LM = pick3(cL[0], cL[1], cL[2], M), L1 = pick3(cL[0], cL[1], cL[2], m1),
+                L2 = pick3(cL[0], cL[1], cL[2], m2);
+  const int32_t S = LM - pick3(cin[0], cin[1], cin[2], M);
+  const uint32_t k2 = (uint32_t)(2 * kQ);
+  const int32_t aM = (int32_t)(KM / k2), a1 = (int32_t)(K1 / k2), a2 = (int32_t)(K2 / k2);
+  uint32_t sc, e;
+  if (S == 0) {  // L in the pair's first slab: every minor crossing since the entry is in it
+    const int32_t n1 = L1 - pick3(cin[0], cin[1], cin[2], m1), n2 = L2 - pick3(cin[0], cin[1], cin[2], m2);
+    sc = (uint32_t)(n1 + n2);
+    e = n1 ? 0u : 1u;
+  } else {  // as slab_rcode: minor m crossed in L's slab iff b_m < 0 at (cL_M - 1, cL_m - 1)
+    const int32_t e1 = (int32_t)((uint32_t)sb1 + ((uint32_t)mul24(LM - 1, a1) - (uint32_t)mul24(L1 - 1, aM)) * k2);
+    const int32_t e2 = (int32_t)((uint32_t)sb2 + ((uint32_t)mul24(LM - 1, a2) - (uint32_t)mul24(L2 - 1, aM)) * k2);
+    const uint32_t t1 = L1 >= 1 && e1 < 0 ? 1u : 0u, t2 = L2 >= 1 && e2 < 0 ? 1u : 0u;
+    sc = t1 + t2;
+    e = t1 ? 0u : 1u;
+  }
+  if (sc == 2) {
+    const int32_t e12 = (int32_t)((uint32_t)sb12 + ((uint32_t)mul24(L1 - 1, a2) - (uint32_t)mul24(L2 - 1, a1)) * k2);
+    e = e12 >= 0 ? 0u : 1u;
+  }
+  if (sc == 0) e = 0;
+  return (uint32_t)S | sc << 5 | e << 7;
+}
+
+// Phase F's walk from a slab code (CPU self-test): S whole slabs, then the cells of L's slab
+// before L, derived from L (coordinates Lc) as phase F does at adoption: L - st_1 - st_2 when
+// s = 2 (its first cell), then L - st_e (s >= 1).  emit(x, y, z) per cell, in walk order.
+template <class F>
+__host__ __device__ inline void slab_walk_code(int M, int32_t b1, int32_t b2, int32_t b12, uint32_t KM, uint32_t K1,
+                                               uint32_t K2, const int32_t st[3], const int32_t p0[3], uint32_t code,
+                                               const int32_t Lc[3], F&& emit) {
+  const int m1 = M == 0 ? 1 : 0, m2 = M == 2 ? 1 : 2;
+  const int S = (int)(code & 31u), sc = (int)((code >> 5) & 3u), e = (int)(code >> 7);
+  int32_t p[3] = {p0[0], p0[1], p0[2]};
+  for (int k = 0; k < S; ++k) {
+    const bool c1 = b1 >= 0, c2 = b2 >= 0, o = b12 >= 0;
+    emit(p[0], p[1], p[2]);
+    if (c1 || c2) {
+      const int f = o ? m2 : m1, s2 = o ? m1 : m2;
+      p[f] += st[f];
+      emit(p[0], p[1], p[2]);
+      if (c1 && c2) {
+        p[s2] += st[s2];
+        emit(p[0], p[1], p[2]);
+      }
+    }
+    p[M] += st[M];
+    b1 = (int32_t)((uint32_t)b1 + K1 - (c1 ? KM : 0u));
+    b2 = (int32_t)((uint32_t)b2 + K2 - (c2 ? KM : 0u));
+    b12 = (int32_t)((uint32_t)b12 + (c1 ? K2 : 0u) - (c2 ? K1 : 0u));
+  }
+  const int ea = e ? m2 : m1;
+  if (sc == 2) {
+    int32_t q[3] = {Lc[0], Lc[1], Lc[2]};
+    q[m1] -= st[m1];
+    q[m2] -= st[m2];
+    emit(q[0], q[1], q[2]);
+  }
+  if (sc >= 1) {
+    int32_t q[3] = {Lc[0], Lc[1], Lc[2]};
+    q[ea] -= st[ea];
+    emit(q[0], q[1], q[2]);
+  }
+}
+
 // Phase F's walk bounded by a slab ownership code R (CPU self-test): slab by slab, cell j
 // of slab k is emitted iff R - 3k > j; stops when R - 3k <= 0.
 template <class F>
@@ -530,12 +611,13 @@ __host__ __device__ inline void slab_walk_owned(int M, int32_t b1, int32_t b2, i
 // |b| < (2Q + 1) max|dq| gives |beta| < 2^18 + 2^9 for grids <= 1024 cells per axis
 // (|dq| < 2^18), a 20-bit two's-complement field; the +-never constant of a non-moving
 // axis (only its sign is ever used) is stored as +-(2^19 - 1).
-//   w0 = beta1 | aM[0:12) << 20          w1 = beta2 | aM[12:18) << 20 | R[0:6) << 26
+//   w0 = beta1 | aM[0:12) << 20          w1 = beta2 | aM[12:18) << 20 | code[0:6) << 26
 //   w2 = beta12 | a1[0:12) << 20         w3 = entry word | last word << 16
-//   w4 = a2 | a1[12:18) << 18 | R[6] << 24 | step signs (x, y, z) << 25 | M << 28 | ends << 30
-// (a = |dq| of the major / minor axes, R = the ownership code of slab_rcode, entry / last =
-// word offsets of the pair's first / last cell in phase F's LDS box).  w[4] >> 24 is the
-// 7-bit stride-table index of phase F.
+//   w4 = a2 | a1[12:18) << 18 | code[6] << 24 | step signs (x, y, z) << 25 | M << 28 | ends << 30
+//        | code[7] << 31
+// (a = |dq| of the major / minor axes, code = the slab code of slab_code (S | s << 5 | e << 7),
+// entry / last = word offsets of the pair's first / last cell in phase F's LDS box).
+// (w[4] >> 24) & 127 is the 7-bit stride-table index of phase F (its bit 0, code[6], unused).
 __host__ __device__ inline uint32_t beta20(int32_t b) {
   const int32_t lim = (1 << 19) - 1;
   const int32_t s = b >> 9;  // arithmetic shift: floor(b / 512)
@@ -543,19 +625,21 @@ __host__ __device__ inline uint32_t beta20(int32_t b) {
 }
 
 __host__ __device__ inline void pack20(int32_t b1, int32_t b2, int32_t b12, uint32_t aM, uint32_t a1, uint32_t a2,
-                                       uint32_t entry, uint32_t last, uint32_t R, uint32_t signs, uint32_t M,
+                                       uint32_t entry, uint32_t last, uint32_t code, uint32_t signs, uint32_t M,
                                        bool ends, uint32_t w[5]) {
   w[0] = beta20(b1) | (aM & 0xfffu) << 20;
-  w[1] = beta20(b2) | ((aM >> 12) & 0x3fu) << 20 | (R & 0x3fu) << 26;
+  w[1] = beta20(b2) | ((aM >> 12) & 0x3fu) << 20 | (code & 0x3fu) << 26;
   w[2] = beta20(b12) | (a1 & 0xfffu) << 20;
   w[3] = entry | last << 16;
-  w[4] = a2 | ((a1 >> 12) & 0x3fu) << 18 | ((R >> 6) & 1u) << 24 | signs << 25 | M << 28 | (ends ? 1u << 30 : 0u);
+  w[4] = a2 | ((a1 >> 12) & 0x3fu) << 18 | ((code >> 6) & 1u) << 24 | signs << 25 | M << 28 | (ends ? 1u << 30 : 0u) |
+         ((code >> 7) & 1u) << 31;
 }
 
 struct Slab20 {
   int32_t b1, b2, b12;  // beta state
   uint32_t aM, a1, a2;  // |dq| of the major / minor axes (the beta walk's K)
-  uint32_t entry, last, R, signs, M;
+  uint32_t entry, last, code, signs, M;
+  uint32_t S, s, e;     // the code's fields (slab_code)
   bool ends;
 };
 
@@ -570,7 +654,10 @@ __host__ __device__ inline void unpack20(const uint32_t w[5], Slab20& s) {
   s.a2 = w[4] & 0x3ffffu;
   s.entry = w[3] & 0xffffu;
   s.last = w[3] >> 16;
-  s.R = (w[1] >> 26) | ((w[4] >> 24) & 1u) << 6;
+  s.code = (w[1] >> 26) | ((w[4] >> 24) & 1u) << 6 | (w[4] >> 31) << 7;
+  s.S = s.code & 31u;
+  s.s = (s.code >> 5) & 3u;
+  s.e = s.code >> 7;
   s.signs = (w[4] >> 25) & 7u;
   s.M = (w[4] >> 28) & 3u;
   s.ends = ((w[4] >> 30) & 1u) != 0;

@@ -1331,12 +1331,13 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
     uint4 cur = entry(c00);
     int32_t idx = 0;                    // crossings before the current pair's first cell
     int32_t ci0 = 0, ci1 = 0, ci2 = 0;  // SLAB: their counts per axis
-    // count field: SLAB = the slab ownership code of dmf_brick.hpp slab_rcode (F's walk
-    // bound), else the pair's cells - 1; cL = crossing counts at the pair's last cell
+    // count field: SLAB = the slab code of dmf_brick.hpp slab_code (S | s << 5 | e << 7: F's
+    // walk bound and its adoption of L's slab), else the pair's cells - 1; cL = crossing counts
+    // at the pair's last cell
     auto count_field = [&](int32_t L0, int32_t L1, int32_t L2) -> uint32_t {
       if (!SLAB) return (uint32_t)(L0 + L1 + L2 - idx);
       const int32_t cin[3] = {ci0, ci1, ci2}, cL[3] = {L0, L1, L2};
-      return bk::slab_rcode(M, sb1, sb2, KM, Km1, Km2, cin, cL);
+      return bk::slab_code(M, sb1, sb2, sb12, KM, Km1, Km2, cin, cL);
     };
     // crossing counts per axis at the boundary event of axis a into brick coordinate (bx, by, bz)
     // the boundary counts in double arithmetic (dmf_brick.hpp counts_at_f64, exact by fma;
@@ -1574,10 +1575,12 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
 // cells between two major-axis crossings, 1 + c1 + c2 of them, with one compare per minor
 // axis instead of a three-way DDA selection per cell, on the 20-byte record's scaled state
 // beta = b >> 9 with increments |dq| (exactly the decisions of b with K = 512 |dq|).  The
-// three LDS adds of a slab are predicated on the pair's slab ownership code r (cell j of the
-// k-th slab from here is owned iff r - 3k > j); the state keeps moving harmlessly past the
-// pair's end (unsigned arithmetic; refilled or ignored).  The pair's last cell is added at
-// adoption (hit or miss).  A wave refills when >= REFILL of its lanes are idle, from
+// pair's slab code (dmf_brick.hpp slab_code) bounds the walk: the S slabs before the last
+// cell L's are taken whole, their LDS adds predicated on ONE test per slab (r > k); the
+// state keeps moving harmlessly past them (unsigned arithmetic; refilled or ignored).  L and
+// the s cells of L's slab before it are added at adoption, from L: L - d_e (s >= 1) and
+// L - d_1 - d_2 (s = 2).  (Round 5 and before: the code R = 3 S + s and three thresholds per
+// slab, r - 3k > j for cell j.)  A wave refills when >= REFILL of its lanes are idle, from
 // per-lane records prefetched one refill ahead through buffer resources over the part.
 // Parts are taken from k_bk_scan's largest-first order (entries (brick, part index); bit 31
 // of the index marks a quarter of a part from the scan's tail split).
@@ -1675,13 +1678,17 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       K2mM = sd.a2 - sd.aM;
       nK1 = 0u - sd.a1;
       cur = sd.entry * 4u;
-      r = (int)sd.R;
+      r = (int)sd.S;
       const uint4 st3 = slut[cw >> 24 & 127u];
       dM = st3.x;
       d1 = st3.y;
       d2 = st3.z;
       // the pair's last cell: a hit when the ray ends there inside the grid, else a miss
-      atomicAdd(&box[sd.last], sd.ends ? 0x10000u : 1u);
+      const uint32_t Lb = sd.last * 4u;
+      atomicAdd((uint32_t*)(lds + Lb), sd.ends ? 0x10000u : 1u);
+      // the cells of L's slab before L (misses): L - d_e, and the slab's first cell L - d_1 - d_2
+      if (sd.s != 0) atomicAdd((uint32_t*)(lds + Lb - (sd.e ? d2 : d1)), 1u);
+      if (sd.s == 2) atomicAdd((uint32_t*)(lds + Lb - d1 - d2), 1u);
     };
     bool more = true;
     // lanes in `need` take the next pair indices (one LDS counter atomic) and load their records
@@ -1736,25 +1743,26 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       if (l == 0) ++nblocks;
       nlanes += (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(r > 0));
 #endif
-      // cell j of the k-th slab from here is owned iff r - 3k > j: inside the block the
-      // thresholds move (3u + j) and r drops by 3 UNROLL once at its end
+      // the k-th slab from here is walked iff r > k: inside the block the threshold moves
+      // (u) and r drops by UNROLL once at its end
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-        const int t = 3 * u;
         const bool c1 = (int32_t)b1 >= 0, c2 = (int32_t)b2 >= 0, o2 = (int32_t)b12 >= 0;
         const uint32_t x1 = c1 ? d1 : 0u, x2 = c2 ? d2 : 0u;
         // the slab's cells: cur, then p1 if a minor crosses (on m2 iff o2, also when only
         // one does: dmf_brick.hpp slab_walk_owned), then p2 if both do
         const uint32_t p1 = cur + (o2 ? x2 : x1), p2 = cur + x1 + x2;
-        if (r > t) atomicAdd((uint32_t*)(lds + cur), 1u);
-        if ((c1 || c2) && r > t + 1) atomicAdd((uint32_t*)(lds + p1), 1u);
-        if (c1 && c2 && r > t + 2) atomicAdd((uint32_t*)(lds + p2), 1u);
+        if (r > u) {
+          atomicAdd((uint32_t*)(lds + cur), 1u);
+          if (c1 || c2) atomicAdd((uint32_t*)(lds + p1), 1u);
+          if (c1 && c2) atomicAdd((uint32_t*)(lds + p2), 1u);
+        }
         cur = p2 + dM;
         b1 += c1 ? K1mM : K1;
         b2 += c2 ? K2mM : K2;
         b12 += (c1 ? K2 : 0u) + (c2 ? nK1 : 0u);
       }
-      r -= 3 * UNROLL;
+      r -= UNROLL;
       DMF_TACC(t_walk, tw0);
     }
     DMF_T(tf0);

@@ -8,10 +8,11 @@
 //      the fine walk visits there;
 //   3. phase F's major-axis slab walk (slab_walk) restarted from the same counts visits
 //      the same cells in the same order;
-//   4. the slab walk bounded by the pair's ownership code (slab_rcode: R = 3 S + s, the
-//      record's count field) visits exactly the pair's cells before its last cell, and
-//      R fits the record's 7 bits;
-//   5. the same walk from the 20-byte record (pack20 -> unpack20, scaled state beta);
+//   4. the slab walk bounded by the pair's ownership code (slab_rcode: R = 3 S + s) visits
+//      exactly the pair's cells before its last cell, and R fits 7 bits; so does phase F's
+//      walk from the slab code (slab_code: S whole slabs, then L's slab before L derived from
+//      L, slab_walk_code), with S <= 31;
+//   5. the slab-code walk from the 20-byte record (pack20 -> unpack20, scaled state beta);
 //   6. pass B's select-based counts_at_sel equals counts_at at the ray's crossing events;
 //   7. so does the double-arithmetic counts_at_f64 (also with its reciprocals 2 ulps and a
 //      relative 2^-22 / 2^-14 off);
@@ -106,14 +107,15 @@ static void restart_slab(const QRay& r, const int32_t c[3], int cells, std::vect
   slab_walk(M, b1, b2, b12, K[M], K[m1], K[m2], r.st, p0, cells, [&](int x, int y, int z) { out.push_back({x, y, z}); });
 }
 
-// Check 4: slab_walk_owned from the pair's entry counts, bounded by slab_rcode.
+// Check 4: slab_walk_owned from the pair's entry counts, bounded by slab_rcode; or (code) the
+// slab-code walk of phase F (slab_code, slab_walk_code from the last cell's coordinates Lc).
 static void restart_owned(const QRay& r, const int32_t c[3], const int32_t cL[3], uint32_t& R,
-                          std::vector<Cell>& out) {
+                          std::vector<Cell>& out, const int32_t* Lc = nullptr) {
   const uint32_t K[3] = {(uint32_t)(2 * kQ * r.adq[0]), (uint32_t)(2 * kQ * r.adq[1]), (uint32_t)(2 * kQ * r.adq[2])};
   const int M = major_axis(r), m1 = M == 0 ? 1 : 0, m2 = M == 2 ? 1 : 2;
   int32_t s1, s2, s12;  // slab state at the ray's start (counts 0), as pass B keeps it
   slab_from_pairwise(M, e0_pair(r, 0, 1), e0_pair(r, 0, 2), e0_pair(r, 1, 2), s1, s2, s12);
-  R = slab_rcode(M, s1, s2, K[M], K[m1], K[m2], c, cL);
+  R = Lc ? slab_code(M, s1, s2, s12, K[M], K[m1], K[m2], c, cL) : slab_rcode(M, s1, s2, K[M], K[m1], K[m2], c, cL);
   const int32_t E01 = (int32_t)((uint32_t)e0_pair(r, 0, 1) + (uint32_t)c[0] * K[1] - (uint32_t)c[1] * K[0]);
   const int32_t E02 = (int32_t)((uint32_t)e0_pair(r, 0, 2) + (uint32_t)c[0] * K[2] - (uint32_t)c[2] * K[0]);
   const int32_t E12 = (int32_t)((uint32_t)e0_pair(r, 1, 2) + (uint32_t)c[1] * K[2] - (uint32_t)c[2] * K[1]);
@@ -121,19 +123,23 @@ static void restart_owned(const QRay& r, const int32_t c[3], const int32_t cL[3]
   slab_from_pairwise(M, E01, E02, E12, b1, b2, b12);
   const int32_t p0[3] = {r.cs[0] + r.st[0] * c[0], r.cs[1] + r.st[1] * c[1], r.cs[2] + r.st[2] * c[2]};
   out.clear();
-  slab_walk_owned(M, b1, b2, b12, K[M], K[m1], K[m2], r.st, p0, (int)R,
-                  [&](int x, int y, int z) { out.push_back({x, y, z}); });
+  if (Lc)
+    slab_walk_code(M, b1, b2, b12, K[M], K[m1], K[m2], r.st, p0, R, Lc,
+                   [&](int x, int y, int z) { out.push_back({x, y, z}); });
+  else
+    slab_walk_owned(M, b1, b2, b12, K[M], K[m1], K[m2], r.st, p0, (int)R,
+                    [&](int x, int y, int z) { out.push_back({x, y, z}); });
 }
 
 // Check 5: the same walk from the 20-byte pair record (pack20 / unpack20): scaled state
 // beta = b >> 9 with increments |dq| instead of K = 512 |dq|.
-static void restart_owned20(const QRay& r, const int32_t c[3], const int32_t cL[3], bool ends,
+static void restart_owned20(const QRay& r, const int32_t c[3], const int32_t cL[3], const int32_t Lc[3], bool ends,
                             std::vector<Cell>& out) {
   const uint32_t K[3] = {(uint32_t)(2 * kQ * r.adq[0]), (uint32_t)(2 * kQ * r.adq[1]), (uint32_t)(2 * kQ * r.adq[2])};
   const int M = major_axis(r), m1 = M == 0 ? 1 : 0, m2 = M == 2 ? 1 : 2;
   int32_t s1, s2, s12;
   slab_from_pairwise(M, e0_pair(r, 0, 1), e0_pair(r, 0, 2), e0_pair(r, 1, 2), s1, s2, s12);
-  const uint32_t R = slab_rcode(M, s1, s2, K[M], K[m1], K[m2], c, cL);
+  const uint32_t R = slab_code(M, s1, s2, s12, K[M], K[m1], K[m2], c, cL);
   int32_t b1, b2, b12;
   slab_from_pairwise(M, (int32_t)((uint32_t)e0_pair(r, 0, 1) + (uint32_t)c[0] * K[1] - (uint32_t)c[1] * K[0]),
                      (int32_t)((uint32_t)e0_pair(r, 0, 2) + (uint32_t)c[0] * K[2] - (uint32_t)c[2] * K[0]),
@@ -146,7 +152,8 @@ static void restart_owned20(const QRay& r, const int32_t c[3], const int32_t cL[
   Slab20 s;
   unpack20(w, s);
   out.clear();
-  if (s.aM != (uint32_t)r.adq[M] || s.a1 != (uint32_t)r.adq[m1] || s.a2 != (uint32_t)r.adq[m2] || s.R != R ||
+  if (s.aM != (uint32_t)r.adq[M] || s.a1 != (uint32_t)r.adq[m1] || s.a2 != (uint32_t)r.adq[m2] || s.code != R ||
+      s.S != (R & 31u) || s.s != ((R >> 5) & 3u) || s.e != (R >> 7) ||
       s.signs != signs || s.M != (uint32_t)M || s.ends != ends || s.entry != 12345u || s.last != 54321u) {
     out.push_back({-1, -1, -1});  // a field did not round-trip
     return;
@@ -155,8 +162,8 @@ static void restart_owned20(const QRay& r, const int32_t c[3], const int32_t cL[
   const int32_t p0[3] = {r.cs[0] + r.st[0] * c[0], r.cs[1] + r.st[1] * c[1], r.cs[2] + r.st[2] * c[2]};
   // a non-moving axis has sign bit 0 (+1) but never steps (its b stays negative / b12 never flips it)
   const int32_t stw[3] = {r.st[0] ? st[0] : 0, r.st[1] ? st[1] : 0, r.st[2] ? st[2] : 0};
-  slab_walk_owned((int)s.M, s.b1, s.b2, s.b12, s.aM, s.a1, s.a2, stw, p0, (int)s.R,
-                  [&](int x, int y, int z) { out.push_back({x, y, z}); });
+  slab_walk_code((int)s.M, s.b1, s.b2, s.b12, s.aM, s.a1, s.a2, stw, p0, s.code, Lc,
+                 [&](int x, int y, int z) { out.push_back({x, y, z}); });
 }
 
 int main(int argc, char** argv) {
@@ -347,8 +354,19 @@ int main(int argc, char** argv) {
         ok = R < 128 && seg.size() == len - 1;
         for (size_t k = 0; ok && k + 1 < len; ++k) ok = seg[k] == fine[pos + k];
         if (!ok) printf("ownership code %u: %zu cells vs %zu\n", R, seg.size(), len - 1);
+        const int32_t Lxyz[3] = {Lc.x, Lc.y, Lc.z};
+        if (ok) {  // 4b. phase F's slab-code walk
+          uint32_t code = 0;
+          restart_owned(r, p.cin, cL, code, seg, Lxyz);
+          const int Mx = major_axis(r);
+          const int32_t Sx = pick3(cL[0], cL[1], cL[2], Mx) - pick3(p.cin[0], p.cin[1], p.cin[2], Mx);
+          ok = code < 256 && Sx >= 0 && Sx <= 31 && (code & 31u) == (uint32_t)Sx && ((code >> 5) & 3u) <= 2u &&
+               seg.size() == len - 1;
+          for (size_t k = 0; ok && k + 1 < len; ++k) ok = seg[k] == fine[pos + k];
+          if (!ok) printf("slab code %u: %zu cells vs %zu\n", code, seg.size(), len - 1);
+        }
         if (ok) {  // 5. the same from the 20-byte record (beta state)
-          restart_owned20(r, p.cin, cL, p.ends && end_inside, seg);
+          restart_owned20(r, p.cin, cL, Lxyz, p.ends && end_inside, seg);
           ok = seg.size() == len - 1;
           for (size_t k = 0; ok && k + 1 < len; ++k) ok = seg[k] == fine[pos + k];
           if (!ok) printf("20-byte record walk: %zu cells vs %zu\n", seg.size(), len - 1);
