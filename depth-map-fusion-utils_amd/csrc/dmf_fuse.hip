@@ -1413,7 +1413,8 @@ template <int S_ORDER>
 __device__ inline uint32_t bk_order(uint32_t k, uint32_t n) {
   if (S_ORDER <= 1) return k;
   const uint32_t per = n / S_ORDER, n1 = per * S_ORDER;
-  return k < n1 ? (k % S_ORDER) * per + k / S_ORDER : k;
+  // (24-bit multiply: per < 2^16 for parts of <= 65535 pairs; a 32-bit one became v_mad_u64_u32)
+  return k < n1 ? (uint32_t)bk::mul24((int32_t)(k % S_ORDER), (int32_t)per) + k / S_ORDER : k;
 }
 
 // Phase F, per-cell walk (variant DMF_FUSE_CELL_WALK = 40: an independent exact walk kept for
@@ -1511,7 +1512,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
     for (;;) {
       const uint64_t act = __builtin_amdgcn_ballot_w64(cur != cend);
       bool any_act = act != 0;
-      if (__builtin_popcountll(act) <= 64 - REFILL) {
+      if ((int)__builtin_popcountll(act) <= 64 - REFILL) {
         const uint64_t take = __builtin_amdgcn_ballot_w64(cur == cend && fok);
         if (take) {
           if (cur == cend && fok) {
@@ -1712,7 +1713,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       const uint64_t act = __builtin_amdgcn_ballot_w64(r > 0);
       bool any_act = act != 0;
       DMF_T(tr0);
-      if (__builtin_popcountll(act) <= 64 - REFILL) {
+      if ((int)__builtin_popcountll(act) <= 64 - REFILL) {
         const uint64_t take = __builtin_amdgcn_ballot_w64(r <= 0 && fok);
         if (take) {
 #if defined(DMF_EXP_STATS)
@@ -1931,7 +1932,11 @@ static bool use_bricks(const dmf_volume* v, const Geom& g) {
 // 1 % faster than 4 at 512^3 and at config 2, the others slower); with 8-slab blocks a wave
 // refills at >= 16 idle lanes (sweep 16/20/24/32, picks over 16/32/64 regions: serial -1 %,
 // config 2 -0.5 %, pipelined within the box's drift)
+#if defined(DMF_EXP_F_UNROLL)  // experiment builds: slabs per walk block
+constexpr int kBkUnroll = DMF_EXP_F_UNROLL;
+#else
 constexpr int kBkUnroll = 8;
+#endif
 #if defined(DMF_EXP_F_REFILL)  // experiment builds: refill threshold / pick spread of phase F
 constexpr int kBkRefill = DMF_EXP_F_REFILL, kBkSpread = DMF_EXP_F_SPREAD;
 #else

@@ -14,7 +14,8 @@ REBUILD=${REBUILD:-dmf_fuse}
 OBJS=""
 for f in dmf_core dmf_trace dmf_fuse dmf_ogrid dmf_comm dmf_io; do
   if [[ " $REBUILD " == *" $f "* ]] || [ -n "$ALL" ]; then
-    /opt/rocm/bin/hipcc $FLAGS "$@" -c csrc/$f.hip -o "$OUT/$f.o" &
+    EXTRA=""; [ $f = dmf_fuse ] && EXTRA="-mllvm -amdgpu-atomic-optimizer-strategy=None"  # as the Makefile
+    /opt/rocm/bin/hipcc $FLAGS $EXTRA "$@" -c csrc/$f.hip -o "$OUT/$f.o" &
     OBJS="$OBJS $OUT/$f.o"
   else
     OBJS="$OBJS build/$f.o"
