@@ -1600,9 +1600,12 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
                                                           const uint2* __restrict__ order, uint32_t part_max,
                                                           unsigned long long* __restrict__ ctl,
                                                           int32_t* __restrict__ hits, int32_t* __restrict__ misses,
-                                                          unsigned long long* __restrict__ stats) {
+                                                          unsigned long long* __restrict__ stats,
+                                                          const ulonglong2* __restrict__ xrays, uint32_t xnrays,
+                                                          uint32_t xnpairs) {
   __shared__ uint32_t box[kBkBoxWords + 4];  // counters (skewed), control words
   uint32_t* sh = box + kBkBoxWords;
+  // (xrays / xnrays / xnpairs: used only by the DMF_EXP_F_REBUILD experiment build below)
   // (dM, d1, d2) LDS byte strides of a pair, looked up by its record bits w4 >> 24 (bits 1-3
   // step signs, 4-5 the major axis): one ds_read instead of ~17 selects per refill (F -1.3 %);
   // written before the first part's barrier
@@ -1618,6 +1621,10 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
   // pass B's layout check failed for this batch (dmf_fuse_status reports it): its pair
   // records are not all in place, so none is walked
   if (ctl[3] != 0) return;
+#if defined(DMF_EXP_F_REBUILD)
+  xnpairs = (uint32_t)ctl[0];  // the batch's pairs (the stand-in ray ids spread over them)
+  uint32_t sink = 0;           // the proxy's result
+#endif
   for (int i = tid; i < kBkBoxWords; i += blockDim.x) box[i] = 0;
   const uint32_t nparts = (uint32_t)ctl[1];
   const Tiles tl = tiles_of(g.n);
@@ -1666,6 +1673,9 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     uint4 ca = make_uint4(0, 0, 0, 0);
     uint32_t cw = 0;
     bool fok = false;
+#if defined(DMF_EXP_F_REBUILD)
+    uint32_t kid = 0;  // the prefetched pair's index in the batch
+#endif
     auto decode = [&]() {
       const uint32_t w[5] = {ca.x, ca.y, ca.z, ca.w, cw};
       bk::Slab20 sd;
@@ -1690,36 +1700,83 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       // the cells of L's slab before L (misses): L - d_e, and the slab's first cell L - d_1 - d_2
       if (sd.s != 0) atomicAdd((uint32_t*)(lds + Lb - (sd.e ? d2 : d1)), 1u);
       if (sd.s == 2) atomicAdd((uint32_t*)(lds + Lb - d1 - d2), 1u);
+#if defined(DMF_EXP_F_REBUILD)
+      {
+        // Cost proxy of a compact pair record (B stores <= 8 B, F rebuilds the
+        // slab state): per adopted pair, pass B's per-pair arithmetic on a ray record -- its
+        // 16-B load (a stand-in ray, monotone in the pair index as B's slot order is), the
+        // decode, the f64 reciprocals, the boundary counts at entry and at exit, the entry
+        // state and the slab code.  The records stay the product's (exact results); the
+        // proxy's values only feed a test that is never true.
+        const uint32_t rid = (uint32_t)(((uint64_t)kid * xnrays) / (xnpairs ? xnpairs : 1u));
+        const ulonglong2 rr = xrays[rid];
+        bk::QRay R;
+        bk::decode_ray(rr.x, rr.y, R);
+        bk::QRayF64 F64;
+        bk::qray_f64(R, F64);
+        const int Mx = bk::major_axis(R), m1x = Mx == 0 ? 1 : 0, m2x = Mx == 2 ? 1 : 2;
+        int32_t c0[3], c1[3];
+        const int32_t ka = (int32_t)(kid & 15u), kb = ka + 1;
+        if (Mx == 0) bk::counts_at_f64<0>(R, F64, min(ka, max(R.n[0] - 1, 0)), c0);
+        else if (Mx == 1) bk::counts_at_f64<1>(R, F64, min(ka, max(R.n[1] - 1, 0)), c0);
+        else bk::counts_at_f64<2>(R, F64, min(ka, max(R.n[2] - 1, 0)), c0);
+        if (m1x == 0) bk::counts_at_f64<0>(R, F64, min(kb, max(R.n[0] - 1, 0)), c1);
+        else bk::counts_at_f64<1>(R, F64, min(kb, max(R.n[1] - 1, 0)), c1);
+        const int32_t aMx = bk::pick3(R.adq[0], R.adq[1], R.adq[2], Mx), a1x = bk::pick3(R.adq[0], R.adq[1], R.adq[2], m1x),
+                      a2x = bk::pick3(R.adq[0], R.adq[1], R.adq[2], m2x);
+        const uint32_t KMx = 512u * (uint32_t)aMx, K1x = 512u * (uint32_t)a1x, K2x = 512u * (uint32_t)a2x;
+        int32_t sb1, sb2, sb12;
+        bk::slab_from_pairwise(Mx, bk::e0_pair(R, 0, 1), bk::e0_pair(R, 0, 2), bk::e0_pair(R, 1, 2), sb1, sb2, sb12);
+        const uint32_t eb1 = (uint32_t)sb1 + ((uint32_t)bk::mul24(bk::pick3(c0[0], c0[1], c0[2], Mx), a1x) -
+                                              (uint32_t)bk::mul24(bk::pick3(c0[0], c0[1], c0[2], m1x), aMx)) * 512u;
+        const uint32_t code = bk::slab_code(Mx, sb1, sb2, sb12, KMx, K1x, K2x, c0, c1);
+        const uint32_t xw = (uint32_t)(R.cs[0] + bk::mul24(R.st[0], c0[0])) & 31u,
+                       yw = (uint32_t)(R.cs[1] + bk::mul24(R.st[1], c0[1])) & 31u,
+                       zw = (uint32_t)(R.cs[2] + bk::mul24(R.st[2], c0[2])) & 31u;
+        sink ^= code ^ eb1 ^ bk_lds_word(xw, yw, zw);
+      }
+#endif
     };
     bool more = true;
-    // lanes in `need` take the next pair indices (one LDS counter atomic) and load their records
-    auto prefetch = [&](uint64_t need) {
-      const uint32_t nn = (uint32_t)__builtin_popcountll(need);
+    // lanes in `need` take the next pair indices (one LDS counter atomic, issued by alloc()
+    // before the refill's decode so that its return latency hides behind it) and load their
+    // records (fetch())
+    auto alloc = [&](uint64_t need) -> uint32_t {
       uint32_t base0 = 0;
-      if (l == 0) base0 = atomicAdd(&sh[1], nn);
+      if (l == 0) base0 = atomicAdd(&sh[1], (uint32_t)__builtin_popcountll(need));
+      return base0;
+    };
+    auto fetch = [&](uint64_t need, uint32_t base0) {
+      const uint32_t nn = (uint32_t)__builtin_popcountll(need);
       const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
       if (base + nn >= n) more = false;
       if ((need >> l) & 1ull) {
         const uint32_t k = base + (uint32_t)lane_prefix(need);
         fok = k < n;
         const uint32_t ob = bk_order<S_ORDER>(k, n);
+#if defined(DMF_EXP_F_REBUILD)
+        kid = p0 + ob;
+#endif
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_a, ob * 16u, 0, 0);
         ca = make_uint4(v[0], v[1], v[2], v[3]);
         cw = __builtin_amdgcn_raw_buffer_load_b32(rs_w, ob * 4u, 0, 0);
       }
     };
-    prefetch(~0ull);
+    fetch(~0ull, alloc(~0ull));
     for (;;) {
       const uint64_t act = __builtin_amdgcn_ballot_w64(r > 0);
       bool any_act = act != 0;
       DMF_T(tr0);
-      if ((int)__builtin_popcountll(act) <= 64 - REFILL) {
+      // (active lanes counted on 32-bit halves: the 64-bit popcount's compare became a VALU op)
+      if (__builtin_popcount((uint32_t)act) + __builtin_popcount((uint32_t)(act >> 32)) <= 64 - REFILL) {
         const uint64_t take = __builtin_amdgcn_ballot_w64(r <= 0 && fok);
         if (take) {
 #if defined(DMF_EXP_STATS)
           if (l == 0) ++nrefill;
 #endif
           DMF_T(td0);
+          const bool pf = more;
+          const uint32_t base0 = pf ? alloc(take) : 0u;
           if (r <= 0 && fok) {
             decode();
             fok = false;
@@ -1729,7 +1786,7 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
 #endif
           DMF_TACC(t_dec, td0);
           DMF_T(tp0);
-          if (more) prefetch(take);
+          if (pf) fetch(take, base0);
           DMF_TACC(t_pf, tp0);
           any_act = __builtin_amdgcn_ballot_w64(r > 0) != 0;
         }
@@ -1816,6 +1873,9 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
     __syncthreads();
     DMF_TACC(t_flush, tf0);
   }
+#if defined(DMF_EXP_F_REBUILD)
+  if (sink == 0x9e3779b9u + xnrays) atomicAdd(&hits[0], 0);  // never true in practice: keeps the proxy
+#endif
   if (stats) {
     for (int o = 32; o > 0; o >>= 1) nflush += __shfl_down(nflush, o, 64);
     if (l == 0 && nflush) atomicAdd(&stats[6], nflush);
@@ -2349,7 +2409,8 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
       if (slab)
         hipLaunchKernelGGL((k_bk_fuse_s<kBkRefill, kBkSpread, kBkUnroll>), dim3(nfF), dim3(kBkThreads), 0, v->stream, g, bg,
                            (const uint4*)b.pra, (const uint32_t*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,
-                           (const uint2*)b.order, pl.part_max, b.ctl, d_hits, d_misses, st);
+                           (const uint2*)b.order, pl.part_max, b.ctl, d_hits, d_misses, st, (const ulonglong2*)b.rays,
+                           (uint32_t)(ps * pl.ppose * 64), (uint32_t)std::min<uint64_t>(pl.pair_cap, UINT32_MAX));
       else
         hipLaunchKernelGGL((k_bk_fuse<16, 8, 8>), dim3(nf), dim3(kBkThreads), 0, v->stream, g, bg, (const uint4*)b.pra,
                            (const uint2*)b.prb, (const uint32_t*)b.off, (const uint32_t*)b.cnt,

@@ -34,6 +34,11 @@ namespace dmf {
 #else
 #define DMF_FWD_OCC
 #endif
+#if defined(DMF_EXP_FWDQ_WAVES)
+#define DMF_FWDQ_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_FWDQ_WAVES)))
+#else
+#define DMF_FWDQ_OCC
+#endif
 
 struct EnumList {
   const float* axes;  // xs | ys | zs (float-accumulated, RayTracingEngine.hpp:54-56)
@@ -1090,6 +1095,242 @@ __global__ __launch_bounds__(256) DMF_FWD_OCC void k_forward(Geom g, DevVol vd, 
   fwd_ray<kSkip>(g, vd, cam, pose + blockIdx.y, zstart, zdelta, rdelta, cdelta, R, C, ri, ci,
                  k_out + (int64_t)blockIdx.y * R * C, slot_out + (int64_t)blockIdx.y * R * C, hazards, samples);
   if (stats) wave_add_u64(&stats[0], (unsigned long long)samples);
+#if defined(DMF_EXP_STATS)
+  // diagnostic build: 64 x the wave's longest march (lane-samples the wave occupies), so that
+  // stats[0] / stats[1] is the march's lane utilisation
+  if (stats) {
+    unsigned long long mx = (unsigned long long)samples;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned long long)__shfl_xor(mx, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicAdd(&stats[1], 64ull * mx);
+  }
+#endif
+}
+
+// ---- forward march with per-wave lane refill (fwd_kernel knob 2) -----------------------
+// fwd_ray's loop, split into a per-pixel setup and one loop iteration (fwd_step), so that a lane
+// whose ray has ended takes the next pixel of its wave's queue while the others march on: the
+// k_reverse_q pattern on the forward march.  Same arithmetic, same outputs.
+struct FwdLane {
+  double dir[3], eA[3], eB[3];
+  float fdir[3], frd[3];
+  int k, zd, dmin_jump;
+  uint32_t known_full;
+  bool entered;
+};
+
+template <bool kSkip>
+__device__ inline void fwd_setup(const Geom& g, const DevVol& vd, const CamP& cam, const float* m, int zstart,
+                                 int zdelta, int r, int c, FwdLane& L) {
+  L.dmin_jump = 1 << 30;
+  if (kSkip) {
+    const double ux = ((double)c - cam.cx) / cam.fx, uy = ((double)r - cam.cy) / cam.fy;
+    double step = 0.0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const double m0 = m[4 * a], m1 = m[4 * a + 1], m2 = m[4 * a + 2];
+      L.dir[a] = 0.001 * (m0 * ux + m1 * uy + m2);
+      L.eA[a] = 0x1p-21 * fabs((double)m[4 * a + 3]);
+      L.eB[a] = 0x1p-21 * 0.001 * (fabs(m0 * ux) + fabs(m1 * uy) + fabs(m2));
+      L.fdir[a] = (float)L.dir[a];
+      L.frd[a] = L.dir[a] != 0.0 ? (float)(1.0 / L.dir[a]) : 0.0f;
+      step = fmax(step, fabs(L.dir[a]) * zdelta / g.dl[a]);
+    }
+    L.dmin_jump = 1 + (int)ceil(2.0 * step / (double)(1 << vd.bsh)) + 1;
+  }
+  L.known_full = 0xffffffffu;
+  L.entered = false;
+  L.k = 0;
+  L.zd = zstart;
+}
+
+// One iteration of fwd_ray's loop for pixel (r, c): 0 = march on, 1 = hit (kk, sl), 2 = the
+// march left the depth range without a hit.
+template <bool kSkip>
+__device__ inline int fwd_step(const Geom& g, const DevVol& vd, const CamP& cam, const float* m, int zstart, int zdelta,
+                               int last_k, int r, int c, FwdLane& L, int32_t& kk, int32_t& sl,
+                               unsigned long long* __restrict__ hazards, int64_t& samples) {
+  if (!((double)L.zd < kZMax * 1000)) return 2;
+  auto margin = [&](int a, double zd) { return 2.0 * (L.eA[a] + zd * L.eB[a]) + 1e-9; };
+  float pc[3], w[3];
+  project(cam, r, c, L.zd, pc);
+  xform(m, pc[0], pc[1], pc[2], w);
+  ++samples;
+  if (!valid_points_f(g, w)) {
+    if (kSkip && !L.entered) {
+      L.entered = true;
+      double tin = -1e300, tout = 1e300;
+      const double zmax = kZMax * 1000;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const double dm = margin(a, zmax);
+        const double lo = g.mn[a] - dm, hi = g.mx[a] + dm, t0 = (double)m[4 * a + 3];
+        if (L.dir[a] == 0.0) {
+          if (t0 <= lo || t0 >= hi) tout = -1e300;
+        } else {
+          const double ta = (lo - t0) / L.dir[a], tb = (hi - t0) / L.dir[a];
+          tin = fmax(tin, fmin(ta, tb));
+          tout = fmin(tout, fmax(ta, tb));
+        }
+      }
+      int kj = tout < tin ? last_k : (int)floor((tin - (double)zstart) / zdelta) - 1;
+      kj = min(kj, last_k);
+      if (kj > L.k) {
+        const int zj = zstart + kj * zdelta;
+        float qc[3], q[3];
+        project(cam, r, c, zj, qc);
+        xform(m, qc[0], qc[1], qc[2], q);
+        ++samples;
+        if (!valid_points_f(g, q)) {
+          L.k = kj;
+          L.zd = zj;
+        }
+      }
+    }
+    L.zd += zdelta;
+    ++L.k;
+    return 0;
+  }
+  L.entered = true;
+  int a, b, cc;
+  bin_point(g, w, a, b, cc);
+  if (!valid_coords(g, a, b, cc)) {
+    atomicAdd(hazards, 1ull);
+    L.zd += zdelta;
+    ++L.k;
+    return 0;
+  }
+  if (occ_test(vd.occ, occ_bit(g, a, b, cc))) {
+    kk = L.k;
+    sl = vd.slot_of[lin_index(g, a, b, cc)];
+    return 1;
+  }
+  if (kSkip) {
+    const int ba = a >> vd.bsh, bb = b >> vd.bsh, bc = cc >> vd.bsh;
+    const uint32_t bl = ((uint32_t)ba * (uint32_t)vd.nb[1] + (uint32_t)bb) * (uint32_t)vd.nb[2] + (uint32_t)bc;
+    if (bl != L.known_full) {
+      bool jumped = false;
+      const int d = vd.bdist[bl];
+      if (d >= L.dmin_jump) {
+        const int Rb = d - 1;
+        const int bx[3] = {ba, bb, bc};
+        double lo[3], hi[3];
+        float zexit = 3.0e38f;
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+          lo[ax] = g.mn[ax] + (double)(max(bx[ax] - Rb, 0) << vd.bsh) * g.dl[ax];
+          hi[ax] = g.mn[ax] + (double)min((bx[ax] + Rb + 1) << vd.bsh, g.n[ax]) * g.dl[ax];
+          if (L.fdir[ax] != 0.0f)
+            zexit = fminf(zexit, ((float)(L.fdir[ax] > 0.0f ? hi[ax] : lo[ax]) - m[4 * ax + 3]) * L.frd[ax]);
+        }
+        int kj = min((int)floorf((zexit - (float)zstart) / (float)zdelta) - 1, last_k);
+        if (kj > L.k + 1) {
+          const int zj = zstart + kj * zdelta;
+          float qc[3], q[3];
+          project(cam, r, c, zj, qc);
+          xform(m, qc[0], qc[1], qc[2], q);
+          ++samples;
+          bool ok = true;
+#pragma unroll
+          for (int ax = 0; ax < 3; ++ax) {
+            const double dm = margin(ax, (double)zj);
+            ok = ok && (double)w[ax] >= lo[ax] + dm && (double)w[ax] <= hi[ax] - dm && (double)q[ax] >= lo[ax] + dm &&
+                 (double)q[ax] <= hi[ax] - dm;
+          }
+          if (ok) {
+            L.k = kj;
+            L.zd = zj;
+            jumped = true;
+          }
+        }
+      }
+      if (!jumped) L.known_full = bl;
+    }
+  }
+  L.zd += zdelta;
+  ++L.k;
+  return 0;
+}
+
+// Each wave owns kUnit consecutive 8x8 tiles of one pose (grid.y) and keeps its lanes busy:
+// a lane whose ray has ended writes its outputs and takes the next pixel of the unit (tile
+// order: neighbouring rays together) when at least kRefill lanes are idle; between refills
+// every busy lane marches up to kBurst samples.
+template <bool kSkip, int kUnit, int kRefill, int kBurst>
+__global__ __launch_bounds__(256) DMF_FWDQ_OCC void k_forward_q(Geom g, DevVol vd, CamP cam,
+                                                                const PoseX* __restrict__ pose, int zstart, int zdelta,
+                                                                int rdelta, int cdelta, int R, int C,
+                                                                int32_t* __restrict__ k_out, int32_t* __restrict__ slot_out,
+                                                                unsigned long long* __restrict__ hazards,
+                                                                unsigned long long* __restrict__ stats) {
+  stats = stat_slot(stats);
+  const int w = threadIdx.x >> 6;
+  const int tpr = (C + 7) >> 3;
+  const int64_t ntiles = (int64_t)((R + 7) >> 3) * tpr;
+  const int64_t t0 = ((int64_t)blockIdx.x * 4 + w) * kUnit;
+  if (t0 >= ntiles) return;
+  const int nitems = (int)min<int64_t>(ntiles - t0, kUnit) * 64;
+  const float* m = pose[blockIdx.y].f;
+  int32_t* const ko = k_out + (int64_t)blockIdx.y * R * C;
+  int32_t* const so = slot_out + (int64_t)blockIdx.y * R * C;
+  const int last_k = (int)((kZMax * 1000 - 1 - zstart) / zdelta);
+  int64_t samples = 0;
+  [[maybe_unused]] unsigned long long busy = 0, slots = 0;  // (diagnostic build: lane utilisation)
+  FwdLane L;
+  int item = -1, r = 0, c = 0;
+  int64_t idx = 0;
+  int next = 0;  // wave-uniform queue head
+  while (true) {
+    const uint64_t idle = __builtin_amdgcn_ballot_w64(item < 0);
+    const int nidle = __builtin_popcountll(idle);
+    if (next < nitems && (nidle >= kRefill || nidle == 64)) {
+      if (item < 0) {
+        const int it = next + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        if (it < nitems) {
+          const int64_t tile = t0 + (it >> 6);
+          const int ln = it & 63;
+          const int ri = (int)(tile / tpr) * 8 + (ln >> 3), ci = (int)(tile % tpr) * 8 + (ln & 7);
+          if (ri < R && ci < C) {
+            item = it;
+            idx = (int64_t)ri * C + ci;
+            r = ri * rdelta;
+            c = ci * cdelta;
+            fwd_setup<kSkip>(g, vd, cam, m, zstart, zdelta, r, c, L);
+          }
+        }
+      }
+      next += nidle;
+    }
+    if (__builtin_amdgcn_ballot_w64(item >= 0) == 0) {
+      if (next >= nitems) break;
+      continue;
+    }
+    int st = 0;
+    int32_t kk = -1, sl = -1;
+#pragma unroll 1
+    for (int b = 0; b < kBurst; ++b) {
+#if defined(DMF_EXP_STATS)
+      if ((threadIdx.x & 63) == 0) slots += 64;
+      if (item >= 0 && st == 0) ++busy;
+#endif
+      if (item >= 0 && st == 0) st = fwd_step<kSkip>(g, vd, cam, m, zstart, zdelta, last_k, r, c, L, kk, sl, hazards, samples);
+      if (__builtin_amdgcn_ballot_w64(item >= 0 && st == 0) == 0) break;
+    }
+    if (item >= 0 && st != 0) {
+      ko[idx] = kk;
+      so[idx] = sl;
+      item = -1;
+    }
+  }
+  if (stats) wave_add_u64(&stats[0], (unsigned long long)samples);
+#if defined(DMF_EXP_STATS)
+  // diagnostic build: busy lane-iterations against 64 x burst iterations (stats[0] / stats[1]
+  // of k_forward is the same utilisation of its lane-per-pixel march)
+  if (stats) {
+    wave_add_u64(&stats[2], busy);
+    wave_add_u64(&stats[3], slots);
+  }
+#endif
 }
 
 // The batched forward march with per-XCD unit queues (as k_reverse_x): a unit is one
@@ -1133,6 +1374,13 @@ __global__ __launch_bounds__(256) void k_forward_x(Geom g, DevVol vd, CamP cam, 
   }
   if (stats) wave_add_u64(&stats[0], (unsigned long long)samples);
 }
+
+// k_forward_q's shape: tiles per wave unit, refill threshold, samples per burst
+#if defined(DMF_EXP_FWDQ_UNIT)
+constexpr int kFwdUnit = DMF_EXP_FWDQ_UNIT, kFwdRefill = DMF_EXP_FWDQ_REFILL, kFwdBurst = DMF_EXP_FWDQ_BURST;
+#else
+constexpr int kFwdUnit = 4, kFwdRefill = 16, kFwdBurst = 8;
+#endif
 
 // threads of a k_forward launch per pose: whole 8x8 tiles of the R x C lattice
 static unsigned fwd_blocks(int R, int C) {
@@ -1593,12 +1841,30 @@ int dmf_forward_first_hits_device(dmf_volume* v, const dmf_camera* cam, const fl
     else
       hipLaunchKernelGGL(k_forward_x<false>, grid, dim3(256), 0, v->stream, v->geom(), v->dev(), cam_params(cam), tab,
                          P, zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot, heads, (unsigned long long*)aux, st);
+  } else if (v->knob[DMF_KNOB_FWD_KERNEL] == 2) {
+    // per-wave lane refill over units of kFwdUnit tiles (k_forward_q)
+    const int64_t ntiles = (int64_t)((R + 7) / 8) * ((C + 7) / 8), nunits = (ntiles + kFwdUnit - 1) / kFwdUnit;
+    const dim3 grid((unsigned)((nunits + 3) / 4), (unsigned)P);
+    if (fwd_skip(v)) {
+      DMF_TRY(ensure_brick_dist(v));
+      hipLaunchKernelGGL((k_forward_q<true, kFwdUnit, kFwdRefill, kFwdBurst>), grid, dim3(256), 0, v->stream, v->geom(),
+                         v->dev(), cam_params(cam), tab, zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot,
+                         (unsigned long long*)aux, st);
+    } else {
+      hipLaunchKernelGGL((k_forward_q<false, kFwdUnit, kFwdRefill, kFwdBurst>), grid, dim3(256), 0, v->stream,
+                         v->geom(), v->dev(), cam_params(cam), tab, zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot,
+                         (unsigned long long*)aux, st);
+    }
   } else {
     DMF_LAUNCH_FORWARD(dim3(fwd_blocks(R, C), (unsigned)P), v->geom(), v->dev(), cam_params(cam), tab,
                        zstart, zdelta, rdelta, cdelta, R, C, d_k, d_slot, (unsigned long long*)aux, st);
   }
   DMF_LAUNCH_CHECK();
+#if defined(DMF_EXP_STATS)
+  if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 4));
+#else
   if (d_stats) DMF_TRY(stats_end(v, st, d_stats, 1));
+#endif
   return DMF_OK;
   DMF_API_END
 }

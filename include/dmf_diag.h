@@ -54,7 +54,8 @@ enum dmf_knob {
                                   then invalid; dmf_fuse_status reports it, and no store leaves the pair
                                   buffers); 0 = off */
   DMF_KNOB_FWD_KERNEL = 11,  /* batched forward first hits (dmf_forward_first_hits_device): 0 default (a grid of
-                                (tile block, pose): k_forward), 1 per-XCD unit queues (k_forward_x) */
+                                (tile block, pose): k_forward), 1 per-XCD unit queues (k_forward_x), 2 per-wave lane refill
+                                over units of 8x8 tiles (k_forward_q) */
   DMF_KNOB_BDIST_CAP = 12,   /* saturation of the brick distance field of the reverse / forward marches' empty-space
                                 jumps, in bricks (1..255; 0 = the default 63); rebuilt at the next march */
   DMF_KNOB_COUNT = 13

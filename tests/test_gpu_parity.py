@@ -595,11 +595,11 @@ def test_golden_config1_gpu(dmf):
     assert np.array_equal(sha(eng.fuse_finalize(vf, hits, misses)), z["fuse_logodds_sha"])
 
 
-@pytest.mark.parametrize("fwd_kernel", [0, 1])
+@pytest.mark.parametrize("fwd_kernel", [0, 1, 2])
 def test_forward_first_hits_batched_device(oracle, engine, oeng, dmf, fwd_kernel):
-    """dmf_forward_first_hits_device over P poses in one launch == the oracle per pose (both
-    batched kernels, DMF_KNOB_FWD_KERNEL: 0 = the (tile block, pose) grid, 1 = per-XCD unit
-    queues)."""
+    """dmf_forward_first_hits_device over P poses in one launch == the oracle per pose (every
+    batched kernel, DMF_KNOB_FWD_KERNEL: 0 = the (tile block, pose) grid, 1 = per-XCD unit
+    queues, 2 = per-wave lane refill k_forward_q; odd strides give partial 8x8 tiles)."""
     import ctypes as C
     from dmf_amd import _lib
     ov = Hh.oracle_volume(oracle, n=100)

@@ -68,6 +68,8 @@ for kf in KS:
     torch.cuda.synchronize(dev)
     out.setdefault(f"ms_fwd{kf}", []).append(round(e0.elapsed_time(e1) / 5, 4))
     out[f"samples_fwd{kf}"] = int(fst[0].item()) // 5
+    if int(fst[1].item()) > 0:  # DMF_EXP_STATS library: lane utilisation of the march
+        out[f"lane_util_fwd{kf}"] = round(int(fst[0].item()) / int(fst[1].item()), 4)
     res[kf] = (kb.cpu().numpy().copy(), sb.cpu().numpy().copy())
 k0 = KS[0]
 out["outputs_equal"] = bool(all(np.array_equal(res[k0][0], r[0]) and np.array_equal(res[k0][1], r[1]) for r in res.values()))
