@@ -1,22 +1,24 @@
 #!/bin/bash
-# Round 6: phase F with the refill's index allocation issued before the decode (pfa) vs the
-# product, and the cost proxy of a compact pair record (rebuild: F redoes pass B's per-pair
-# arithmetic on a ray record per adopted pair); kernel times of each.
+# Round 6: phase F's refill and walk bookkeeping -- pfa (index allocation before the decode),
+# vs (+ strides from the record bits in VALU instead of the LDS table slut), fasm / vsasm (the
+# walk block as inline asm: 6 SALU per slab instead of 8 + a branch + an s_nop), against the
+# product build; alternating, headline and config 2, then F / B kernel times.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
-O=gpurun_out/r06e
+O=gpurun_out/r06f
 mkdir -p $O
 B=depth-map-fusion-utils_amd
+LIBS="product pfa vs fasm vsasm"
 for rep in 1 2; do
-  for lib in product pfa fasm rebuild; do
+  for lib in $LIBS; do
     L=$B/build/libdmf.so; [ $lib != product ] && L=$B/build_exp/$lib/libdmf.so
     DMF_LIB=$L timeout -k 10 200 python3 tools/exp_fuse.py --tag $lib --calls 60 > $O/c4_${lib}_$rep.json 2> $O/c4_${lib}_$rep.err || { echo "FAIL $lib"; tail -5 $O/c4_${lib}_$rep.err; exit 3; }
     DMF_LIB=$L timeout -k 10 200 python3 tools/exp_fuse.py --tag $lib --grid 256 --poses 64 --calls 150 > $O/c2_${lib}_$rep.json 2> /dev/null || { echo "FAIL $lib"; exit 3; }
     python3 -c "import json; b=json.load(open('$O/c4_${lib}_$rep.json')); c=json.load(open('$O/c2_${lib}_$rep.json')); print('$lib', round(b['serial_ms'],4), round(b['pipelined_ms'],4), b['digest']=='36708f70245952ff', round(c['serial_ms'],4), round(c['pipelined_ms'],4), c['digest']=='605646542483b87f')"
   done
 done
-for lib in product pfa fasm rebuild; do
+for lib in $LIBS; do
   L=$B/build/libdmf.so; [ $lib != product ] && L=$B/build_exp/$lib/libdmf.so
   DMF_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$lib -o run -- python3 tools/exp_fuse.py --calls 20 --modes serial > /dev/null 2> $O/kt_$lib.err || { echo "KTFAIL $lib"; exit 4; }
   python3 -c "
