@@ -1592,17 +1592,6 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
 #define DMF_T(x)
 #define DMF_TACC(acc, x)
 #endif
-// Phase F's (dM, d1, d2) LDS byte strides of a 20-B record from its word 4 (step signs at bits
-// 25-27, major axis M at 28-29): the axis strides with their signs, then permuted into (major,
-// minor 1, minor 2) order -- the VALU form of the round-5 table slut.
-__device__ inline uint4 bk_strides(uint32_t w4) {
-  const int32_t sx = (int32_t)(4u * kBkSx) - (int32_t)(8u * kBkSx) * (int32_t)((w4 >> 25) & 1u),
-                sy = (int32_t)(4u * kBkSy) - (int32_t)(8u * kBkSy) * (int32_t)((w4 >> 26) & 1u),
-                sz = 4 - 8 * (int32_t)((w4 >> 27) & 1u);
-  const uint32_t M = (w4 >> 28) & 3u;
-  return make_uint4((uint32_t)(M == 0 ? sx : (M == 1 ? sy : sz)), (uint32_t)(M == 0 ? sy : sx),
-                    (uint32_t)(M == 2 ? sy : sz), 0u);
-}
 template <int REFILL, int S_ORDER, int UNROLL>
 __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, const uint4* __restrict__ pa,
                                                           const uint32_t* __restrict__ pw,
@@ -1702,15 +1691,9 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       nK1 = 0u - sd.a1;
       cur = sd.entry * 4u;
       r = (int)sd.S;
-#if defined(DMF_EXP_F_SLUT)
+      // (the strides computed from the record bits in VALU instead measured slower: F 3.39 ->
+      // 3.50 ms, profiles/r06f -- the table read's latency is not what the refill waits on)
       const uint4 st3 = slut[cw >> 24 & 127u];
-#else
-      // the pair's (dM, d1, d2) LDS byte strides from its step signs and major axis, in VALU:
-      // round 5 read them from the 128-entry table slut, an LDS read whose latency the refill
-      // waited out behind the walk's queued, bank-conflicted adds (32 % of F's wave time was
-      // refill, profiles/r06d)
-      const uint4 st3 = bk_strides(cw);
-#endif
       dM = st3.x;
       d1 = st3.y;
       d2 = st3.z;
@@ -1823,61 +1806,8 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
 #endif
       // the k-th slab from here is walked iff r > k: inside the block the threshold moves
       // (u) and r drops by UNROLL once at its end
-#if defined(DMF_EXP_F_ASM)
-      // experiment build: the block's slabs as asm statements -- the same 17 VALU per slab,
-      // but each slab's three masked adds under 6 SALU (the masks as s_or / s_and, exec taken
-      // and restored once) instead of the compiler's 8 + a branch + an s_nop; the box's LDS
-      // offset is added to the addresses (cur is relative to the box)
-      {
-        typedef __attribute__((address_space(3))) uint32_t lds_u32;
-        const uint32_t lbase = (uint32_t)(uintptr_t)(lds_u32*)box;
-        uint32_t cura = cur + lbase, x1, x2, t, p1, p2;
-        uint64_t c1m, c2m, ownm, o1m, morm, mandm, svm;
-        const uint32_t one = 1u;
-#define DMF_SLAB_ASM(U)                                                   \
-  "v_cmp_le_i32_e64 %[c1], 0, %[b1]\n"                                    \
-  "v_cmp_le_i32_e64 %[c2], 0, %[b2]\n"                                    \
-  "v_cmp_lt_i32_e64 %[own], " #U ", %[r]\n"                               \
-  "v_cmp_gt_i32_e64 %[o1], 0, %[b12]\n"                                   \
-  "v_cndmask_b32_e64 %[x1], 0, %[d1], %[c1]\n"                            \
-  "v_cndmask_b32_e64 %[x2], 0, %[d2], %[c2]\n"                            \
-  "v_cndmask_b32_e64 %[t], %[K1], %[K1mM], %[c1]\n"                       \
-  "v_add_u32_e32 %[b1], %[b1], %[t]\n"                                    \
-  "v_cndmask_b32_e64 %[t], %[K2], %[K2mM], %[c2]\n"                       \
-  "v_add_u32_e32 %[b2], %[b2], %[t]\n"                                    \
-  "v_cndmask_b32_e64 %[t], 0, %[K2], %[c1]\n"                             \
-  "v_cndmask_b32_e64 %[p1], 0, %[nK1], %[c2]\n"                           \
-  "v_add3_u32 %[b12], %[b12], %[t], %[p1]\n"                              \
-  "v_cndmask_b32_e64 %[t], %[x2], %[x1], %[o1]\n"                         \
-  "v_add_u32_e32 %[p1], %[cur], %[t]\n"                                   \
-  "v_add3_u32 %[p2], %[cur], %[x1], %[x2]\n"                              \
-  "s_or_b64 %[mor], %[c1], %[c2]\n"                                       \
-  "s_and_b64 %[mand], %[c1], %[c2]\n"                                     \
-  "s_and_saveexec_b64 %[sv], %[own]\n"                                    \
-  "ds_add_u32 %[cur], %[one]\n"                                           \
-  "s_and_b64 exec, exec, %[mor]\n"                                        \
-  "ds_add_u32 %[p1], %[one]\n"                                            \
-  "s_and_b64 exec, exec, %[mand]\n"                                       \
-  "ds_add_u32 %[p2], %[one]\n"                                            \
-  "s_mov_b64 exec, %[sv]\n"                                               \
-  "v_add_u32_e32 %[cur], %[p2], %[dM]\n"
-        static_assert(UNROLL == 8, "the asm walk block holds 8 slabs");
-#define DMF_SLAB_ASM_OPS                                                                                      \
-  : [b1] "+v"(b1), [b2] "+v"(b2), [b12] "+v"(b12), [cur] "+v"(cura), [x1] "=&v"(x1), [x2] "=&v"(x2), [t] "=&v"(t), \
-    [p1] "=&v"(p1), [p2] "=&v"(p2), [c1] "=&s"(c1m), [c2] "=&s"(c2m), [own] "=&s"(ownm), [o1] "=&s"(o1m),          \
-    [mor] "=&s"(morm), [mand] "=&s"(mandm), [sv] "=&s"(svm)                                                     \
-  : [r] "v"(r), [d1] "v"(d1), [d2] "v"(d2), [dM] "v"(dM), [K1] "v"(K1), [K1mM] "v"(K1mM), [K2] "v"(K2),          \
-    [K2mM] "v"(K2mM), [nK1] "v"(nK1), [one] "v"(one)
-        asm volatile(DMF_SLAB_ASM(0) DMF_SLAB_ASM(1) DMF_SLAB_ASM(2) DMF_SLAB_ASM(3) DMF_SLAB_ASM(4) DMF_SLAB_ASM(5)
-                         DMF_SLAB_ASM(6) DMF_SLAB_ASM(7) DMF_SLAB_ASM_OPS);
-#undef DMF_SLAB_ASM_OPS
-#undef DMF_SLAB_ASM
-        cur = cura - lbase;
-      }
-#else
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-
         const bool c1 = (int32_t)b1 >= 0, c2 = (int32_t)b2 >= 0, o2 = (int32_t)b12 >= 0;
         const uint32_t x1 = c1 ? d1 : 0u, x2 = c2 ? d2 : 0u;
         // the slab's cells: cur, then p1 if a minor crosses (on m2 iff o2, also when only
@@ -1893,14 +1823,10 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
         b2 += c2 ? K2mM : K2;
         b12 += (c1 ? K2 : 0u) + (c2 ? nK1 : 0u);
       }
-#endif
       r -= UNROLL;
       DMF_TACC(t_walk, tw0);
     }
     DMF_T(tf0);
-#if defined(DMF_EXP_F_ASM)
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the asm walk's LDS adds, unknown to the compiler
-#endif
     __syncthreads();
     if constexpr (bk::kLog != 5) {
       // (experiment builds with another brick edge: the generic mapping of k_bk_fuse)
