@@ -975,6 +975,7 @@ def secondary_reverse(vol, L, cam, dev, stream, d_depth, d_poses, P, K, poses_h,
     against the GPU's."""
     import ctypes as C
     H, W = HEIGHT, WIDTH
+    n_int = min(n_int, P)  # (a rank with fewer frames integrates all of them)
     xyz = torch.empty((n_int, H, W, 3), dtype=torch.float32, device=dev)
     _lib.check(L.dmf_backproject_device(vol._h, C.addressof(cam), d_depth.data_ptr(), d_poses.data_ptr(), n_int,
                                         xyz.data_ptr()))

@@ -234,8 +234,8 @@ __device__ inline int pixel_ray(const Geom& g, const CamP& cam, const uint16_t* 
 
 // The brick path's ray record: pixel_ray up to the quantised endpoints, with the pose's grid
 // origin already computed (go = grid_origin of poses[p]'s translation; d < 0: outside the frame).
-__device__ inline bool pixel_quant_go(const Geom& g, const CamP& cam, int d, const PoseX& T, const double go[3], int r,
-                                      int c, int dmin, int dmax, int64_t qs[3], int64_t qe[3], bool& inside,
+__device__ inline bool pixel_quant_go(const Geom& g, const CamP& cam, int d, const float Tf[12], const double go[3],
+                                      int r, int c, int dmin, int dmax, int64_t qs[3], int64_t qe[3], bool& inside,
                                       bool& valid) {
   valid = false;
   inside = false;
@@ -243,7 +243,7 @@ __device__ inline bool pixel_quant_go(const Geom& g, const CamP& cam, int d, con
   valid = true;
   float pc[3], E[3];
   project(cam, r, c, d, pc);
-  xform(T.f, pc[0], pc[1], pc[2], E);
+  xform(Tf, pc[0], pc[1], pc[2], E);
   inside = endpoint_inside(g, E);
   return dda_quantize_go(g, go, E, inside, qs, qe);
 }
@@ -709,22 +709,42 @@ __device__ inline void bk_rays_wg(const BkRaysArgs& A_, unsigned wg, uint32_t* h
   unsigned long long upd = 0, nvalid = 0, nhit = 0;
   // (loading the next packet's depth one packet ahead measured slower: 0.79 -> 0.84 ms)
   double go[3];
+  // the workgroup's pose, held in registers: read in the packet loop, it was reloaded after
+  // every packet's record stores (they might alias it), and the load's vmcnt wait then drained
+  // those stores each packet
+  float Tf[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) Tf[i] = A_.poses[pw].f[i];
   {
-    const float O[3] = {A_.poses[pw].f[3], A_.poses[pw].f[7], A_.poses[pw].f[11]};
+    const float O[3] = {Tf[3], Tf[7], Tf[11]};
     grid_origin(g, O, go);
   }
+#if defined(DMF_EXP_A_DNEXT)
+  // experiment build: the next packet's depth loaded one packet ahead, before this packet's two
+  // record stores (a static count, so its wait need not drain them)
+  auto depth_of = [&](int64_t pkx) {
+    const int qx = (int)(pkx - (int64_t)pw * A_.packets_pose);
+    return pixel_depth(A_.cam, A_.depth, pw, (qx / A_.packets_x) * 8 + (l >> 3), (qx % A_.packets_x) * 8 + (l & 7));
+  };
+  int dnext = pk0 + w < pk1 ? depth_of(pk0 + w) : -1;
+#endif
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
     const int p = pw;
     const int q = (int)(pk - (int64_t)p * A_.packets_pose);
     const int r = (q / A_.packets_x) * 8 + (l >> 3), c = (q % A_.packets_x) * 8 + (l & 7);
+#if defined(DMF_EXP_A_DNEXT)
+    const int d = dnext;
+    if (pk + nw < pk1) dnext = depth_of(pk + nw);
+#else
     const int d = pixel_depth(A_.cam, A_.depth, p, r, c);
+#endif
     int64_t qs[3], qe[3];
     bool inside, valid;
     ulonglong2 rec;
     rec.x = 0;
     rec.y = 0;
     uint64_t path = 0;  // the crossing axes of the coarse walk (pass B replays them)
-    if (pixel_quant_go(g, A_.cam, d, A_.poses[p], go, r, c, A_.dmin, A_.dmax, qs, qe, inside, valid)) {
+    if (pixel_quant_go(g, A_.cam, d, Tf, go, r, c, A_.dmin, A_.dmax, qs, qe, inside, valid)) {
       uint64_t A, B;
       bk::pack_ray(qs, qe, inside, A, B);
       rec.x = A;
@@ -1780,7 +1800,10 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
           DMF_T(td0);
           const bool pf = more;
           const uint32_t base0 = pf ? alloc(take) : 0u;
-          if (r <= 0 && fok) {
+          // the lanes of `take`, as a lane mask (their next records are loaded under the same
+          // mask: no lane test of `take` in the fetch)
+          const bool tk = r <= 0 && fok;
+          if (tk) {
             decode();
             fok = false;
           }
@@ -1789,7 +1812,24 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
 #endif
           DMF_TACC(t_dec, td0);
           DMF_T(tp0);
-          if (pf) fetch(take, base0);
+          // (read on every path, so that no path leaves the allocation's LDS return pending
+          // into the walk block: the compiler's wait for it there drained the LDS queue at every
+          // block's end)
+          const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base0);
+          if (pf) {
+            if (base + (uint32_t)__builtin_popcountll(take) >= n) more = false;
+            if (tk) {
+              const uint32_t k = base + (uint32_t)lane_prefix(take);
+              fok = k < n;
+              const uint32_t ob = bk_order<S_ORDER>(k, n);
+#if defined(DMF_EXP_F_REBUILD)
+              kid = p0 + ob;
+#endif
+              const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_a, ob * 16u, 0, 0);
+              ca = make_uint4(v[0], v[1], v[2], v[3]);
+              cw = __builtin_amdgcn_raw_buffer_load_b32(rs_w, ob * 4u, 0, 0);
+            }
+          }
           DMF_TACC(t_pf, tp0);
           any_act = __builtin_amdgcn_ballot_w64(r > 0) != 0;
         }

@@ -1,16 +1,15 @@
 #!/bin/bash
-# Round 6: phase F's refill and walk bookkeeping -- pfa (index allocation before the decode),
-# vs (+ strides from the record bits in VALU instead of the LDS table slut), fasm / vsasm (the
-# walk block as inline asm: 6 SALU per slab instead of 8 + a branch + an s_nop), against the
-# product build; alternating, headline and config 2, then F / B kernel times.
+# Round 6: phase F with the refill's allocation read on every path (tkw: no LDS-queue drain at
+# every walk block's end, which the compiler had inserted for a possibly pending allocation
+# return) vs tkf and the product; three alternations, headline and config 2, kernel times.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
-O=gpurun_out/r06f
+O=gpurun_out/r06h
 mkdir -p $O
 B=depth-map-fusion-utils_amd
-LIBS="product pfa vs fasm vsasm vsl vsasml"
-for rep in 1 2; do
+LIBS="product tkf tkw"
+for rep in 1 2 3; do
   for lib in $LIBS; do
     L=$B/build/libdmf.so; [ $lib != product ] && L=$B/build_exp/$lib/libdmf.so
     DMF_LIB=$L timeout -k 10 200 python3 tools/exp_fuse.py --tag $lib --calls 60 > $O/c4_${lib}_$rep.json 2> $O/c4_${lib}_$rep.err || { echo "FAIL $lib"; tail -5 $O/c4_${lib}_$rep.err; exit 3; }
