@@ -709,9 +709,9 @@ __device__ inline void bk_rays_wg(const BkRaysArgs& A_, unsigned wg, uint32_t* h
   unsigned long long upd = 0, nvalid = 0, nhit = 0;
   // (loading the next packet's depth one packet ahead measured slower: 0.79 -> 0.84 ms)
   double go[3];
-  // the workgroup's pose, held in registers: read in the packet loop, it was reloaded after
-  // every packet's record stores (they might alias it), and the load's vmcnt wait then drained
-  // those stores each packet
+  // the workgroup's pose, held in registers (read in the packet loop, it was reloaded after
+  // every packet's record stores, which might alias it: ±0, profiles/r06i -- as the next
+  // packet's depth loaded a packet ahead, +5 % A, pass A is not waiting on its stores)
   float Tf[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) Tf[i] = A_.poses[pw].f[i];
@@ -719,25 +719,11 @@ __device__ inline void bk_rays_wg(const BkRaysArgs& A_, unsigned wg, uint32_t* h
     const float O[3] = {Tf[3], Tf[7], Tf[11]};
     grid_origin(g, O, go);
   }
-#if defined(DMF_EXP_A_DNEXT)
-  // experiment build: the next packet's depth loaded one packet ahead, before this packet's two
-  // record stores (a static count, so its wait need not drain them)
-  auto depth_of = [&](int64_t pkx) {
-    const int qx = (int)(pkx - (int64_t)pw * A_.packets_pose);
-    return pixel_depth(A_.cam, A_.depth, pw, (qx / A_.packets_x) * 8 + (l >> 3), (qx % A_.packets_x) * 8 + (l & 7));
-  };
-  int dnext = pk0 + w < pk1 ? depth_of(pk0 + w) : -1;
-#endif
   for (int64_t pk = pk0 + w; pk < pk1; pk += nw) {
     const int p = pw;
     const int q = (int)(pk - (int64_t)p * A_.packets_pose);
     const int r = (q / A_.packets_x) * 8 + (l >> 3), c = (q % A_.packets_x) * 8 + (l & 7);
-#if defined(DMF_EXP_A_DNEXT)
-    const int d = dnext;
-    if (pk + nw < pk1) dnext = depth_of(pk + nw);
-#else
     const int d = pixel_depth(A_.cam, A_.depth, p, r, c);
-#endif
     int64_t qs[3], qe[3];
     bool inside, valid;
     ulonglong2 rec;
