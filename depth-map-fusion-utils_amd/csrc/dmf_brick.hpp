@@ -611,13 +611,13 @@ __host__ __device__ inline void slab_walk_owned(int M, int32_t b1, int32_t b2, i
 // |b| < (2Q + 1) max|dq| gives |beta| < 2^18 + 2^9 for grids <= 1024 cells per axis
 // (|dq| < 2^18), a 20-bit two's-complement field; the +-never constant of a non-moving
 // axis (only its sign is ever used) is stored as +-(2^19 - 1).
-//   w0 = beta1 | aM[0:12) << 20          w1 = beta2 | aM[12:18) << 20 | code[0:6) << 26
+//   w0 = beta1 | aM[0:12) << 20          w1 = beta2 | aM[12:18) << 20 | S << 26 | ends << 31
 //   w2 = beta12 | a1[0:12) << 20         w3 = entry word | last word << 16
-//   w4 = a2 | a1[12:18) << 18 | code[6] << 24 | step signs (x, y, z) << 25 | M << 28 | ends << 30
-//        | code[7] << 31
-// (a = |dq| of the major / minor axes, code = the slab code of slab_code (S | s << 5 | e << 7),
-// entry / last = word offsets of the pair's first / last cell in phase F's LDS box).
-// (w[4] >> 24) & 127 is the 7-bit stride-table index of phase F (its bit 0, code[6], unused).
+//   w4 = a2 | a1[12:18) << 18 | T << 24,  T = s | e << 2 | step signs (x, y, z) << 3 | M << 6
+// (a = |dq| of the major / minor axes, (S, s, e) = the slab code of slab_code (S | s << 5 |
+// e << 7), entry / last = word offsets of the pair's first / last cell in phase F's LDS box).
+// T = w[4] >> 24 is the index of phase F's stride table: one LDS read gives the pair's three
+// strides and the offsets from L of the cells of L's slab that the code adopts (k_bk_fuse_s).
 __host__ __device__ inline uint32_t beta20(int32_t b) {
   const int32_t lim = (1 << 19) - 1;
   const int32_t s = b >> 9;  // arithmetic shift: floor(b / 512)
@@ -628,11 +628,25 @@ __host__ __device__ inline void pack20(int32_t b1, int32_t b2, int32_t b12, uint
                                        uint32_t entry, uint32_t last, uint32_t code, uint32_t signs, uint32_t M,
                                        bool ends, uint32_t w[5]) {
   w[0] = beta20(b1) | (aM & 0xfffu) << 20;
-  w[1] = beta20(b2) | ((aM >> 12) & 0x3fu) << 20 | (code & 0x3fu) << 26;
+  w[1] = beta20(b2) | ((aM >> 12) & 0x3fu) << 20 | (code & 31u) << 26 | (ends ? 1u << 31 : 0u);
   w[2] = beta20(b12) | (a1 & 0xfffu) << 20;
   w[3] = entry | last << 16;
-  w[4] = a2 | ((a1 >> 12) & 0x3fu) << 18 | ((code >> 6) & 1u) << 24 | signs << 25 | M << 28 | (ends ? 1u << 30 : 0u) |
-         ((code >> 7) & 1u) << 31;
+  w[4] = a2 | ((a1 >> 12) & 0x3fu) << 18 | ((code >> 5) & 7u) << 24 | signs << 27 | M << 30;
+}
+
+// Phase F's stride-table entry for T = w[4] >> 24 (k_bk_fuse_s reads one per refill): e[0..2] =
+// (dM, d1, d2), the signed steps of the major and minor axes in units of the box strides bx, by,
+// bz of +x, +y, +z (mod 2^32); e[3] = the offsets from L of the cells of L's slab that the slab
+// code adopts: L - d_e in the low 16 bits (signed; s >= 1) and L - d1 - d2 in the high 16 bits
+// (s == 2), 0 = none (needs |d1| + |d2| < 2^15).  Entries with M = 3 are never read.
+__host__ __device__ inline void slab_table_entry(uint32_t T, uint32_t bx, uint32_t by, uint32_t bz, uint32_t e[4]) {
+  const uint32_t s = T & 3u, ee = (T >> 2) & 1u, sg = (T >> 3) & 7u, M = T >> 6;
+  const uint32_t sx = sg & 1u ? 0u - bx : bx, sy = sg & 2u ? 0u - by : by, sz = sg & 4u ? 0u - bz : bz;
+  e[0] = M == 0 ? sx : (M == 1 ? sy : sz);
+  e[1] = M == 0 ? sy : sx;
+  e[2] = M == 2 ? sy : sz;
+  const uint32_t o1 = s >= 1 ? 0u - (ee ? e[2] : e[1]) : 0u, o2 = s == 2 ? 0u - e[1] - e[2] : 0u;
+  e[3] = (o1 & 0xffffu) | o2 << 16;
 }
 
 struct Slab20 {
@@ -654,13 +668,13 @@ __host__ __device__ inline void unpack20(const uint32_t w[5], Slab20& s) {
   s.a2 = w[4] & 0x3ffffu;
   s.entry = w[3] & 0xffffu;
   s.last = w[3] >> 16;
-  s.code = (w[1] >> 26) | ((w[4] >> 24) & 1u) << 6 | (w[4] >> 31) << 7;
-  s.S = s.code & 31u;
-  s.s = (s.code >> 5) & 3u;
-  s.e = s.code >> 7;
-  s.signs = (w[4] >> 25) & 7u;
-  s.M = (w[4] >> 28) & 3u;
-  s.ends = ((w[4] >> 30) & 1u) != 0;
+  s.S = (w[1] >> 26) & 31u;
+  s.s = (w[4] >> 24) & 3u;
+  s.e = (w[4] >> 26) & 1u;
+  s.code = s.S | s.s << 5 | s.e << 7;
+  s.signs = (w[4] >> 27) & 7u;
+  s.M = w[4] >> 30;
+  s.ends = (w[1] >> 31) != 0;
 }
 
 }  // namespace brick

@@ -1612,15 +1612,17 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
   __shared__ uint32_t box[kBkBoxWords + 4];  // counters (skewed), control words
   uint32_t* sh = box + kBkBoxWords;
   // (xrays / xnrays / xnpairs: used only by the DMF_EXP_F_REBUILD experiment build below)
-  // (dM, d1, d2) LDS byte strides of a pair, looked up by its record bits w4 >> 24 (bits 1-3
-  // step signs, 4-5 the major axis): one ds_read instead of ~17 selects per refill (F -1.3 %);
+  // F's stride table, indexed by a record's T = w4 >> 24 (dmf_brick.hpp pack20: the slab code's
+  // s and e, the step signs, the major axis M): (dM, d1, d2) the LDS byte strides of the pair's
+  // major and minor axes, and the byte offsets from L of the cells of L's slab the code adopts
+  // (low 16 bits, signed: L - d_e when s >= 1; high 16: L - d1 - d2 when s == 2; 0 = none).
+  // (dmf_brick.hpp slab_table_entry).  One ds_read per refill instead of ~25 VALU of selects;
   // written before the first part's barrier
-  __shared__ uint4 slut[128];
-  if (threadIdx.x < 128) {
-    const uint32_t c = threadIdx.x, sg = c >> 1, M = (c >> 4) & 3u;
-    const uint32_t sx = sg & 1u ? 0u - 4u * kBkSx : 4u * kBkSx, sy = sg & 2u ? 0u - 4u * kBkSy : 4u * kBkSy,
-                   sz = sg & 4u ? 0u - 4u : 4u;
-    slut[c] = make_uint4(M == 0 ? sx : (M == 1 ? sy : sz), M == 0 ? sy : sx, M == 2 ? sy : sz, 0u);
+  __shared__ uint4 slut[256];
+  if (threadIdx.x < 256) {
+    uint32_t e[4];
+    bk::slab_table_entry(threadIdx.x, 4u * kBkSx, 4u * kBkSy, 4u, e);
+    slut[threadIdx.x] = make_uint4(e[0], e[1], e[2], e[3]);
   }
   stats = stat_slot(stats);
   const int tid = threadIdx.x, l = tid & 63;
@@ -1699,16 +1701,17 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       r = (int)sd.S;
       // (the strides computed from the record bits in VALU instead measured slower: F 3.39 ->
       // 3.50 ms, profiles/r06f -- the table read's latency is not what the refill waits on)
-      const uint4 st3 = slut[cw >> 24 & 127u];
+      const uint4 st3 = slut[cw >> 24];
       dM = st3.x;
       d1 = st3.y;
       d2 = st3.z;
       // the pair's last cell: a hit when the ray ends there inside the grid, else a miss
       const uint32_t Lb = sd.last * 4u;
       atomicAdd((uint32_t*)(lds + Lb), sd.ends ? 0x10000u : 1u);
-      // the cells of L's slab before L (misses): L - d_e, and the slab's first cell L - d_1 - d_2
-      if (sd.s != 0) atomicAdd((uint32_t*)(lds + Lb - (sd.e ? d2 : d1)), 1u);
-      if (sd.s == 2) atomicAdd((uint32_t*)(lds + Lb - d1 - d2), 1u);
+      // the cells of L's slab before L (misses), at the table's offsets: L - d_e (s >= 1) and
+      // the slab's first cell L - d_1 - d_2 (s == 2)
+      if (st3.w != 0u) atomicAdd((uint32_t*)(lds + Lb + (uint32_t)(int32_t)(int16_t)(uint16_t)st3.w), 1u);
+      if (st3.w > 0xffffu) atomicAdd((uint32_t*)(lds + Lb + (uint32_t)((int32_t)st3.w >> 16)), 1u);
 #if defined(DMF_EXP_F_REBUILD)
       {
         // Cost proxy of a compact pair record (B stores <= 8 B, F rebuilds the
@@ -1821,10 +1824,10 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
         }
       }
       DMF_TACC(t_refill, tr0);
-      if (!any_act) {
-        if (__builtin_amdgcn_ballot_w64(fok) == 0) break;
-        continue;
-      }
+      // (no `continue` when no lane walks but records wait -- rare: every decoded pair had no
+      // whole slab -- the block below then adds nothing; one loop latch, so that the compiler
+      // keeps the walk state in place instead of copying it at every block's end)
+      if (!any_act && __builtin_amdgcn_ballot_w64(fok) == 0) break;
       DMF_T(tw0);
 #if defined(DMF_EXP_STATS)
       if (l == 0) ++nblocks;

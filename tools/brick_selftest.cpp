@@ -12,7 +12,8 @@
 //      exactly the pair's cells before its last cell, and R fits 7 bits; so does phase F's
 //      walk from the slab code (slab_code: S whole slabs, then L's slab before L derived from
 //      L, slab_walk_code), with S <= 31;
-//   5. the slab-code walk from the 20-byte record (pack20 -> unpack20, scaled state beta);
+//   5. the slab-code walk from the 20-byte record (pack20 -> unpack20, scaled state beta), and
+//      phase F's stride-table entry for it (slab_table_entry: strides and adopted cells);
 //   6. pass B's select-based counts_at_sel equals counts_at at the ray's crossing events;
 //   7. so does the double-arithmetic counts_at_f64 (also with its reciprocals 2 ulps and a
 //      relative 2^-22 / 2^-14 off);
@@ -164,6 +165,21 @@ static void restart_owned20(const QRay& r, const int32_t c[3], const int32_t cL[
   const int32_t stw[3] = {r.st[0] ? st[0] : 0, r.st[1] ? st[1] : 0, r.st[2] ? st[2] : 0};
   slab_walk_code((int)s.M, s.b1, s.b2, s.b12, s.aM, s.a1, s.a2, stw, p0, s.code, Lc,
                  [&](int x, int y, int z) { out.push_back({x, y, z}); });
+  // phase F adopts L's slab through its stride table (slab_table_entry at T = w[4] >> 24, in
+  // the LDS box's byte strides): the offsets must land on the cells slab_walk_code adopted
+  uint32_t te[4];
+  const int64_t bx = 4 * 1057, by = 4 * 33, bz = 4;
+  slab_table_entry(w[4] >> 24, (uint32_t)bx, (uint32_t)by, (uint32_t)bz, te);
+  auto lin = [&](int64_t x, int64_t y, int64_t z) { return x * bx + y * by + z * bz; };
+  const int64_t L = lin(Lc[0], Lc[1], Lc[2]);
+  const int64_t sb[3] = {bx, by, bz};
+  const int64_t o1 = (int16_t)(te[3] & 0xffffu), o2 = (int16_t)(te[3] >> 16);
+  const int64_t want1 = s.s >= 1 ? -st[s.e ? m2 : m1] * sb[s.e ? m2 : m1] : 0;
+  const int64_t want2 = s.s == 2 ? -st[m1] * sb[m1] - st[m2] * sb[m2] : 0;
+  const int64_t dM = (int32_t)te[0], d1 = (int32_t)te[1], d2 = (int32_t)te[2];
+  if (o1 != want1 || o2 != want2 || dM != st[s.M] * sb[s.M] || d1 != st[m1] * sb[m1] || d2 != st[m2] * sb[m2] ||
+      (L + o1 == L) != (s.s == 0))
+    out.push_back({-2, -2, -2});  // the table disagrees with the record's adoption
 }
 
 int main(int argc, char** argv) {
