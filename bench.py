@@ -765,6 +765,8 @@ def main():
             if st[7] > 0:  # diagnostic build (DMF_EXP_STATS): F wave blocks, lanes active, refills
                 diagnostics.update({"f_blocks": int(st[7]) // args.steps, "f_refills": int(st[9]) // args.steps,
                                     "f_lane_util": float(st[8]) / max(64.0 * float(st[7]), 1.0),
+                                    "b_replay_iters": int(st[18]) // args.steps,
+                                    "b_lane_util": float(st[19]) / max(64.0 * float(st[18]), 1.0),
                                     "f_wave_cycles": {"refill": int(st[10]) // args.steps, "walk": int(st[11]) // args.steps,
                                                       "flush": int(st[12]) // args.steps,
                                                       "part_barrier": int(st[15]) // args.steps,

@@ -219,6 +219,7 @@ __host__ __device__ inline void counts_at_sel(const QRay& r, int a, int32_t k, i
 // runs the counts with inv perturbed by +-2 ulps and by relative errors of +-2^-22 and +-2^-14.
 struct QRayF64 {
   double adq[3], h[3], inv[3];  // |dq|, first-crossing numerator h0, ~1 / (2Q |dq|) (0: non-moving)
+  double hx[3][3];              // [A][b], b != A: -(h_b |dq_A|) - (b > A), count_at's tie rule folded in
 };
 __host__ __device__ inline void qray_f64(const QRay& r, QRayF64& f) {
 #pragma unroll
@@ -231,6 +232,10 @@ __host__ __device__ inline void qray_f64(const QRay& r, QRayF64& f) {
     f.inv[a] = r.adq[a] ? 1.0 / (2.0 * (double)kQ * (double)r.adq[a]) : 0.0;
 #endif
   }
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) f.hx[a][b] = -(f.h[b] * f.adq[a]) - (b > a ? 1.0 : 0.0);  // exact: < 2^53
 }
 template <int A>
 __host__ __device__ inline void counts_at_f64(const QRay& r, const QRayF64& f, int32_t k, int32_t c[3]) {
@@ -242,11 +247,11 @@ __host__ __device__ inline void counts_at_f64(const QRay& r, const QRayF64& f, i
       c[b] = k + 1;
       continue;
     }
-    const double X = fma(Ha, f.adq[b], -(f.h[b] * f.adq[A])) - (b > A ? 1.0 : 0.0);
-    double q = floor(X * f.inv[A]);
+    const double X = fma(Ha, f.adq[b], f.hx[A][b]);
+    const double q = floor(X * f.inv[A]);
     const double rm = fma(-q, Y, X);
-    q += rm < 0.0 ? -1.0 : (rm >= Y ? 1.0 : 0.0);
-    const int32_t cq = (int32_t)q + 1;
+    // floor(X / Y) + 1 = q + 1, corrected by the exact remainder (one of the two terms at most)
+    const int32_t cq = (int32_t)q + (rm < 0.0 ? 0 : 1) + (rm >= Y ? 1 : 0);
     c[b] = (r.st[b] == 0 || X < 0.0) ? 0 : (cq < r.n[b] ? cq : r.n[b]);
   }
 }

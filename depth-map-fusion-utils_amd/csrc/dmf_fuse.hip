@@ -1194,7 +1194,8 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
                                                          const uint32_t* __restrict__ wg_list, int wgl_stride,
                                                          uint4* __restrict__ pa, void* __restrict__ pbv,
                                                          unsigned long long* __restrict__ ctl,
-                                                         uint32_t* __restrict__ fault, int inject) {
+                                                         uint32_t* __restrict__ fault, int inject,
+                                                         unsigned long long* __restrict__ stats) {
   uint2* const pb = (uint2*)pbv;
   uint32_t* const pw = (uint32_t*)pbv;
   extern __shared__ uint32_t hist[];
@@ -1228,6 +1229,9 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
   }
   __syncthreads();
   uint32_t over = 0;  // one past the lane's largest slot (the layout check; 0 = no pair)
+#if defined(DMF_EXP_STATS)
+  unsigned long long b_iters = 0, b_lanes = 0;
+#endif
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int q0 = (int)(blockIdx.x - (unsigned)pz * (unsigned)wg_pose) * span;
   const int64_t pk0 = (int64_t)pz * packets_pose + q0, pk1 = (int64_t)pz * packets_pose + min(packets_pose, q0 + span);
@@ -1367,6 +1371,15 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
 #endif
     uint32_t slot = 0;
     bk_replay(bg, R, path, [&](int b, int a, int bx, int by, int bz) {
+#if defined(DMF_EXP_STATS)
+      {  // diagnostic build: the replay loop's wave iterations and the lanes active in them
+        const uint64_t am = __builtin_amdgcn_ballot_w64(true);
+        if (l == __builtin_ctzll(am)) {
+          ++b_iters;
+          b_lanes += (unsigned long long)__builtin_popcountll(am);
+        }
+      }
+#endif
       if (a >= 0) {
         int32_t c[3];
         counts(a, bx, by, bz, c);
@@ -1382,6 +1395,13 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
     });
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }
+#if defined(DMF_EXP_STATS)
+  if (stats && b_iters) {
+    unsigned long long* const sl = stat_slot(stats);
+    atomicAdd(&sl[18], b_iters);
+    atomicAdd(&sl[19], b_lanes);
+  }
+#endif
   // layout check: the slots taken in each touched brick must be pass A's count for it
 #if DMF_B_GUARD != 0
   __syncthreads();
@@ -1497,6 +1517,9 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       atomicAdd(&box[ca.w >> 16], (cb.y >> 26) & 1u ? 0x10000u : 1u);
     };
     bool more = true;
+#if defined(DMF_EXP_F_XVALU)
+    uint32_t xv = 0;
+#endif
     // lanes in `need` take the next pair indices (one LDS allocation) and load their records
     auto prefetch = [&](uint64_t need) {
       const uint32_t nn = (uint32_t)__builtin_popcountll(need);
@@ -1750,6 +1773,9 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
 #endif
     };
     bool more = true;
+#if defined(DMF_EXP_F_XVALU)
+    uint32_t xv = 0;
+#endif
     // lanes in `need` take the next pair indices (one LDS counter atomic, issued by alloc()
     // before the refill's decode so that its return latency hides behind it) and load their
     // records (fetch())
@@ -1846,7 +1872,16 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
           atomicAdd((uint32_t*)(lds + cur), 1u);
           if (c1 || c2) atomicAdd((uint32_t*)(lds + p1), 1u);
           if (c1 && c2) atomicAdd((uint32_t*)(lds + p2), 1u);
+#if defined(DMF_EXP_F_XLDS)  // diagnostic (wrong counts): every walk atomic twice
+          atomicAdd((uint32_t*)(lds + cur), 1u);
+          if (c1 || c2) atomicAdd((uint32_t*)(lds + p1), 1u);
+          if (c1 && c2) atomicAdd((uint32_t*)(lds + p2), 1u);
+#endif
         }
+#if defined(DMF_EXP_F_XVALU)  // diagnostic: independent VALU per slab, kept by a never-true test
+        xv = ((xv ^ cur) + b1) ^ (b2 << 1);
+        xv = ((xv ^ b12) + p1) ^ (p2 << 2);
+#endif
         cur = p2 + dM;
         b1 += c1 ? K1mM : K1;
         b2 += c2 ? K2mM : K2;
@@ -1855,6 +1890,9 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
       r -= UNROLL;
       DMF_TACC(t_walk, tw0);
     }
+#if defined(DMF_EXP_F_XVALU)
+    if (xv == 0x9e3779b9u + n) atomicAdd(&hits[0], 0);
+#endif
     DMF_T(tf0);
     __syncthreads();
     if constexpr (bk::kLog != 5) {
@@ -2418,13 +2456,13 @@ static int fuse_bricks(dmf_volume* v, const CamP& cp, const Geom& g, const uint1
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
                            (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb, b.ctl,
-                           v->d_fault, (int)std::min<int64_t>(v->knob[DMF_KNOB_FAULT_INJECT], 1 << 20));
+                           v->d_fault, (int)std::min<int64_t>(v->knob[DMF_KNOB_FAULT_INJECT], 1 << 20), st);
       else
         hipLaunchKernelGGL(k_bk_pairs<false>, dim3(nwg), dim3(pl.ab_threads), pl.hist_bytes, sj, (int)pl.ppose,
                            pl.wg_pose, pl.span, bg, (const ulonglong2*)b.rays, (const uint64_t*)b.paths, (const uint32_t*)b.off,
                            (const uint32_t*)b.pose_base, (const uint32_t*)b.wgb, (const uint32_t*)b.bt, (int)j,
                            (const uint32_t*)b.wgl, pl.wgl_stride, b.pra, b.prb, b.ctl,
-                           v->d_fault, (int)std::min<int64_t>(v->knob[DMF_KNOB_FAULT_INJECT], 1 << 20));
+                           v->d_fault, (int)std::min<int64_t>(v->knob[DMF_KNOB_FAULT_INJECT], 1 << 20), st);
       DMF_LAUNCH_CHECK();
       // the call's phase F begins (not while capturing: the record would become a graph node
       // and the caller's event would never be re-recorded by the graph's launches)
