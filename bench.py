@@ -51,6 +51,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # VALU issue peak: 256 CUs x 4 SIMD-32 x one wave64 VALU instruction per 2 cycles at 2.4 GHz
 # (MI355X_MICROARCH.md "Wave scheduling"), in wave-instructions/s
 VALU_PEAK_WIPS = 256 * 4 * 2.4e9 / 2
+# LDS-add peak: 256 CUs x one ds_add_u32 wave-instruction per 4 cycles (address + data moved to
+# the LDS at 2 cycles per dword per wave-instruction, MI355X_MICROARCH.md §LDS) at 2.4 GHz
+LDS_ADD_PEAK_WIPS = 256 * 2.4e9 / 4
 BYTES_PER_UPDATE = 4   # int16 read + int16 write per cell update
 BYTES_PER_DEPTH = 2    # uint16 depth read per pixel
 
@@ -881,12 +884,18 @@ def attach_pmc(result, pmc):
                                    "mode (child run): passes A and B run beside the previous call's F when "
                                    "pipelined, so their averages include the stretch")
     fvalu = pmc_per_dispatch(pmc, rf.get("f_kernel") or "", "SQ_INSTS_VALU") if rf.get("f_kernel") else None
+    flds = pmc_per_dispatch(pmc, rf.get("f_kernel") or "", "SQ_INSTS_LDS") if rf.get("f_kernel") else None
+    fconf = pmc_per_dispatch(pmc, rf.get("f_kernel") or "", "SQ_LDS_BANK_CONFLICT") if rf.get("f_kernel") else None
     rf["companion"] = {
         "bound": "valu-issue", "achieved": valu / (rf["step_ms"] * 1e-3), "peak": VALU_PEAK_WIPS,
         "unit": "wave-instr/s", "frac": valu / (rf["step_ms"] * 1e-3) / VALU_PEAK_WIPS,
         "valu_per_call": valu, "lane_slots_per_update": valu * 64.0 / max(rf["updates_per_launch"], 1.0),
         "f_valu_per_launch": fvalu,
         "f_frac": (fvalu / (rf["f_kernel_ms"] * 1e-3) / VALU_PEAK_WIPS) if fvalu and rf.get("f_kernel_ms") else None,
+        # phase F is bound by its LDS adds as much as by its VALU (at the margin one
+        # LDS add costs about 5.8 VALU): its LDS instructions against one ds_add per 4 cycles per CU
+        "f_lds_per_launch": flds, "f_lds_bank_conflict_cycles": fconf,
+        "f_lds_frac": (flds / (rf["f_kernel_ms"] * 1e-3) / LDS_ADD_PEAK_WIPS) if flds and rf.get("f_kernel_ms") else None,
         "basis": "what binds the pipeline: SQ_INSTS_VALU of every fusion kernel per call (PMC child) over the step "
                  "interval, vs 1024 SIMD-32 x one wave64 VALU instruction per 2 cycles at 2.4 GHz"}
     rf["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes of this configuration (child runs after "
