@@ -1652,6 +1652,9 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse_s(Geom g, BkGeom bg, con
   // pass B's layout check failed for this batch (dmf_fuse_status reports it): its pair
   // records are not all in place, so none is walked
   if (ctl[3] != 0) return;
+#if defined(DMF_EXP_F_PRIO)  // experiment builds: phase F's waves at a raised issue priority
+  __builtin_amdgcn_s_setprio(DMF_EXP_F_PRIO);
+#endif
 #if defined(DMF_EXP_F_REBUILD)
   xnpairs = (uint32_t)ctl[0];  // the batch's pairs (the stand-in ray ids spread over them)
   uint32_t sink = 0;           // the proxy's result
