@@ -2137,6 +2137,9 @@ static int bk_plan(const dmf_volume* v, const CamP& cp, const Geom& g, int P, Bk
   const uint64_t one_pose = (uint64_t)rays_pose * (uint64_t)pl.max_pairs_ray;  // pairs of one pose, at most
   if (one_pose > (uint64_t)UINT32_MAX) return fail(DMF_ERR_RANGE, "one frame exceeds the 32-bit pair offsets");
   pl.ab_threads = pl.bg.nbricks > kBkBigHist ? kBkPassThreadsBig : kBkPassThreads;
+#if defined(DMF_EXP_AB_THREADS)  // experiment builds: passes A/B workgroup size below kBkBigHist bricks
+  if (pl.bg.nbricks <= kBkBigHist) pl.ab_threads = DMF_EXP_AB_THREADS;
+#endif
   // packets per workgroup of passes A/B (>= 16 per wave; the histogram's zero + flush
   // amortised over >= 64 packets per 1k bricks).  Up to 512 bricks (grids <= 256^3) the
   // histogram is small enough for 8 per wave: config 2 fusion 2.05 -> 2.02 ms, while 384^3
