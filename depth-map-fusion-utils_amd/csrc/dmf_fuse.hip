@@ -1517,9 +1517,6 @@ __global__ __launch_bounds__(kBkThreads) void k_bk_fuse(Geom g, BkGeom bg, const
       atomicAdd(&box[ca.w >> 16], (cb.y >> 26) & 1u ? 0x10000u : 1u);
     };
     bool more = true;
-#if defined(DMF_EXP_F_XVALU)
-    uint32_t xv = 0;
-#endif
     // lanes in `need` take the next pair indices (one LDS allocation) and load their records
     auto prefetch = [&](uint64_t need) {
       const uint32_t nn = (uint32_t)__builtin_popcountll(need);
