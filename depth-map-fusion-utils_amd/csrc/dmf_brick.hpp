@@ -368,19 +368,19 @@ __host__ __device__ inline int32_t pinned(int32_t x) {
 #endif
   return x;
 }
-__host__ __device__ inline int coarse_next_at(const QRay& r, int b0, int b1, int b2) {
+// coarse_next_at from the three next-boundary crossing indices k_a themselves (pass B carries
+// them per axis: k_a grows by kB per brick step along a)
+__host__ __device__ inline int coarse_next_k(const QRay& r, int32_t k0, int32_t k1, int32_t k2) {
   int best = -1;
   int64_t Hb = 0;
   int32_t db = 0;
-  const int bc[3] = {b0, b1, b2};
+  const int32_t ks[3] = {k0, k1, k2};
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     const int32_t st = pinned(r.st[a]);
     if (st == 0) continue;
-    const int32_t cs = pinned(r.cs[a]), da = pinned(r.adq[a]);
-    const int32_t nb = bc[a] + st;
-    const int32_t k = st > 0 ? nb * kB - cs - 1 : cs - nb * kB - kB;  // (nb may be -1: past the grid)
-    const int64_t H = (int64_t)pinned(r.h0[a]) + 2 * kQ * (int64_t)k;
+    const int32_t da = pinned(r.adq[a]);
+    const int64_t H = (int64_t)pinned(r.h0[a]) + 2 * kQ * (int64_t)ks[a];
     // ev_before(r, a, H, best, Hb): H |dq_best| < Hb |dq_a| (a > best: ties keep best)
     if (best < 0 || H * (int64_t)db < Hb * (int64_t)da) {
       best = a;
@@ -389,6 +389,16 @@ __host__ __device__ inline int coarse_next_at(const QRay& r, int b0, int b1, int
     }
   }
   return best;
+}
+// the fine-crossing index of the boundary into brick coordinate b + st along axis a (moving up,
+// cell nb*kB is reached by crossing nb*kB - cs - 1; moving down, cell nb*kB + kB - 1 by crossing
+// cs - nb*kB - kB; nb may be -1: past the grid)
+__host__ __device__ inline int32_t next_boundary_k(const QRay& r, int a, int b) {
+  const int32_t st = r.st[a], nb = b + st;
+  return st > 0 ? nb * kB - r.cs[a] - 1 : r.cs[a] - nb * kB - kB;
+}
+__host__ __device__ inline int coarse_next_at(const QRay& r, int b0, int b1, int b2) {
+  return coarse_next_k(r, next_boundary_k(r, 0, b0), next_boundary_k(r, 1, b1), next_boundary_k(r, 2, b2));
 }
 
 // The coarse walk's crossing axes, 2 bits per brick boundary (step t at bits 2t, 2t + 1), for

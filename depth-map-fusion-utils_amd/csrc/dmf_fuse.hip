@@ -548,26 +548,6 @@ __device__ inline void bk_coarse(const BkGeom& bg, const bk::QRay& R, F&& f) {
   }
 }
 
-// Pass B's coarse walk: the brick sequence from the crossing axes pass A recorded (path, see
-// dmf_brick.hpp path_put), calling f exactly as bk_coarse does; past the path's kPathSteps
-// boundaries each next axis is recomputed from the current brick (coarse_next_at: no 64-bit
-// walk state lives across the replay, which held pass B at 116 VGPRs).
-template <class F>
-__device__ inline void bk_replay(const BkGeom& bg, const bk::QRay& R, uint64_t path, F&& f) {
-  const int total = bk::coarse_total(R);
-  int b0 = R.cs[0] >> bk::kLog, b1 = R.cs[1] >> bk::kLog, b2 = R.cs[2] >> bk::kLog;
-  f(bk_index(bg, b0, b1, b2), -1, b0, b1, b2);
-  for (int t = 0; t < total; ++t) {
-    int a;
-    if (t < bk::kPathSteps) a = bk::path_axis(path, t);
-    else a = bk::coarse_next_at(R, b0, b1, b2);  // (branch: skipped by the waves whose lanes all replay)
-    b0 += a == 0 ? R.st[0] : 0;
-    b1 += a == 1 ? R.st[1] : 0;
-    b2 += a == 2 ? R.st[2] : 0;
-    f(bk_index(bg, b0, b1, b2), a, b0, b1, b2);
-  }
-}
-
 // Wave-aggregated LDS histogram add: the lanes of a packet walk near-parallel rays and
 // name the same brick at the same coarse step, so one atomic per distinct brick among
 // the active lanes replaces a same-address atomic per lane (which the LDS serialises).
@@ -1330,13 +1310,12 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
     };
     // the end cell (brick-local): the last cell of the ray's last pair
     const uint32_t endc = bk_lds_word((uint32_t)R.ce[0] & m5, (uint32_t)R.ce[1] & m5, (uint32_t)R.ce[2] & m5);
-    // fine-crossing index of the boundary crossed (axis a) to enter brick coordinate nb:
-    // moving up, cell nb*32 is reached by crossing nb*32 - cs - 1; moving down, cell
-    // nb*32 + 31 by crossing cs - nb*32 - 32.  (Derived from the brick coordinate, not
-    // carried per axis: per-axis counters indexed by a became a scratch array.)
-    auto boundary_k = [&](int ax, int nb) {
-      return R.st[ax] > 0 ? (nb << bk::kLog) - R.cs[ax] - 1 : R.cs[ax] - (nb << bk::kLog) - bk::kB;
-    };
+    // per axis, the fine-crossing index of the boundary into the next brick along it
+    // (dmf_brick.hpp next_boundary_k): a boundary event on axis a takes P_a, which then grows by
+    // kB -- selects, not per-axis branches: the compiler merged branch-wise updates into a
+    // stack array indexed by the axis (scratch, as an axis-indexed array in round 4)
+    const int cb0 = R.cs[0] >> bk::kLog, cb1 = R.cs[1] >> bk::kLog, cb2 = R.cs[2] >> bk::kLog;
+    int32_t P0 = bk::next_boundary_k(R, 0, cb0), P1 = bk::next_boundary_k(R, 1, cb1), P2 = bk::next_boundary_k(R, 2, cb2);
     const int32_t c00[3] = {0, 0, 0};
     uint4 cur = entry(c00);
     int32_t idx = 0;                    // crossings before the current pair's first cell
@@ -1349,28 +1328,36 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
       const int32_t cin[3] = {ci0, ci1, ci2}, cL[3] = {L0, L1, L2};
       return bk::slab_code(M, sb1, sb2, sb12, KM, Km1, Km2, cin, cL);
     };
-    // crossing counts per axis at the boundary event of axis a into brick coordinate (bx, by, bz)
+    // crossing counts per axis at the boundary event of axis a (fine crossing P_a)
     // the boundary counts in double arithmetic (dmf_brick.hpp counts_at_f64, exact by fma;
     // B 1.41 -> 1.37 ms): per ray three reciprocals, per event two fma
     // quotients instead of 64-bit products and float quotient estimates.  Constant axis in each
     // call: no dynamically indexed (scratch) arrays.
 #if defined(DMF_EXP_B_INT_COUNTS)  // experiment builds: the integer counts_at
-    auto counts = [&](int a, int bx, int by, int bz, int32_t c[3]) {
-      if (a == 0) bk::counts_at(R, 0, boundary_k(0, bx), c);
-      else if (a == 1) bk::counts_at(R, 1, boundary_k(1, by), c);
-      else bk::counts_at(R, 2, boundary_k(2, bz), c);
+    auto counts = [&](int a, int32_t k, int32_t c[3]) {
+      if (a == 0) bk::counts_at(R, 0, k, c);
+      else if (a == 1) bk::counts_at(R, 1, k, c);
+      else bk::counts_at(R, 2, k, c);
     };
 #else
     bk::QRayF64 F64;
     bk::qray_f64(R, F64);
-    auto counts = [&](int a, int bx, int by, int bz, int32_t c[3]) {
-      if (a == 0) bk::counts_at_f64<0>(R, F64, boundary_k(0, bx), c);
-      else if (a == 1) bk::counts_at_f64<1>(R, F64, boundary_k(1, by), c);
-      else bk::counts_at_f64<2>(R, F64, boundary_k(2, bz), c);
+    auto counts = [&](int a, int32_t k, int32_t c[3]) {
+      if (a == 0) bk::counts_at_f64<0>(R, F64, k, c);
+      else if (a == 1) bk::counts_at_f64<1>(R, F64, k, c);
+      else bk::counts_at_f64<2>(R, F64, k, c);
     };
 #endif
-    uint32_t slot = 0;
-    bk_replay(bg, R, path, [&](int b, int a, int bx, int by, int bz) {
+    // the replay of the brick sequence (bk_coarse's order): the crossing axes pass A recorded
+    // (path), past its kPathSteps boundaries the stateless next axis from the P's; the brick
+    // index moves by a per-axis step
+    const int total = bk::coarse_total(R);
+    const int32_t nb12 = bg.nb[1] * bg.nb[2];
+    const int32_t D0 = bk::mul24(R.st[0], nb12), D1 = bk::mul24(R.st[1], bg.nb[2]), D2 = R.st[2];
+    int b = bk_index(bg, cb0, cb1, cb2);
+    uint32_t slot = atomicAdd(&hist[b], 1u + extra);
+    extra = 0;
+    for (int t = 0; t < total; ++t) {
 #if defined(DMF_EXP_STATS)
       {  // diagnostic build: the replay loop's wave iterations and the lanes active in them
         const uint64_t am = __builtin_amdgcn_ballot_w64(true);
@@ -1380,19 +1367,25 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
         }
       }
 #endif
-      if (a >= 0) {
-        int32_t c[3];
-        counts(a, bx, by, bz, c);
-        put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
-        cur = entry(c);
-        idx = c[0] + c[1] + c[2];
-        ci0 = c[0];
-        ci1 = c[1];
-        ci2 = c[2];
-      }
+      int a;
+      if (t < bk::kPathSteps) a = bk::path_axis(path, t);
+      else a = bk::coarse_next_k(R, P0, P1, P2);  // (branch: skipped by the waves whose lanes all replay)
+      b += a == 0 ? D0 : (a == 1 ? D1 : D2);
+      const int32_t k = a == 0 ? P0 : (a == 1 ? P1 : P2);
+      P0 += a == 0 ? bk::kB : 0;
+      P1 += a == 1 ? bk::kB : 0;
+      P2 += a == 2 ? bk::kB : 0;
+      int32_t c[3];
+      counts(a, k, c);
+      put(slot, cur, last_before(c, a), count_field(c[0] - (a == 0), c[1] - (a == 1), c[2] - (a == 2)), false);
+      cur = entry(c);
+      idx = c[0] + c[1] + c[2];
+      ci0 = c[0];
+      ci1 = c[1];
+      ci2 = c[2];
       slot = atomicAdd(&hist[b], 1u + extra);
       extra = 0;
-    });
+    }
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }
 #if defined(DMF_EXP_STATS)

@@ -19,7 +19,8 @@
 //      relative 2^-22 / 2^-14 off);
 //   8. pass B's replay of pass A's recorded crossing path (path_put / path_axis, the first
 //      kPathSteps boundaries; coarse_total = the walk's step count) lists the same bricks,
-//      and so does its replay past them by the stateless coarse_next_at (also over whole rays).
+//      and so does its replay past them by the stateless coarse_next_at (also over whole rays),
+//      and by the incremental per-axis boundary indices pass B carries (check 8c).
 // Build: make -C depth-map-fusion-utils_amd build/brick_selftest ; run: <exe> [rays] [seed]
 #include <cmath>
 #include <cstdio>
@@ -300,6 +301,30 @@ int main(int argc, char** argv) {
         if (w2.total > kPathSteps && from == 0) ++long_replayed;
       }
       if (!okp) { printf("ray %ld: stateless replay differs (%d boundaries)\n", i, w2.total); ++bad; continue; }
+      // 8c. pass B's replay as k_bk_pairs runs it: per axis the crossing index of the boundary
+      //     into the next brick (next_boundary_k, +kB per step along it), the next axis past
+      //     the path from those (coarse_next_k), the brick index moved by a per-axis step; the
+      //     bricks and every event's crossing index equal the coordinate-based ones
+      {
+        std::vector<int> rb;
+        const int c0 = r.cs[0] >> kLog, c1 = r.cs[1] >> kLog, c2 = r.cs[2] >> kLog;
+        int32_t P[3] = {next_boundary_k(r, 0, c0), next_boundary_k(r, 1, c1), next_boundary_k(r, 2, c2)};
+        const int D[3] = {r.st[0] * nby * nbz, r.st[1] * nbz, r.st[2]};
+        int b = (c0 * nby + c1) * nbz + c2, pc[3] = {c0, c1, c2};
+        rb.push_back(b);
+        for (int s = 0; s < w2.total && okp; ++s) {
+          const int a = s < kPathSteps ? path_axis(path, s) : coarse_next_k(r, P[0], P[1], P[2]);
+          b += D[a];
+          const int32_t k = P[a];
+          P[a] += kB;
+          pc[a] += r.st[a];
+          const int32_t kc = r.st[a] > 0 ? (pc[a] << kLog) - r.cs[a] - 1 : r.cs[a] - (pc[a] << kLog) - kB;
+          okp = k == kc;
+          rb.push_back(b);
+        }
+        okp = okp && rb == cb;
+      }
+      if (!okp) { printf("ray %ld: incremental replay differs (%d boundaries)\n", i, w2.total); ++bad; continue; }
     }
     // 6. pass B's select-based counts_at_sel equals counts_at at every crossing event
     //    (every k for short axes, 97 spread k's for long ones)
