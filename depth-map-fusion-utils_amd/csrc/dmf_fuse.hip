@@ -1209,6 +1209,11 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
   }
   __syncthreads();
   uint32_t over = 0;  // one past the lane's largest slot (the layout check; 0 = no pair)
+#if defined(DMF_EXP_B_NOSLOT)
+  uint32_t dslot = blockIdx.x * blockDim.x + threadIdx.x, dmask = 1u;
+  while (dmask * 2u <= total && dmask < 0x80000000u) dmask *= 2u;
+  dmask -= 1u;
+#endif
 #if defined(DMF_EXP_STATS)
   unsigned long long b_iters = 0, b_lanes = 0;
 #endif
@@ -1355,7 +1360,13 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
     const int32_t nb12 = bg.nb[1] * bg.nb[2];
     const int32_t D0 = bk::mul24(R.st[0], nb12), D1 = bk::mul24(R.st[1], bg.nb[2]), D2 = R.st[2];
     int b = bk_index(bg, cb0, cb1, cb2);
-    uint32_t slot = atomicAdd(&hist[b], 1u + extra);
+#if defined(DMF_EXP_B_NOSLOT)  // diagnostic (wrong layout: the check fails, F skips): no slot atomics,
+    // each lane's stores to distinct records, lanes of a wave adjacent (an ideal store stream)
+#define DMF_B_SLOT(b) ((dslot += gridDim.x * blockDim.x) & dmask)
+#else
+#define DMF_B_SLOT(b) atomicAdd(&hist[b], 1u + extra)
+#endif
+    uint32_t slot = DMF_B_SLOT(b);
     extra = 0;
     for (int t = 0; t < total; ++t) {
 #if defined(DMF_EXP_STATS)
@@ -1383,9 +1394,10 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
       ci0 = c[0];
       ci1 = c[1];
       ci2 = c[2];
-      slot = atomicAdd(&hist[b], 1u + extra);
+      slot = DMF_B_SLOT(b);
       extra = 0;
     }
+#undef DMF_B_SLOT
     put(slot, cur, endc, count_field(R.n[0], R.n[1], R.n[2]), R.end_inside);
   }
 #if defined(DMF_EXP_STATS)
@@ -1415,11 +1427,15 @@ __global__ __launch_bounds__(kBkPassThreadsBig) DMF_B_OCC void k_bk_pairs(int pa
                off[i], pbz[i], wb[i], e >> 16, total);
 #endif
     }
+#if defined(DMF_EXP_B_NOSLOT)  // (the diagnostic's layout is wrong: one flag per workgroup, F skips)
+    if (threadIdx.x == 0) atomicOr(&ctl[3], 1ull);
+#else
     if (bad) {
       atomicAdd(&fault[0], bad);
       atomicAdd(&fault[1], bad);
       atomicOr(&ctl[3], 1ull);  // phase F skips this batch: its records are not all in place
     }
+#endif
   }
 #endif
 }
