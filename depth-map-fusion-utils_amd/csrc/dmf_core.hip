@@ -663,6 +663,7 @@ dmf::Geom dmf_volume::geom() const {
     g.vhi[a] = hi;
   }
   fbin_setup(g);
+  jump_margin_setup(g);
   return g;
 }
 

@@ -32,7 +32,20 @@ struct Geom {
   // unless that float estimate lies within feps of a cell boundary (fbin_setup)
   float fmn[3], finv[3], feps[3];
   int fbin;       // 1: the float estimate is usable on every axis
+  // reverse march: the distance by which an empty cube's exit face is moved toward the sample
+  // before a jump is computed from it, 32 * 2^-24 * max(|min|, |max|) per axis -- more than
+  // the float rounding of the face, of the sample coordinates and of the bins together, so a
+  // jump target computed from the moved face lies inside the cube without evaluating it
+  // (jump_margin_setup)
+  float jmarg[3];
 };
+
+inline void jump_margin_setup(Geom& g) {
+  for (int a = 0; a < 3; ++a) {
+    const double b = std::fmax(std::fabs(g.mn[a]), std::fabs(g.mx[a]));
+    g.jmarg[a] = (float)(32.0 * 0x1p-24 * b) + 1e-30f;
+  }
+}
 
 // Error bound of the float estimate qf = RN(RN(x - fmn) * finv) of Q = (x - mn) / dl and of
 // the double getVoxel value Qd (bin_axis) for |Q| <= n + 2, in cells: with

@@ -29,6 +29,20 @@ namespace dmf {
 #define DMF_EXP_REV_WAVES 7
 #endif
 #define DMF_REV_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_REV_WAVES)))
+// The queue marches' empty-space jumps: 0 (default) = the target is computed from the cube's
+// faces moved in by Geom::jmarg and needs no check (round 6: 5.19 -> 4.77 ms per 128 poses,
+// samples 937M -> 649M, DESIGN.md §5.5, profiles/r06y); 1 = the landing sample is evaluated and
+// checked against the cube before the jump is taken (experiment builds)
+#ifndef DMF_REV_VERIFY_JUMPS
+#define DMF_REV_VERIFY_JUMPS 0
+#endif
+// The forward marches' jumps: 0 (default) = the line's point at the landing is checked against
+// the cube shrunk by twice the rounding margin, and the entry jump's target is taken as computed
+// (round 6: 6.16 -> 5.51 ms per 128 poses, samples 1.10G -> 0.77G, DESIGN.md §5.6,
+// profiles/r06z); 1 = the landing sample is evaluated and checked (experiment builds)
+#ifndef DMF_FWD_VERIFY_JUMPS
+#define DMF_FWD_VERIFY_JUMPS 0
+#endif
 #if defined(DMF_EXP_FWD_WAVES)
 #define DMF_FWD_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_FWD_WAVES)))
 #else
@@ -285,6 +299,36 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   const uint32_t bl = ((uint32_t)ba * (uint32_t)vd.nb[1] + (uint32_t)bb) * (uint32_t)vd.nb[2] + (uint32_t)bc;
   if (bl != L.known_full) {
     const int d = vd.bdist[bl];
+#if !DMF_REV_VERIFY_JUMPS
+    if (d > 0) {
+      // the jump target from the cube's exit faces moved toward the sample by g.jmarg: no
+      // sample of the jump is evaluated here; the target j is the next one marched, and the
+      // samples s+1 .. j-1 lie inside the empty cube (the moved face is
+      // farther inside than every rounding of the face, the samples and their bins, so sample
+      // j is inside the cube; the samples before it follow by monotonicity)
+      const int R = d - 1;  // bricks within R of this one are empty
+      const int bx[3] = {ba, bb, bc};
+      float fdmax = 3.0e38f;
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax) {
+        if (L.v[ax] == 0.0f) continue;
+        const int cf = L.v[ax] > 0.0f ? min((bx[ax] + R + 1) << vd.bsh, g.n[ax]) : max(bx[ax] - R, 0) << vd.bsh;
+        const float face = (float)(g.mn[ax] + (double)cf * g.dl[ax]);
+        const float fin = L.v[ax] > 0.0f ? face - g.jmarg[ax] : face + g.jmarg[ax];
+        fdmax = fminf(fdmax, (fin - L.cen[ax]) * L.rv[ax]);
+      }
+      const float jf = floorf(fdmax) - (float)depth0 - 2.0f;
+      if (jf > (float)(L.s + 1) && jf < (float)max_steps && jf < 4194304.0f) {
+        DMF_RS(4, 1);
+        DMF_RS(5, 1);
+        DMF_RS(6, (int)jf - L.s);
+        L.s = (int)jf;
+        return 0;
+      }
+    } else {
+      DMF_RS(12, 1);
+    }
+#else
     if (d > 0) {
       const int R = d - 1;  // bricks within R of this one are empty
       const int bx[3] = {ba, bb, bc};
@@ -319,6 +363,7 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
     } else {
       DMF_RS(12, 1);
     }
+#endif
     L.known_full = bl;  // occupied brick, or the jump failed: step through it
   }
   DMF_RS(3, 1);
@@ -1007,6 +1052,7 @@ __device__ inline void fwd_ray(const Geom& g, const DevVol& vd, const CamP& cam,
           kj = min(kj, last_k);
           if (kj > k) {
             const int zj = zstart + kj * zdelta;
+#if DMF_FWD_VERIFY_JUMPS
             float qc[3], q[3];
             project(cam, r, c, zj, qc);
             xform(m, qc[0], qc[1], qc[2], q);
@@ -1015,6 +1061,12 @@ __device__ inline void fwd_ray(const Geom& g, const DevVol& vd, const CamP& cam,
               k = kj;
               zd = zj;
             }
+#else
+            // zj is a whole step before the line enters the volume grown by the margin, so every
+            // sample up to it is outside the volume: no sample is evaluated to check it
+            k = kj;
+            zd = zj;
+#endif
           }
         }
         continue;
@@ -1051,17 +1103,28 @@ __device__ inline void fwd_ray(const Geom& g, const DevVol& vd, const CamP& cam,
         int kj = min((int)floorf((zexit - (float)zstart) / (float)zdelta) - 1, last_k);
         if (kj > k + 1) {
           const int zj = zstart + kj * zdelta;
+          bool ok = true;
+#if DMF_FWD_VERIFY_JUMPS
           float qc[3], q[3];
           project(cam, r, c, zj, qc);
           xform(m, qc[0], qc[1], qc[2], q);
           ++samples;
-          bool ok = true;
 #pragma unroll
           for (int ax = 0; ax < 3; ++ax) {
             const double dm = margin(ax, (double)zj);
             ok = ok && (double)w[ax] >= lo[ax] + dm && (double)w[ax] <= hi[ax] - dm && (double)q[ax] >= lo[ax] + dm &&
                  (double)q[ax] <= hi[ax] - dm;
           }
+#else
+          // sample j is not evaluated: the line's point at zj inside the cube shrunk by 2 delta
+          // puts sample j inside it shrunk by delta (its rounding is within eps of the line)
+#pragma unroll
+          for (int ax = 0; ax < 3; ++ax) {
+            const double dm = margin(ax, (double)zj), lq = (double)m[4 * ax + 3] + (double)zj * dir[ax];
+            ok = ok && (double)w[ax] >= lo[ax] + dm && (double)w[ax] <= hi[ax] - dm && lq >= lo[ax] + 2.0 * dm &&
+                 lq <= hi[ax] - 2.0 * dm;
+          }
+#endif
           if (ok) {  // samples k+1 .. kj lie inside the empty cube
             k = kj;
             zd = zj;
@@ -1176,6 +1239,7 @@ __device__ inline int fwd_step(const Geom& g, const DevVol& vd, const CamP& cam,
       kj = min(kj, last_k);
       if (kj > L.k) {
         const int zj = zstart + kj * zdelta;
+#if DMF_FWD_VERIFY_JUMPS
         float qc[3], q[3];
         project(cam, r, c, zj, qc);
         xform(m, qc[0], qc[1], qc[2], q);
@@ -1184,6 +1248,10 @@ __device__ inline int fwd_step(const Geom& g, const DevVol& vd, const CamP& cam,
           L.k = kj;
           L.zd = zj;
         }
+#else
+        L.k = kj;  // (as fwd_ray)
+        L.zd = zj;
+#endif
       }
     }
     L.zd += zdelta;
@@ -1225,17 +1293,26 @@ __device__ inline int fwd_step(const Geom& g, const DevVol& vd, const CamP& cam,
         int kj = min((int)floorf((zexit - (float)zstart) / (float)zdelta) - 1, last_k);
         if (kj > L.k + 1) {
           const int zj = zstart + kj * zdelta;
+          bool ok = true;
+#if DMF_FWD_VERIFY_JUMPS
           float qc[3], q[3];
           project(cam, r, c, zj, qc);
           xform(m, qc[0], qc[1], qc[2], q);
           ++samples;
-          bool ok = true;
 #pragma unroll
           for (int ax = 0; ax < 3; ++ax) {
             const double dm = margin(ax, (double)zj);
             ok = ok && (double)w[ax] >= lo[ax] + dm && (double)w[ax] <= hi[ax] - dm && (double)q[ax] >= lo[ax] + dm &&
                  (double)q[ax] <= hi[ax] - dm;
           }
+#else
+#pragma unroll
+          for (int ax = 0; ax < 3; ++ax) {  // (as fwd_ray)
+            const double dm = margin(ax, (double)zj), lq = (double)m[4 * ax + 3] + (double)zj * L.dir[ax];
+            ok = ok && (double)w[ax] >= lo[ax] + dm && (double)w[ax] <= hi[ax] - dm && lq >= lo[ax] + 2.0 * dm &&
+                 lq <= hi[ax] - 2.0 * dm;
+          }
+#endif
           if (ok) {
             L.k = kj;
             L.zd = zj;

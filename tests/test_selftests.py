@@ -5,6 +5,9 @@
   projection and reverse-march domains;
 * tools/binning_selftest.cpp — the marches' certified float binning (dmf_geom.hpp
   bin_axis_f) equals the reference getVoxel binning in double whenever it certifies;
+* tools/jump_selftest.cpp — the marches' empty-space jumps taken without evaluating the
+  landing sample (reverse: faces moved in by Geom::jmarg; forward: the line checked against the
+  cube shrunk by twice the rounding margin) land inside the cube, and every sample in between;
 * ASan + UBSan builds of both self-tests and of the CPU oracle
   (tools/oracle_sanitize.cpp drives every oracle entry point on a small scene): undefined
   behaviour or an out-of-bounds access in the checkers fails the CPU suite."""
@@ -49,6 +52,14 @@ def test_fast_division_selftest(tmp_path):
 
 
 @pytest.mark.timeout(300)
+def test_unchecked_jumps_selftest(tmp_path):
+    r = _build_and_run(os.path.join(ROOT, "tools", "jump_selftest.cpp"), str(tmp_path), ["400000", "7"],
+                       ["-I", os.path.join(ROOT, "depth-map-fusion-utils_amd", "csrc")])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "total 0 failures" in r.stdout
+
+
+@pytest.mark.timeout(300)
 def test_selftests_and_oracle_under_sanitizers(tmp_path):
     inc = ["-I", os.path.join(ROOT, "depth-map-fusion-utils_amd", "csrc")]
     r = _build_and_run(os.path.join(ROOT, "tools", "brick_selftest.cpp"), str(tmp_path), ["20000", "11"], inc, SAN)
@@ -57,6 +68,8 @@ def test_selftests_and_oracle_under_sanitizers(tmp_path):
     assert r.returncode == 0 and " 0 mismatches" in r.stdout, r.stdout + r.stderr
     r = _build_and_run(os.path.join(ROOT, "tools", "binning_selftest.cpp"), str(tmp_path), ["20011"], inc, SAN)
     assert r.returncode == 0 and " 0 mismatches" in r.stdout.splitlines()[-1], r.stdout + r.stderr
+    r = _build_and_run(os.path.join(ROOT, "tools", "jump_selftest.cpp"), str(tmp_path), ["20000", "5"], inc, SAN)
+    assert r.returncode == 0 and "total 0 failures" in r.stdout, r.stdout + r.stderr
     r = _build_and_run(os.path.join(ROOT, "tools", "oracle_sanitize.cpp"), str(tmp_path), [], ["-fopenmp"], SAN,
                        [os.path.join(ROOT, "oracle", "oracle.cpp")])
     assert r.returncode == 0 and "oracle sanitize ok" in r.stdout, r.stdout + r.stderr

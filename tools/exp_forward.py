@@ -73,4 +73,12 @@ for kf in KS:
     res[kf] = (kb.cpu().numpy().copy(), sb.cpu().numpy().copy())
 k0 = KS[0]
 out["outputs_equal"] = bool(all(np.array_equal(res[k0][0], r[0]) and np.array_equal(res[k0][1], r[1]) for r in res.values()))
+# the committed oracle digests of every pixel's (k, slot) (tests/golden/march_digests.json)
+try:
+    import hashlib
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "march_digests.json")))["config4_shard_N1"]
+    dg = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]  # noqa: E731
+    out["digest_match"] = bool(dg(res[k0][0]) == gold["forward_k_digest"] and dg(res[k0][1]) == gold["forward_slot_digest"])
+except (OSError, KeyError) as e:
+    out["digest_error"] = str(e)
 print(json.dumps(out), flush=True)
