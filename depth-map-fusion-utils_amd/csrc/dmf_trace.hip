@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void k_reverse(Geom g, DevVol vd, CamP cam, co
 // divergent code, so it is batched).
 struct RevLane {
   float cen[3], v[3], rv[3];
-  int cx, cy, cz;
+  uint32_t cob;         // occupancy bit of the centroid's cell (0xffffffff: outside the grid)
   int s;                // next sample index
   uint32_t known_full;  // last brick found occupied / not skippable
   int item;             // local item index, -1 = idle
@@ -290,9 +290,12 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   int a, b, c;
   if (!valid_points_f(g, p)) return 2;
   bin_point(g, p, a, b, c);
-  if (a == L.cx && b == L.cy && c == L.cz) { DMF_RS(2, 1); ++L.s; return 0; }
+  // (the reference tests the centroid's hash before validCoords; the centroid's cell is inside
+  // the grid, so testing validCoords first and then the cell by its occupancy bit, which is
+  // one-to-one on the grid, takes the same branches with one compare instead of three)
   if (!valid_coords(g, a, b, c)) return 2;
   const uint32_t ob = occ_bit(g, a, b, c);
+  if (ob == L.cob) { DMF_RS(2, 1); ++L.s; return 0; }
   if ((ob >> 5) != L.occi) { L.occi = ob >> 5; L.occw = vd.occ[L.occi]; }
   if ((L.occw >> (ob & 31)) & 1u) return 1;
   const int ba = a >> vd.bsh, bb = b >> vd.bsh, bc = c >> vd.bsh;
@@ -435,9 +438,10 @@ __device__ inline bool rev_wave(const Geom& g, const DevVol& vd, const CamP& cam
               L.cen[a] = cen[a];
               L.rv[a] = L.v[a] != 0.0f ? 1000.0f / L.v[a] : 0.0f;
             }
-            L.cx = bin_axis(g, 0, cen[0]);
-            L.cy = bin_axis(g, 1, cen[1]);
-            L.cz = bin_axis(g, 2, cen[2]);
+            {
+              const int cx = bin_axis(g, 0, cen[0]), cy = bin_axis(g, 1, cen[1]), cz = bin_axis(g, 2, cen[2]);
+              L.cob = valid_coords(g, cx, cy, cz) ? occ_bit(g, cx, cy, cz) : 0xffffffffu;
+            }
             L.s = 0;
             L.known_full = 0xffffffffu;
             L.occi = 0xffffffffu;
