@@ -859,8 +859,10 @@ static int run_reverse(dmf_volume* v, const dmf_camera* cam, const float* poses,
     constexpr int kSpItems = DMF_EXP_REV_ITEMS, kSpRefill = DMF_EXP_REV_REFILL, kSpBurst = DMF_EXP_REV_BURST;
 #else
     // (round 5, per-XCD queues: burst 32 5.24-5.25 ms vs 16 5.29-5.32, 24 5.25-5.26, 8 5.39-5.41;
-    // refill 4 / 12 / 16 at burst 16 within +-0.5 %: profiles/r05j/)
-    constexpr int kSpItems = 64, kSpRefill = 8, kSpBurst = 32;
+    // refill 4 / 12 / 16 at burst 16 within +-0.5 %: profiles/r05j/.  Round 6, after the
+    // unchecked jumps: burst 64 4.67-4.69 ms vs 32 4.71-4.72, 48 4.71-4.74, 96 4.68-4.70, 128 4.68;
+    // refill 4 / 16 at burst 32 +-0.2 %: profiles/r06ab/, r06ac/)
+    constexpr int kSpItems = 64, kSpRefill = 8, kSpBurst = 64;
 #endif
     const dim3 gridq((unsigned)((nelem + 4 * kRevItems - 1) / (4 * kRevItems)), (unsigned)P);
     const dim3 gridqs((unsigned)((nelem + 4 * kSpItems - 1) / (4 * kSpItems)), (unsigned)P);
