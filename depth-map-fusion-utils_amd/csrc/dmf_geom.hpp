@@ -43,7 +43,9 @@ struct Geom {
 inline void jump_margin_setup(Geom& g) {
   for (int a = 0; a < 3; ++a) {
     const double b = std::fmax(std::fabs(g.mn[a]), std::fabs(g.mx[a]));
-    g.jmarg[a] = (float)(32.0 * 0x1p-24 * b) + 1e-30f;
+    // (non-finite bounds: an infinite margin, so no jump is ever taken -- a NaN would drop the
+    // axis from the jump's fminf instead)
+    g.jmarg[a] = b < INFINITY ? (float)(32.0 * 0x1p-24 * b) + 1e-30f : INFINITY;
   }
 }
 
