@@ -23,10 +23,12 @@ namespace dmf {
 
 // Register budgets of the march kernels: DMF_EXP_REV_WAVES / DMF_EXP_FWD_WAVES = n keeps their
 // registers for n waves per SIMD (experiment builds override them)
-// k_reverse_x at 7 waves per SIMD (72 VGPRs, no spill; 76 / 6 waves before: 5.19 vs 5.21 ms,
-// 8 waves spill and lose: 5.84 ms)
+// k_reverse_x at 6 waves per SIMD (round 6: the next sample computed while a sample's loads are
+// in flight needs 4 more VGPRs; at 7 waves 2 spill: 4.49-4.51 ms at 6 waves vs 4.56 at 7 with
+// the spill and 4.54-4.56 without the precompute at 7; round 5: 7 waves, 72
+// VGPRs, 5.19 vs 5.21 ms at 6; 8 waves spilled and lost)
 #if !defined(DMF_EXP_REV_WAVES)
-#define DMF_EXP_REV_WAVES 7
+#define DMF_EXP_REV_WAVES 6
 #endif
 #define DMF_REV_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_REV_WAVES)))
 // The queue marches' empty-space jumps: 0 (default) = the target is computed from the cube's
@@ -42,6 +44,12 @@ namespace dmf {
 // profiles/r06z); 1 = the landing sample is evaluated and checked (experiment builds)
 #ifndef DMF_FWD_VERIFY_JUMPS
 #define DMF_FWD_VERIFY_JUMPS 0
+#endif
+// The reverse march computes sample s + 1 while sample s's occupancy and distance loads are in
+// flight (used when the step is a plain step; a jump or the centroid's cell recomputes): 1 (the
+// default, round 6); 0 = one sample computed per step (experiment builds)
+#ifndef DMF_EXP_REV_PRECOMP
+#define DMF_EXP_REV_PRECOMP 1
 #endif
 #if defined(DMF_EXP_FWD_WAVES)
 #define DMF_FWD_OCC __attribute__((amdgpu_waves_per_eu(DMF_EXP_FWD_WAVES)))
@@ -244,6 +252,10 @@ struct RevLane {
   int32_t slot;
   float tz;             // camera-frame z of the centroid (z-range test)
   uint32_t occi, occw;  // cached occupancy word
+#if DMF_EXP_REV_PRECOMP
+  float pn[3];          // sample pns, computed ahead
+  int pns;
+#endif
 };
 
 __device__ inline bool valid_points_f(const Geom& g, const float p[3]) {
@@ -278,14 +290,27 @@ constexpr int kRevStatN = 11;
 // cube of bricks of radius d - 1 around the current brick; every sample coordinate is
 // a monotone function of the step index, so if samples s and j both lie in that cube
 // (and inside the volume) so does every sample between them — none can hit an
-// occupied cell, the centroid's cell (occupied) or leave the volume.  j is estimated
-// from the cube faces and verified by evaluating sample j exactly.
+// occupied cell, the centroid's cell (occupied) or leave the volume.  j is computed from the
+// cube's faces moved in by Geom::jmarg, which puts sample j inside the cube without evaluating
+// it (DMF_REV_VERIFY_JUMPS = 0, the default), or estimated from the faces themselves and
+// verified by evaluating sample j exactly (= 1).
 __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int depth0, int max_steps,
                                int64_t& samples, unsigned long long* rst) {
   (void)rst;
   if (L.s >= max_steps) return 3;
   float p[3];
+#if DMF_EXP_REV_PRECOMP
+  // sample s was computed by the previous step while that step's loads were in flight
+  if (L.pns == L.s) {
+    p[0] = L.pn[0];
+    p[1] = L.pn[1];
+    p[2] = L.pn[2];
+  } else {
+    march_sample(L.cen, L.v, depth0 + L.s, p);
+  }
+#else
   march_sample(L.cen, L.v, depth0 + L.s, p);
+#endif
   ++samples;
   int a, b, c;
   if (!valid_points_f(g, p)) return 2;
@@ -303,6 +328,10 @@ __device__ inline int rev_step(const Geom& g, const DevVol& vd, RevLane& L, int 
   const uint32_t bl = ((uint32_t)ba * (uint32_t)vd.nb[1] + (uint32_t)bb) * (uint32_t)vd.nb[2] + (uint32_t)bc;
   const int dpre = vd.bdist[bl];
   if ((ob >> 5) != L.occi) { L.occi = ob >> 5; L.occw = vd.occ[L.occi]; }
+#if DMF_EXP_REV_PRECOMP
+  march_sample(L.cen, L.v, depth0 + L.s + 1, L.pn);  // the next sample, while the loads are in flight
+  L.pns = L.s + 1;
+#endif
   if ((L.occw >> (ob & 31)) & 1u) return 1;
   if (bl != L.known_full) {
     const int d = dpre;
@@ -449,6 +478,9 @@ __device__ inline bool rev_wave(const Geom& g, const DevVol& vd, const CamP& cam
             L.s = 0;
             L.known_full = 0xffffffffu;
             L.occi = 0xffffffffu;
+#if DMF_EXP_REV_PRECOMP
+            L.pns = -1;
+#endif
             L.item = it;
             L.slot = slot;
             L.tz = t[2];

@@ -50,4 +50,4 @@ def test_no_scratch_no_spills(src, tmp_path):
         assert b and all(v["vgpr_count"] <= 128 for v in b)  # pass B: 4 waves per SIMD
     if src == "dmf_trace.hip":
         r = [v for n, v in ks.items() if "k_reverse_x" in n]
-        assert r and all(v["vgpr_count"] <= 72 for v in r)   # reverseRayTraceFast: 7 waves per SIMD
+        assert r and all(v["vgpr_count"] <= 80 for v in r)   # reverseRayTraceFast: 6 waves per SIMD
